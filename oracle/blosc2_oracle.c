@@ -1,0 +1,764 @@
+/*
+ * blosc2_oracle.c -- clean-room CPU restatement of the c-blosc2 (3.3.3.dev) per-block
+ * filter -> BloscLZ pipeline and its chunk framing, used ONLY as the parity checker.
+ *
+ * TEST INFRASTRUCTURE.  The product (c-blosc2_amd/) never links, loads or calls this file.
+ * Pinned by the reference's own golden vectors (compat/ .cdata files) and by the reference library
+ * compiled from its own sources (oracle/_ref), see tests/test_oracle_*.py.
+ *
+ * Every function cites the reference file:line whose behaviour it restates.  The code is written
+ * index-based (no pointer walking) and the probe and the emitter of BloscLZ share one routine.
+ */
+#include "blosc2_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+enum {
+  HDR_MIN = 16, HDR_EXT = 32,                 /* include/blosc2.h:177-180 */
+  MIN_BUF = 32,                               /* BLOSC_MIN_BUFFERSIZE, include/blosc2.h:193 */
+  F_SHUF = 1, F_MEMCPY = 2, F_BITSHUF = 4, F_DELTA = 8, /* include/blosc2.h:273-277 */
+  FLT_NONE = 0, FLT_SHUFFLE = 1, FLT_BITSHUFFLE = 2, FLT_DELTA = 3, FLT_TRUNC = 4,
+  SPLIT_ALWAYS = 1, SPLIT_NEVER = 2, SPLIT_AUTO = 3, SPLIT_FWD = 4,
+  SPECIAL_ZERO = 1, SPECIAL_NAN = 2, SPECIAL_VALUE = 3, SPECIAL_UNINIT = 4,
+  ERR_DATA = -3, ERR_READ = -5, ERR_WRITE = -6, ERR_PARAM = -12, ERR_CODEC = -7,
+  ERR_RUNLEN = -33, ERR_FILTER = -8, ERR_HEADER = -39,
+};
+
+static inline uint32_t ld32(const uint8_t *p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+static inline void st32(uint8_t *p, int32_t v) {
+  uint32_t u = (uint32_t)v;
+  p[0] = (uint8_t)u; p[1] = (uint8_t)(u >> 8); p[2] = (uint8_t)(u >> 16); p[3] = (uint8_t)(u >> 24);
+}
+
+/* ------------------------------------------------------------------ shuffle / unshuffle ---- */
+/* blosc/shuffle.c:416-430 (param check) + blosc/shuffle-generic.h:34-55 (dst[j*n+i]=src[i*ts+j],
+ * tail bs%ts bytes copied verbatim). */
+int32_t or_shuffle(int32_t ts, int32_t nbytes, const uint8_t *src, uint8_t *dst) {
+  if (ts < 1 || ts > 256 || nbytes < 0) return ERR_PARAM;
+  int32_t n = nbytes / ts, tail = nbytes % ts;
+  for (int32_t plane = 0; plane < ts; plane++)
+    for (int32_t e = 0; e < n; e++) dst[(int64_t)plane * n + e] = src[(int64_t)e * ts + plane];
+  memcpy(dst + nbytes - tail, src + nbytes - tail, (size_t)tail);
+  return nbytes;
+}
+
+/* blosc/shuffle.c:435-449 + blosc/shuffle-generic.h:62-83 */
+int32_t or_unshuffle(int32_t ts, int32_t nbytes, const uint8_t *src, uint8_t *dst) {
+  if (ts < 1 || ts > 256 || nbytes < 0) return ERR_PARAM;
+  int32_t n = nbytes / ts, tail = nbytes % ts;
+  for (int32_t e = 0; e < n; e++)
+    for (int32_t plane = 0; plane < ts; plane++) dst[(int64_t)e * ts + plane] = src[(int64_t)plane * n + e];
+  memcpy(dst + nbytes - tail, src + nbytes - tail, (size_t)tail);
+  return nbytes;
+}
+
+/* ------------------------------------------------------------------------- bitshuffle ---- */
+/* blosc/shuffle.c:454-478 (m = (bs/ts) rounded down to a multiple of 8, tail copied) and
+ * blosc/bitshuffle-generic.c:147-167 (byte transpose, 8x8 bit transpose, bit-row transpose).
+ * Net layout: out row r = 8*b + k (b = byte within element, k = bit) is m/8 bytes long and bit
+ * (e % 8) of its byte (e / 8) is bit k of byte b of element e. */
+static void bit_rows_forward(int32_t ts, int32_t m, const uint8_t *src, uint8_t *dst) {
+  int32_t rowlen = m / 8;
+  for (int32_t b = 0; b < ts; b++)
+    for (int32_t k = 0; k < 8; k++) {
+      uint8_t *row = dst + (int64_t)(8 * b + k) * rowlen;
+      for (int32_t g = 0; g < rowlen; g++) {
+        uint8_t v = 0;
+        for (int32_t r = 0; r < 8; r++) v |= (uint8_t)(((src[(int64_t)(8 * g + r) * ts + b] >> k) & 1u) << r);
+        row[g] = v;
+      }
+    }
+}
+
+static void bit_rows_inverse(int32_t ts, int32_t m, const uint8_t *src, uint8_t *dst) {
+  int32_t rowlen = m / 8;
+  memset(dst, 0, (size_t)m * (size_t)ts);
+  for (int32_t b = 0; b < ts; b++)
+    for (int32_t k = 0; k < 8; k++) {
+      const uint8_t *row = src + (int64_t)(8 * b + k) * rowlen;
+      for (int32_t g = 0; g < rowlen; g++)
+        for (int32_t r = 0; r < 8; r++)
+          dst[(int64_t)(8 * g + r) * ts + b] |= (uint8_t)(((row[g] >> r) & 1u) << k);
+    }
+}
+
+int32_t or_bitshuffle(int32_t ts, int32_t nbytes, const uint8_t *src, uint8_t *dst) {
+  if (ts < 1 || ts > 256 || nbytes < 0) return ERR_PARAM;
+  int32_t m = (nbytes / ts) & ~7;
+  bit_rows_forward(ts, m, src, dst);
+  int32_t done = m * ts;
+  memcpy(dst + done, src + done, (size_t)(nbytes - done));
+  return nbytes;
+}
+
+/* blosc/shuffle.c:482-521: a chunk whose version byte is 2 (Blosc1) is un-bitshuffled only when
+ * its element count is a multiple of 8 (else copied); newer formats work like or_bitshuffle. */
+int32_t or_bitunshuffle(int32_t ts, int32_t nbytes, const uint8_t *src, uint8_t *dst,
+                        uint8_t format_version) {
+  if (ts < 1 || ts > 256 || nbytes < 0) return ERR_PARAM;
+  int32_t n = nbytes / ts;
+  if (format_version == 2) {
+    if (n % 8 == 0) bit_rows_inverse(ts, n, src, dst);
+    else memcpy(dst, src, (size_t)nbytes);
+    return nbytes;
+  }
+  int32_t m = n & ~7;
+  bit_rows_inverse(ts, m, src, dst);
+  int32_t done = m * ts;
+  memcpy(dst + done, src + done, (size_t)(nbytes - done));
+  return nbytes;
+}
+
+/* ------------------------------------------------------------------------------ delta ---- */
+/* blosc/delta.c:18-92.  Word width w = ts for ts in {1,2,4,8}, else 8 if ts%8==0, else 1.
+ * Block 0 (offset 0): d[0]=ref[0], d[i]=s[i]^ref[i-1]; other blocks: d[i]=s[i]^ref[i].
+ * Only nbytes/w words are written. */
+static int delta_width(int32_t ts) {
+  if (ts == 1 || ts == 2 || ts == 4 || ts == 8) return ts;
+  return (ts % 8 == 0) ? 8 : 1;
+}
+
+static inline uint64_t ldw(const uint8_t *p, int w) {
+  uint64_t v = 0;
+  memcpy(&v, p, (size_t)w);
+  return v;
+}
+static inline void stw(uint8_t *p, uint64_t v, int w) { memcpy(p, &v, (size_t)w); }
+
+void or_delta_encode(const uint8_t *dref, int32_t offset, int32_t nbytes, int32_t ts,
+                     const uint8_t *src, uint8_t *dst) {
+  int w = delta_width(ts);
+  int32_t nw = nbytes / w;
+  if (nw <= 0) return;
+  if (offset == 0) {
+    /* Walk backwards so that dst may alias src (the reference works out of place). */
+    uint64_t first = ldw(dref, w);
+    for (int32_t i = nw - 1; i >= 1; i--) stw(dst + (int64_t)i * w, ldw(src + (int64_t)i * w, w) ^ ldw(dref + (int64_t)(i - 1) * w, w), w);
+    stw(dst, first, w);
+  } else {
+    for (int32_t i = 0; i < nw; i++) stw(dst + (int64_t)i * w, ldw(src + (int64_t)i * w, w) ^ ldw(dref + (int64_t)i * w, w), w);
+  }
+}
+
+/* blosc/delta.c:96-161: block 0 is an in-place running XOR (prefix scan over words, with
+ * dref == dst); other blocks XOR with the decoded block 0. */
+void or_delta_decode(const uint8_t *dref, int32_t offset, int32_t nbytes, int32_t ts, uint8_t *dst) {
+  int w = delta_width(ts);
+  int32_t nw = nbytes / w;
+  if (offset == 0) {
+    for (int32_t i = 1; i < nw; i++) stw(dst + (int64_t)i * w, ldw(dst + (int64_t)i * w, w) ^ ldw(dref + (int64_t)(i - 1) * w, w), w);
+  } else {
+    for (int32_t i = 0; i < nw; i++) stw(dst + (int64_t)i * w, ldw(dst + (int64_t)i * w, w) ^ ldw(dref + (int64_t)i * w, w), w);
+  }
+}
+
+/* ------------------------------------------------------------------------- trunc-prec ---- */
+/* blosc/trunc-prec.c:23-86 */
+int or_trunc_prec(int8_t prec_bits, int32_t ts, int32_t nbytes, const uint8_t *src, uint8_t *dst) {
+  int mant;
+  if (ts == 4) mant = 23;
+  else if (ts == 8) mant = 52;
+  else return -1;
+  int p = prec_bits;
+  if ((p < 0 ? -p : p) > mant) return -1;
+  int zeroed = p >= 0 ? mant - p : -p;
+  if (zeroed >= mant) return -1;
+  uint64_t mask = ~((1ULL << zeroed) - 1ULL);
+  int32_t n = nbytes / ts;
+  for (int32_t i = 0; i < n; i++) stw(dst + (int64_t)i * ts, ldw(src + (int64_t)i * ts, ts) & mask, ts);
+  return 0;
+}
+
+/* ---------------------------------------------------------------------------- BloscLZ ---- */
+enum { LZ_MAX_COPY = 32, LZ_NEAR = 8191, LZ_FAR = 65535 + 8191 - 1, LZ_SHIFT = 4, LZ_MINLEN = 4 };
+
+static inline uint32_t lz_hash(uint32_t seq, int hashlog) { return (seq * 2654435761U) >> (32 - hashlog); }
+
+/* End of the common prefix of in[p..] and in[r..] (p > r), as returned by the reference's
+ * get_match / get_match_16 / get_run (blosc/blosclz.c:119-190): one past the first mismatching
+ * byte, never beyond `bound`.  All three variants give this same answer (distance-1 runs too). */
+static inline int32_t lz_match_end(const uint8_t *in, int32_t p, int32_t r, int32_t bound) {
+  while (p < bound) {
+    int same = in[p] == in[r];
+    p++; r++;
+    if (!same) return p;
+  }
+  return bound;
+}
+
+/* One greedy parse over in[0..length) (blosc/blosclz.c:422-619 main loop, or the probe
+ * get_cratio at 320-419 when `probe` is set).  The probe only counts output bytes, uses
+ * `limit` = min(length, 2^hashlog), stops at the main loop (no tail) and has neither the
+ * far-distance short-match rule nor the clevel-9 double rehash.
+ * Returns: probe -> writes *ratio; emit -> compressed size or 0 if it does not fit. */
+static int lz_parse(const uint8_t *in, int32_t length, int hashlog, int clevel, int probe,
+                    uint8_t *out, int32_t maxout, double *ratio, uint32_t *htab) {
+  int32_t limit = length;
+  if (probe) {
+    int32_t hashlen = 1 << hashlog;
+    limit = length > hashlen ? hashlen : length;
+  }
+  const int32_t bound = limit - 1, loop_end = limit - 12;
+  memset(htab, 0, sizeof(uint32_t) << hashlog);
+
+  int32_t o = 0;          /* output cursor (emit) or output byte count (probe) */
+  int32_t lit = 4;        /* literals in the open literal run */
+  int32_t pos = 4;
+  if (probe) {
+    o = 5;
+  } else {
+    out[0] = LZ_MAX_COPY - 1;
+    for (int i = 0; i < 4; i++) out[1 + i] = in[i];
+    o = 5;
+  }
+  if (probe) pos = 0;     /* get_cratio starts hashing at its first byte */
+  if (probe) lit = 4;
+
+  while (pos < loop_end) {
+    const int32_t anchor = pos;
+    const uint32_t h = lz_hash(ld32(in + anchor), hashlog);
+    const int32_t ref = (int32_t)htab[h];
+    uint32_t dist = (uint32_t)(anchor - ref);
+    htab[h] = (uint32_t)anchor;
+
+    int literal = (dist == 0 || dist >= LZ_FAR) || ld32(in + ref) != ld32(in + anchor);
+    int32_t len = 0;
+    if (!literal) {
+      dist--;  /* biased distance */
+      int32_t end = lz_match_end(in, anchor + 4, ref + 4, bound);
+      len = end - LZ_SHIFT - anchor;
+      if (len < LZ_MINLEN) literal = 1;
+      else if (!probe && len <= 5 && dist >= LZ_NEAR) literal = 1;
+    }
+    if (literal) {
+      /* LITERAL / LITERAL2 macros, blosc/blosclz.c:248-268 */
+      if (probe) {
+        o++;
+      } else {
+        if (o + 2 > maxout) return 0;
+        out[o++] = in[anchor];
+      }
+      pos = anchor + 1;
+      if (++lit == LZ_MAX_COPY) {
+        lit = 0;
+        if (probe) o++; else out[o++] = LZ_MAX_COPY - 1;
+      }
+      continue;
+    }
+    /* close the literal run (blosc/blosclz.c:546-554 / 387-391) */
+    if (probe) {
+      if (!lit) o--;
+    } else {
+      if (lit) out[o - lit - 1] = (uint8_t)(lit - 1);
+      else o--;
+    }
+    lit = 0;
+    pos = anchor + len;
+    const uint32_t ulen = (uint32_t)len;
+    if (probe) {
+      if (ulen >= 7) o += (int32_t)((ulen - 7) / 255) + 1;
+      o += dist < LZ_NEAR ? 2 : 4;
+    } else if (dist < LZ_NEAR) {
+      /* MATCH_SHORT / MATCH_LONG, blosc/blosclz.c:270-290 */
+      if (ulen < 7) {
+        if (o + 2 > maxout) return 0;
+        out[o++] = (uint8_t)((ulen << 5) + (dist >> 8));
+        out[o++] = (uint8_t)(dist & 255);
+      } else {
+        if (o + 1 > maxout) return 0;
+        out[o++] = (uint8_t)((7u << 5) + (dist >> 8));
+        uint32_t rem = ulen - 7;
+        for (; rem >= 255; rem -= 255) {
+          if (o + 1 > maxout) return 0;
+          out[o++] = 255;
+        }
+        if (o + 2 > maxout) return 0;
+        out[o++] = (uint8_t)rem;
+        out[o++] = (uint8_t)(dist & 255);
+      }
+    } else {
+      /* MATCH_SHORT_FAR / MATCH_LONG_FAR, blosc/blosclz.c:292-316 */
+      uint32_t fd = dist - LZ_NEAR;
+      if (ulen < 7) {
+        if (o + 4 > maxout) return 0;
+        out[o++] = (uint8_t)((ulen << 5) + 31);
+        out[o++] = 255;
+        out[o++] = (uint8_t)(fd >> 8);
+        out[o++] = (uint8_t)(fd & 255);
+      } else {
+        if (o + 1 > maxout) return 0;
+        out[o++] = (7u << 5) + 31;
+        uint32_t rem = ulen - 7;
+        for (; rem >= 255; rem -= 255) {
+          if (o + 1 > maxout) return 0;
+          out[o++] = 255;
+        }
+        if (o + 4 > maxout) return 0;
+        out[o++] = (uint8_t)rem;
+        out[o++] = 255;
+        out[o++] = (uint8_t)(fd >> 8);
+        out[o++] = (uint8_t)(fd & 255);
+      }
+    }
+    /* rehash at the match boundary (blosc/blosclz.c:573-586 / 408-412) */
+    const uint32_t seq = ld32(in + pos);
+    htab[lz_hash(seq, hashlog)] = (uint32_t)pos;
+    if (!probe && clevel == 9) htab[lz_hash(seq >> 8, hashlog)] = (uint32_t)(pos + 1);
+    pos += 2;
+    if (probe) {
+      o++;
+    } else {
+      if (o + 1 > maxout) return 0;
+      out[o++] = LZ_MAX_COPY - 1;
+    }
+  }
+  if (probe) {
+    *ratio = (double)pos / (double)o;
+    return 0;
+  }
+  /* tail literals (blosc/blosclz.c:595-610) */
+  for (; pos <= bound; pos++) {
+    if (o + 2 > maxout) return 0;
+    out[o++] = in[pos];
+    if (++lit == LZ_MAX_COPY) {
+      lit = 0;
+      out[o++] = LZ_MAX_COPY - 1;
+    }
+  }
+  if (lit) out[o - lit - 1] = (uint8_t)(lit - 1);
+  else o--;
+  out[0] |= 1u << 5;  /* blosc/blosclz.c:613 */
+  return o;
+}
+
+/* blosc/blosclz.c:422-468: entropy probe over the last `maxlen` bytes, then the real pass. */
+int or_blosclz_compress(int clevel, const uint8_t *in, int length, uint8_t *out, int maxout) {
+  static const uint8_t hashlogs[10] = {0, 12, 13, 14, 14, 14, 14, 14, 14, 14};
+  static const double min_ratio[10] = {0, 2, 1.5, 1.2, 1.2, 1.2, 1.2, 1.15, 1.1, 1.0};
+  if (clevel < 1 || clevel > 9) return 0;
+  int hashlog = hashlogs[clevel];
+  uint32_t *htab = (uint32_t *)malloc(sizeof(uint32_t) << 14);
+  if (!htab) return -1;
+  int32_t maxlen = length;
+  if (clevel < 2) maxlen /= 8;
+  else if (clevel < 4) maxlen /= 4;
+  else if (clevel < 7) maxlen /= 2;
+  double ratio = 0.0;
+  lz_parse(in + (length - maxlen), maxlen, hashlog, clevel, 1, NULL, 0, &ratio, htab);
+  int r = 0;
+  if (!(ratio < min_ratio[clevel]) && length >= 16 && maxout >= 66)
+    r = lz_parse(in, length, hashlog, clevel, 0, out, maxout, NULL, htab);
+  free(htab);
+  return r;
+}
+
+/* blosc/blosclz.c:685-795.  Returns the decoded size, 0 on any bound violation. */
+int or_blosclz_decompress(const uint8_t *in, int length, uint8_t *out, int maxout) {
+  if (length == 0) return 0;
+  int32_t ip = 0, op = 0;
+  uint32_t ctrl = in[ip++] & 31u;
+  for (;;) {
+    if (ctrl >= 32) {
+      int32_t len = (int32_t)(ctrl >> 5) - 1;
+      int32_t ofs = (int32_t)(ctrl & 31u) << 8;
+      uint8_t code;
+      if (len == 6) {
+        do {
+          if (ip + 1 >= length) return 0;
+          code = in[ip++];
+          len += code;
+        } while (code == 255);
+      } else if (ip + 1 >= length) {
+        return 0;
+      }
+      code = in[ip++];
+      len += 3;
+      int64_t ref = (int64_t)op - ofs - code;
+      if (code == 255 && ofs == (31 << 8)) {
+        if (ip + 1 >= length) return 0;
+        int32_t far = (int32_t)in[ip] << 8 | in[ip + 1];
+        ip += 2;
+        ref = (int64_t)op - far - LZ_NEAR;
+      }
+      if (op + len > maxout) return 0;
+      if (ref - 1 < 0) return 0;
+      /* a match that ends the input is dropped, not copied (blosc/blosclz.c:742) */
+      if (ip >= length) break;
+      ctrl = in[ip++];
+      ref--;
+      for (int32_t i = 0; i < len; i++) out[op + i] = out[ref + i];  /* forward, overlap-safe */
+      op += len;
+    } else {
+      int32_t run = (int32_t)ctrl + 1;
+      if (op + run > maxout) return 0;
+      if (ip + run > length) return 0;
+      memcpy(out + op, in + ip, (size_t)run);
+      op += run;
+      ip += run;
+      if (ip >= length) break;
+      ctrl = in[ip++];
+    }
+  }
+  return op;
+}
+
+/* ----------------------------------------------------------------------- chunk framing ---- */
+/* blosc/stune.c:186-215 */
+int or_split_block(const or_cparams *cp, int32_t typesize, int32_t blocksize) {
+  if (cp->splitmode == SPLIT_ALWAYS) return 1;
+  if (cp->splitmode == SPLIT_NEVER) return 0;
+  int shuffle_on = 0;
+  for (int i = 0; i < 6; i++) shuffle_on |= cp->filters[i] == FLT_SHUFFLE;
+  return cp->compcode == 0 && shuffle_on && typesize <= 16 && (blocksize / typesize) >= MIN_BUF;
+}
+
+static int32_t eff_typesize(const or_cparams *cp) { return cp->typesize > 255 ? 1 : cp->typesize; }
+
+/* blosc/stune.c:47-165 (BloscLZ is not an HCR codec) */
+int32_t or_compute_blocksize(const or_cparams *cp, int32_t nbytes) {
+  int32_t ts = cp->typesize;   /* stune runs before the >255 typesize cap (blosc2.c:2468, 2530) */
+  int32_t clevel = cp->clevel;
+  if (nbytes < ts) return 1;
+  int split = or_split_block(cp, ts, nbytes);
+  int32_t bs = nbytes;
+  if (cp->blocksize) {
+    bs = cp->blocksize;
+  } else {
+    if (nbytes >= 32 * 1024) {
+      static const int32_t scale[10] = {8 * 1024, 16 * 1024, 32 * 1024, 64 * 1024, 128 * 1024,
+                                        128 * 1024, 256 * 1024, 256 * 1024, 256 * 1024, 256 * 1024};
+      bs = scale[clevel];
+    }
+    if (clevel > 0 && split) {
+      static const int32_t per_ts[10] = {0, 32, 32, 32, 64, 64, 64, 128, 256, 512};
+      bs = per_ts[clevel] * 1024 * ts;
+      if (bs > 4 * 1024 * 1024) bs = 4 * 1024 * 1024;
+      if (bs < 32 * 1024) bs = 32 * 1024;
+    }
+  }
+  if (bs > nbytes) bs = nbytes;
+  if (bs > ts) bs = bs / ts * ts;
+  return bs;
+}
+
+/* blosc/blosc2.c:1184-1206: the whole stream is a single repeated byte. */
+static int whole_run(const uint8_t *p, int32_t n) {
+  for (int32_t i = 1; i < n; i++)
+    if (p[i] != p[0]) return 0;
+  return 1;
+}
+
+/* pipeline_forward, blosc/blosc2.c:1055-1180 (no prefilter, built-in filters only).
+ * The reference rotates three buffers with _cycle_buffers (blosc2.c:1048): the k-th active
+ * filter (0-based) writes into tmp, tmp2, then the caller's own source block, cyclically.  So a
+ * 3rd (or 6th) active filter overwrites the input chunk in place, and DELTA on later blocks then
+ * XORs against that rewritten block 0.  `chunk` is therefore a private, writable copy here.
+ * Returns the buffer holding the filtered block, NULL on filter error. */
+static const uint8_t *pipe_forward(const or_cparams *cp, int32_t ts, uint8_t *chunk,
+                                   int32_t offset, int32_t bsize, uint8_t *t1, uint8_t *t2) {
+  uint8_t *cur = chunk + offset;
+  uint8_t *ring[3] = {t1, t2, chunk + offset};
+  int k = 0;
+  for (int i = 0; i < 6; i++) {
+    uint8_t f = cp->filters[i];
+    if (f == FLT_NONE) continue;
+    uint8_t *dst = ring[k % 3];
+    uint8_t meta = cp->filters_meta[i];
+    switch (f) {
+      case FLT_SHUFFLE: or_shuffle(meta ? meta : ts, bsize, cur, dst); break;
+      case FLT_BITSHUFFLE: or_bitshuffle(ts, bsize, cur, dst); break;
+      case FLT_DELTA: or_delta_encode(offset == 0 ? cur : chunk, offset, bsize, ts, cur, dst); break;
+      case FLT_TRUNC:
+        if (or_trunc_prec((int8_t)meta, ts, bsize, cur, dst) < 0) return NULL;
+        break;
+      default: return NULL;
+    }
+    cur = dst;
+    k++;
+  }
+  return cur;
+}
+
+typedef struct {
+  uint8_t flags, typesize;
+  int32_t nbytes, blocksize, cbytes, nblocks, leftover, overhead;
+  uint8_t filters[6], filters_meta[6];
+  uint8_t version, bflags;
+} or_hdr;
+
+static void flags_to_filter_list(uint8_t flags, uint8_t *filters) {
+  memset(filters, 0, 6);
+  if (flags & F_SHUF) filters[5] = FLT_SHUFFLE;
+  if (flags & F_BITSHUF) filters[5] = FLT_BITSHUFFLE;
+  if (flags & F_DELTA) filters[4] = FLT_DELTA;
+}
+
+/* blosc_c for one block, serial mode: blosc/blosc2.c:1210-1469.  Returns the bytes written
+ * (>0), 0 when the chunk does not fit, <0 on error. */
+static int32_t compress_block(const or_cparams *cp, int32_t ts, int split, uint8_t *chunk,
+                              int32_t offset, int32_t bsize, int leftover, uint8_t *dest,
+                              int32_t ntbytes, int32_t destsize, uint8_t *t1, uint8_t *t2) {
+  const uint8_t *blk = pipe_forward(cp, ts, chunk, offset, bsize, t1, t2);
+  if (!blk) return ERR_FILTER;
+  int32_t nstreams = (split && !leftover) ? ts : 1;
+  int32_t neblock = bsize / nstreams;
+  int32_t written = 0;
+  for (int32_t j = 0; j < nstreams; j++) {
+    const uint8_t *s = blk + (int64_t)j * neblock;
+    uint8_t *csize_at = dest + written;
+    written += 4; ntbytes += 4;
+    if (whole_run(s, neblock)) {
+      if (ntbytes > destsize) return 0;
+      st32(csize_at, -(int32_t)s[0]);
+      if (s[0]) {
+        ntbytes++;
+        if (ntbytes > destsize) return 0;
+        dest[written++] = 0x1;
+      }
+      continue;
+    }
+    int32_t maxout = neblock;
+    if (ntbytes + maxout > destsize) {
+      maxout = destsize - ntbytes;
+      if (maxout <= 0) return 0;
+    }
+    int32_t cb = or_blosclz_compress(cp->clevel, s, neblock, dest + written, maxout);
+    if (cb < 0) return ERR_DATA;
+    if (cb == 0) cb = neblock;
+    if (cb == neblock) {
+      if (ntbytes + neblock > destsize) return 0;
+      memcpy(dest + written, s, (size_t)neblock);
+    }
+    st32(csize_at, cb);
+    written += cb; ntbytes += cb;
+  }
+  return written;
+}
+
+/* blosc2_compress_ctx with nthreads == 1 (blosc/blosc2.c:3121-3148, header 2911-3001,
+ * body 3004-3107, per-block loop serial_blosc 2161-2228). */
+int or_compress_chunk(const or_cparams *cp, const void *src_, int32_t srcsize, void *dest_,
+                      int32_t destsize) {
+  const uint8_t *src = (const uint8_t *)src_;
+  uint8_t *dest = (uint8_t *)dest_;
+  if (cp->compcode != 0) return ERR_CODEC;
+  if (srcsize > 0x7fffffff - 32) return -9;
+  if (destsize < 32) return -9;
+  if (cp->clevel < 0 || cp->clevel > 9) return -10;
+  int32_t ts = eff_typesize(cp);
+  int32_t bs = or_compute_blocksize(cp, srcsize);
+  int32_t nblocks = bs ? srcsize / bs : 0, leftover = bs ? srcsize % bs : 0;
+  if (leftover) nblocks++;
+
+  uint8_t flags = F_SHUF | F_BITSHUF;   /* extended-header marker */
+  int memcpyed = cp->clevel == 0 || srcsize < MIN_BUF;
+  int32_t out = HDR_EXT + (memcpyed ? 0 : 4 * nblocks);
+  if (!memcpyed && out > destsize) { memcpyed = 1; out = HDR_EXT; }
+  int split = 0;
+  if (memcpyed) {
+    flags |= F_MEMCPY;
+  } else {
+    for (int i = 0; i < 6; i++) {
+      if (cp->filters[i] == FLT_SHUFFLE) flags |= F_SHUF;
+      if (cp->filters[i] == FLT_BITSHUFFLE) flags |= F_BITSHUF;
+      if (cp->filters[i] == FLT_DELTA) flags |= F_DELTA;
+    }
+    split = or_split_block(cp, ts, bs);
+    flags |= (uint8_t)((!split) << 4);       /* dont_split, bit 4; compformat 0 in bits 5-7 */
+  }
+  /* header: blosc2_initialize_header_from_context, blosc/blosc2.c:1000-1046 */
+  memset(dest, 0, HDR_EXT);
+  dest[0] = 5; dest[1] = 1; dest[2] = flags; dest[3] = (uint8_t)ts;
+  st32(dest + 4, srcsize);
+  /* the header carries the context's incoming blocksize when it is set (header_blocksize,
+   * blosc/blosc2.c:2414 and 1001-1005), else the computed one; clamped to nbytes */
+  int32_t hb = cp->blocksize > 0 ? cp->blocksize : bs;
+  st32(dest + 8, (srcsize > 0 && hb > srcsize) ? srcsize : hb);
+  for (int i = 0; i < 6; i++) { dest[16 + i] = cp->filters[i]; dest[24 + i] = cp->filters_meta[i]; }
+  dest[22] = (uint8_t)cp->compcode;
+
+  int32_t ntbytes = 0;
+  /* private copy of the input: the reference may rewrite it (see pipe_forward), and a later
+   * memcpy fallback copies whatever the input holds by then (blosc/blosc2.c:2185-2189) */
+  uint8_t *work = (uint8_t *)malloc((size_t)srcsize + 64);
+  if (!work) return -1;
+  memcpy(work, src, (size_t)srcsize);
+  if (!memcpyed) {
+    uint8_t *t1 = (uint8_t *)malloc((size_t)bs + 64), *t2 = (uint8_t *)malloc((size_t)bs + 64);
+    if (!t1 || !t2) { free(t1); free(t2); free(work); return -1; }
+    ntbytes = out;
+    for (int32_t j = 0; j < nblocks; j++) {
+      st32(dest + HDR_EXT + 4 * j, ntbytes);
+      int lo = (j == nblocks - 1) && leftover;
+      int32_t bsize = lo ? leftover : bs;
+      int32_t cb = compress_block(cp, ts, split, work, j * bs, bsize, lo, dest + ntbytes, ntbytes,
+                                  destsize, t1, t2);
+      if (cb < 0) { free(t1); free(t2); free(work); return cb; }
+      if (cb == 0) { ntbytes = 0; break; }
+      ntbytes += cb;
+    }
+    free(t1); free(t2);
+    if (ntbytes == 0) memcpyed = 2;   /* fall back to a plain copy (blosc/blosc2.c:3017-3051) */
+  }
+  if (memcpyed) {
+    if (srcsize + HDR_EXT > destsize) {
+      ntbytes = 0;
+    } else {
+      memcpy(dest + HDR_EXT, work, (size_t)srcsize);
+      ntbytes = HDR_EXT + srcsize;
+      dest[2] = flags | F_MEMCPY;
+    }
+  } else {
+    /* all streams zero runs -> SPECIAL_ZERO chunk (blosc/blosc2.c:3054-3063) */
+    int32_t nstreams = nblocks;
+    if (split) nstreams = leftover ? (nblocks - 1) * ts + 1 : nblocks * ts;
+    if (ntbytes == HDR_EXT + 4 * nblocks + 4 * nstreams) {
+      dest[31] |= SPECIAL_ZERO << 4;
+      ntbytes = HDR_EXT;
+    }
+  }
+  free(work);
+  st32(dest + 12, ntbytes);
+  return ntbytes;
+}
+
+/* read_chunk_header + initialize_context_decompression (blosc/blosc2.c:738-852, 2688-2909),
+ * restricted to non-VL, non-lazy, dictionary-free chunks. */
+static int parse_header(const uint8_t *src, int32_t srcsize, or_hdr *h) {
+  memset(h, 0, sizeof *h);
+  if (srcsize < HDR_MIN) return ERR_READ;
+  h->version = src[0]; h->flags = src[2]; h->typesize = src[3];
+  h->nbytes = (int32_t)ld32(src + 4); h->blocksize = (int32_t)ld32(src + 8); h->cbytes = (int32_t)ld32(src + 12);
+  if (h->cbytes < HDR_MIN || h->blocksize <= 0 || h->blocksize > 536866816 || h->typesize == 0) return ERR_HEADER;
+  if ((h->flags & F_SHUF) && (h->flags & F_BITSHUF)) {
+    if (h->cbytes < HDR_EXT || srcsize < HDR_EXT) return ERR_HEADER;
+    memcpy(h->filters, src + 16, 6);
+    memcpy(h->filters_meta, src + 24, 6);
+    h->bflags = src[31];
+    if (src[30] != 0) return ERR_HEADER;      /* VL blocks: not part of this oracle */
+    if (h->version == 3) { h->filters[5] = 0; h->filters_meta[5] = 0; }
+    h->overhead = HDR_EXT;
+  } else {
+    flags_to_filter_list(h->flags, h->filters);
+    if ((h->flags & F_SHUF) && h->typesize <= 1) h->filters[5] = 0;  /* get_filter_flags */
+    h->overhead = HDR_MIN;
+  }
+  if (h->nbytes > 0 && h->blocksize > h->nbytes) h->blocksize = h->nbytes;
+  h->nblocks = h->nbytes / h->blocksize;
+  h->leftover = h->nbytes % h->blocksize;
+  if (h->leftover) h->nblocks++;
+  if (h->cbytes > srcsize) return ERR_HEADER;
+  return 0;
+}
+
+/* pipeline_backward, blosc/blosc2.c:1473-1609 (serial mode, built-in filters). `cur` holds the
+ * decoded streams of block nblock; the result lands in out + offset. */
+static int pipe_backward(const or_hdr *h, uint8_t *out, int32_t offset, int32_t bsize,
+                         uint8_t *cur, uint8_t *t1, uint8_t *t2) {
+  int32_t ts = h->typesize;
+  uint8_t *bufs[2] = {t1, t2};
+  int nb = 0;
+  for (int i = 5; i >= 0; i--) {
+    uint8_t f = h->filters[i];
+    if (f == FLT_NONE || f == FLT_TRUNC) continue;
+    uint8_t *dst = bufs[nb];
+    uint8_t meta = h->filters_meta[i];
+    switch (f) {
+      case FLT_SHUFFLE: or_unshuffle(meta ? meta : ts, bsize, cur, dst); break;
+      case FLT_BITSHUFFLE: or_bitunshuffle(ts, bsize, cur, dst, h->version); break;
+      case FLT_DELTA:
+        memcpy(dst, cur, (size_t)bsize);
+        if (offset == 0) {
+          /* block 0 decodes in place inside the output chunk */
+          memcpy(out, dst, (size_t)bsize);
+          or_delta_decode(out, 0, bsize, ts, out);
+          memcpy(dst, out, (size_t)bsize);
+        } else {
+          or_delta_decode(out, offset, bsize, ts, dst);
+        }
+        break;
+      default: return ERR_FILTER;
+    }
+    cur = dst;
+    nb ^= 1;
+  }
+  memcpy(out + offset, cur, (size_t)bsize);
+  return 0;
+}
+
+int or_decompress_chunk(const void *src_, int32_t srcsize, void *dest_, int32_t destsize) {
+  const uint8_t *src = (const uint8_t *)src_;
+  uint8_t *dest = (uint8_t *)dest_;
+  or_hdr h;
+  int rc = parse_header(src, srcsize, &h);
+  if (rc < 0) return rc;
+  if (h.nbytes > destsize) return ERR_WRITE;
+  int special = (h.overhead == HDR_EXT) ? (h.bflags >> 4) & 7 : 0;
+  int memcpyed = (h.flags & F_MEMCPY) != 0;
+  if (memcpyed && h.cbytes != h.nbytes + h.overhead) return ERR_DATA;
+  if (h.nbytes == 0 && h.cbytes == h.overhead && !special) return 0;
+  if (special) {
+    if (special == SPECIAL_ZERO) memset(dest, 0, (size_t)h.nbytes);
+    else if (special == SPECIAL_UNINIT) { /* nothing */ }
+    else return ERR_DATA;   /* NaN / value specials are outside this oracle */
+    return h.nbytes;
+  }
+  if (memcpyed) {
+    memcpy(dest, src + h.overhead, (size_t)h.nbytes);
+    return h.nbytes;
+  }
+  if ((h.flags >> 5) != 0) return ERR_CODEC;   /* only BloscLZ */
+  int32_t bstarts_end = h.overhead + 4 * h.nblocks;
+  if (srcsize < bstarts_end) return ERR_READ;
+  int dont_split = (h.flags >> 4) & 1;
+  int32_t bs = h.blocksize;
+  uint8_t *t0 = (uint8_t *)malloc((size_t)bs + 64), *t1 = (uint8_t *)malloc((size_t)bs + 64),
+          *t2 = (uint8_t *)malloc((size_t)bs + 64);
+  if (!t0 || !t1 || !t2) { free(t0); free(t1); free(t2); return -1; }
+  int32_t total = 0;
+  rc = 0;
+  for (int32_t j = 0; j < h.nblocks && rc == 0; j++) {
+    int lo = (j == h.nblocks - 1) && h.leftover;
+    int32_t bsize = lo ? h.leftover : bs;
+    int32_t off = (int32_t)ld32(src + h.overhead + 4 * j);
+    if (off <= 0 || off >= srcsize) { rc = ERR_DATA; break; }
+    int32_t avail = srcsize - off;
+    const uint8_t *p = src + off;
+    int32_t nstreams = (!dont_split && !lo) ? h.typesize : 1;
+    int32_t neblock = bsize / nstreams;
+    if (neblock == 0) { rc = ERR_WRITE; break; }
+    int has_filters = 0;
+    for (int i = 0; i < 6; i++) has_filters |= h.filters[i] != FLT_NONE && h.filters[i] != FLT_TRUNC;
+    uint8_t *stage = has_filters ? t0 : dest + (int64_t)j * bs;
+    for (int32_t s = 0; s < nstreams; s++) {
+      if (avail < 4) { rc = ERR_READ; break; }
+      int32_t cb = (int32_t)ld32(p);
+      p += 4; avail -= 4;
+      uint8_t *d = stage + (int64_t)s * neblock;
+      if (cb == 0) {
+        memset(d, 0, (size_t)neblock);
+      } else if (cb < 0) {
+        if (avail < 1) { rc = ERR_READ; break; }
+        uint8_t token = *p++; avail--;
+        if (!(token & 1) || cb < -255) { rc = ERR_RUNLEN; break; }
+        memset(d, (uint8_t)(-cb), (size_t)neblock);
+      } else {
+        if (avail < cb) { rc = ERR_READ; break; }
+        if (cb == neblock) {
+          memcpy(d, p, (size_t)neblock);
+        } else if (or_blosclz_decompress(p, cb, d, neblock) != neblock) {
+          rc = ERR_DATA; break;
+        }
+        p += cb; avail -= cb;
+      }
+    }
+    if (rc) break;
+    if (has_filters) rc = pipe_backward(&h, dest, j * bs, bsize, t0, t1, t2);
+    total += bsize;
+  }
+  free(t0); free(t1); free(t2);
+  return rc < 0 ? rc : total;
+}

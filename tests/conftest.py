@@ -1,0 +1,28 @@
+import os
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (runs the HIP path)")
+    config.addinivalue_line("markers", "slow: long-running parity sweep")
+
+
+def pytest_collection_modifyitems(config, items):
+    # GPU tests need the device; without one they are skipped rather than failed so that the
+    # CPU tier (-m "not gpu") and a plain local run both stay green.
+    try:
+        import torch  # noqa: F401
+        have_gpu = torch.cuda.is_available()
+    except Exception:
+        have_gpu = False
+    if have_gpu:
+        return
+    skip = pytest.mark.skip(reason="no GPU in this container")
+    for item in items:
+        if "gpu" in item.keywords:
+            item.add_marker(skip)
