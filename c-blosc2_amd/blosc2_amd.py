@@ -1,0 +1,168 @@
+"""Python host-side mirror of the drop-in library (c-blosc2_amd/lib/libblosc2.so).
+
+This mirrors the reference's C entry points one-to-one over ctypes (same names, same argument
+meaning, same integer return codes) so tests and bench read like the reference's own C tests.
+It never falls back to anything: if the HIP library is missing, importing this module raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libblosc2.so")
+
+MAX_FILTERS = 6
+NOFILTER, SHUFFLE, BITSHUFFLE, DELTA, TRUNC_PREC = 0, 1, 2, 3, 4
+ALWAYS_SPLIT, NEVER_SPLIT, AUTO_SPLIT, FORWARD_COMPAT_SPLIT = 1, 2, 3, 4
+BLOSC2_MAX_OVERHEAD = 32
+
+
+class CParams(C.Structure):
+    """blosc2_cparams (include/blosc2.h; reference include/blosc2.h:1173-1211)."""
+    _fields_ = [
+        ("compcode", C.c_uint8), ("compcode_meta", C.c_uint8), ("clevel", C.c_uint8),
+        ("use_dict", C.c_int), ("typesize", C.c_int32), ("nthreads", C.c_int16),
+        ("blocksize", C.c_int32), ("splitmode", C.c_int32), ("schunk", C.c_void_p),
+        ("filters", C.c_uint8 * MAX_FILTERS), ("filters_meta", C.c_uint8 * MAX_FILTERS),
+        ("prefilter", C.c_void_p), ("preparams", C.c_void_p), ("tuner_params", C.c_void_p),
+        ("tuner_id", C.c_int), ("instr_codec", C.c_bool), ("codec_params", C.c_void_p),
+        ("filter_params", C.c_void_p * MAX_FILTERS),
+    ]
+
+
+class DParams(C.Structure):
+    """blosc2_dparams (reference include/blosc2.h:1232-1243)."""
+    _fields_ = [("nthreads", C.c_int16), ("schunk", C.c_void_p), ("postfilter", C.c_void_p),
+                ("postparams", C.c_void_p), ("typesize", C.c_int32)]
+
+
+def cparams(clevel=5, typesize=8, filters=(0, 0, 0, 0, 0, SHUFFLE), filters_meta=(0,) * 6,
+            blocksize=0, splitmode=FORWARD_COMPAT_SPLIT, compcode=0, nthreads=1):
+    p = CParams()
+    p.compcode, p.clevel, p.typesize, p.nthreads = compcode, clevel, typesize, nthreads
+    p.blocksize, p.splitmode = blocksize, splitmode
+    for i in range(MAX_FILTERS):
+        p.filters[i] = filters[i]
+        p.filters_meta[i] = filters_meta[i] & 0xFF
+    return p
+
+
+def dparams(nthreads=1):
+    d = DParams()
+    d.nthreads, d.typesize = nthreads, 8
+    return d
+
+
+def _bind(lib):
+    vp, i32, i16, i64 = C.c_void_p, C.c_int32, C.c_int16, C.c_int64
+    sig = {
+        "blosc2_init": ([], None), "blosc2_destroy": ([], None),
+        "blosc2_create_cctx": ([CParams], vp), "blosc2_create_dctx": ([DParams], vp),
+        "blosc2_free_ctx": ([vp], None),
+        "blosc2_compress_ctx": ([vp, vp, i32, vp, i32], C.c_int),
+        "blosc2_decompress_ctx": ([vp, vp, i32, vp, i32], C.c_int),
+        "blosc2_getitem_ctx": ([vp, vp, i32, C.c_int, C.c_int, vp, i32], C.c_int),
+        "blosc2_set_maskout": ([vp, vp, C.c_int], C.c_int),
+        "blosc2_shuffle": ([i32, i32, vp, vp], i32), "blosc2_unshuffle": ([i32, i32, vp, vp], i32),
+        "blosc2_bitshuffle": ([i32, i32, vp, vp], i32), "blosc2_bitunshuffle": ([i32, i32, vp, vp], i32),
+        "blosc2_set_nthreads": ([i16], i16),
+        "blosc1_set_compressor": ([C.c_char_p], C.c_int),
+        "blosc1_compress": ([C.c_int, C.c_int, C.c_size_t, C.c_size_t, vp, vp, C.c_size_t], C.c_int),
+        "blosc1_decompress": ([vp, vp, C.c_size_t], C.c_int),
+        "blosc2_compress": ([C.c_int, C.c_int, i32, vp, i32, vp, i32], C.c_int),
+        "blosc2_decompress": ([vp, i32, vp, i32], C.c_int),
+        "blosc2_cbuffer_sizes": ([vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)], C.c_int),
+        "blosc2_get_version_string": ([], C.c_char_p),
+        "b2h_compress_batch": ([C.POINTER(CParams), vp, i32, i32, i64, vp, i64, i32, vp, vp], C.c_int),
+        "b2h_decompress_batch": ([vp, i64, vp, i32, vp, i64, i32, vp, vp], C.c_int),
+        "b2h_shuffle": ([i32, i32, vp, vp, C.c_int, vp], i32),
+        "b2h_bitshuffle": ([i32, i32, vp, vp, C.c_int, vp], i32),
+        "b2h_enable_timing": ([C.c_int], None),
+        "b2h_last_times": ([C.POINTER(C.c_float)], None),
+        "b2h_last_error": ([], C.c_char_p),
+        "b2h_device_count": ([], C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(lib, name)
+        f.argtypes, f.restype = args, res
+    return lib
+
+
+_lib = None
+
+
+def lib():
+    """Load the HIP library (raises if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: build it with `make -C c-blosc2_amd` "
+                               "(the MI355X engine has no CPU fallback)")
+        _lib = _bind(C.CDLL(LIB_PATH))
+        _lib.blosc2_init()
+    return _lib
+
+
+def _p(a):
+    return C.c_void_p(a.ctypes.data)
+
+
+# ------------------------------------------------------------ host-buffer convenience ----
+def compress_ctx(ctx, src: np.ndarray, destsize=None):
+    raw = np.ascontiguousarray(src).view(np.uint8).reshape(-1)
+    if destsize is None:
+        destsize = raw.nbytes + BLOSC2_MAX_OVERHEAD
+    out = np.zeros(destsize + 16, np.uint8)
+    n = lib().blosc2_compress_ctx(ctx, _p(raw), raw.nbytes, _p(out), destsize)
+    return out[:n] if n > 0 else n
+
+
+def decompress_ctx(ctx, chunk: np.ndarray, nbytes: int):
+    out = np.zeros(max(nbytes, 1), np.uint8)
+    n = lib().blosc2_decompress_ctx(ctx, _p(chunk), chunk.nbytes, _p(out), nbytes)
+    return out[:nbytes] if n >= 0 else n
+
+
+def compress(src: np.ndarray, **kw):
+    """One chunk through a fresh compression context (blosc2_create_cctx + compress_ctx)."""
+    L = lib()
+    ctx = L.blosc2_create_cctx(cparams(**kw))
+    try:
+        return compress_ctx(ctx, src)
+    finally:
+        L.blosc2_free_ctx(ctx)
+
+
+def decompress(chunk: np.ndarray, nbytes: int):
+    L = lib()
+    ctx = L.blosc2_create_dctx(dparams())
+    try:
+        return decompress_ctx(ctx, chunk, nbytes)
+    finally:
+        L.blosc2_free_ctx(ctx)
+
+
+# ------------------------------------------------------------- device batch interface ----
+def compress_batch(cp: CParams, d_src: int, chunk_nbytes: int, nchunks: int, src_stride: int,
+                   d_dst: int, dst_stride: int, dst_capacity: int, d_cbytes: int, stream: int = 0):
+    rc = lib().b2h_compress_batch(C.byref(cp), C.c_void_p(d_src), chunk_nbytes, nchunks, src_stride,
+                                  C.c_void_p(d_dst), dst_stride, dst_capacity, C.c_void_p(d_cbytes),
+                                  C.c_void_p(stream))
+    if rc < 0:
+        raise RuntimeError(f"b2h_compress_batch: {rc} {lib().b2h_last_error()}")
+
+
+def decompress_batch(d_src: int, src_stride: int, d_cbytes: int, nchunks: int, d_dst: int,
+                     dst_stride: int, dst_capacity: int, d_status: int, stream: int = 0):
+    rc = lib().b2h_decompress_batch(C.c_void_p(d_src), src_stride, C.c_void_p(d_cbytes), nchunks,
+                                    C.c_void_p(d_dst), dst_stride, dst_capacity, C.c_void_p(d_status),
+                                    C.c_void_p(stream))
+    if rc < 0:
+        raise RuntimeError(f"b2h_decompress_batch: {rc} {lib().b2h_last_error()}")
+
+
+def last_times():
+    buf = (C.c_float * 5)()
+    lib().b2h_last_times(buf)
+    return dict(zip(("filter_ms", "encode_ms", "finalize_ms", "decode_ms", "unfilter_ms"), list(buf)))

@@ -1,0 +1,68 @@
+// b2h_engine.h -- host-side interface of the MI355X batch engine (C++, internal).
+// The public C-ABI wrappers live in blosc2_api.cpp (include/blosc2.h) and b2h_api.cpp
+// (include/b2h.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace b2h {
+
+// Uniform compression batch: every chunk has `nbytes` bytes and the same cparams, which is what
+// a super-chunk's shared cctx produces (blosc/schunk.c:1459-1477).
+struct CompressPlan {
+  int32_t nbytes;          // bytes per chunk
+  int32_t typesize;        // effective typesize (the reference caps > 255 to 1)
+  int32_t clevel;
+  int32_t blocksize;       // computed (stune)
+  int32_t header_blocksize;
+  int32_t destsize;        // per-chunk output capacity (serial-mode bound checks use it)
+  bool split;              // streams per block = typesize
+  bool memcpyed;           // chunk-level memcpy decided before compressing (clevel 0, tiny, no room)
+  int32_t overhead;        // 32 (extended header, blosc2_compress_ctx) or 16 (BLOSC_BLOSC1_COMPAT)
+  uint8_t filters[6];
+  uint8_t filters_meta[6];
+  uint8_t header[32];      // header template (cbytes patched per chunk)
+};
+
+// Fill the plan from cparams-level values the way blosc2_compress_ctx does (initialize_context_
+// compression + write_compression_header, blosc/blosc2.c:2385-2533, 2911-3001).  Returns < 0 on
+// invalid parameters.  `ctx_blocksize` is the blocksize the context currently holds (0 = auto).
+int make_compress_plan(CompressPlan* p, int32_t nbytes, int32_t destsize, int clevel, int32_t typesize,
+                       int32_t ctx_blocksize, int32_t splitmode, const uint8_t* filters,
+                       const uint8_t* filters_meta, int32_t* computed_blocksize, bool extended = true);
+
+// Compress `nchunks` chunks: chunk i is d_src + i*src_stride, its output goes to
+// d_dst + i*dst_stride (capacity plan.destsize), its cbytes (>0, 0 = does not fit) to d_cbytes[i].
+// Asynchronous on `stream`.
+int compress_batch(const CompressPlan& plan, const uint8_t* d_src, int64_t src_stride, int32_t nchunks,
+                   uint8_t* d_dst, int64_t dst_stride, int32_t* d_cbytes, hipStream_t stream);
+
+// Decompress `n` arbitrary chunks (device pointer arrays).  d_status[i] = nbytes or BLOSC2_ERROR_*.
+// `dst_bound` is an upper bound of the sum of decompressed sizes (sizes the staging scratch).
+// d_maskout (optional, only with n == 1): one byte per block, nonzero = skip (blosc2_set_maskout).
+// Synchronises `stream` once (to size the stream table).
+int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint8_t* const* d_dst,
+                     const int32_t* d_dstsize, int32_t n, int64_t dst_bound, int32_t* d_status,
+                     const uint8_t* d_maskout, hipStream_t stream);
+
+// Strided convenience form: chunk i at d_src + i*src_stride with cbytes d_cbytes[i], output at
+// d_dst + i*dst_stride with capacity dst_cap.
+int decompress_batch_strided(const uint8_t* d_src, int64_t src_stride, const int32_t* d_cbytes, int32_t n,
+                             uint8_t* d_dst, int64_t dst_stride, int32_t dst_cap, int32_t* d_status,
+                             hipStream_t stream);
+
+// Raw filters on device buffers (blosc2_shuffle & co. use these on staged copies).
+int shuffle_dev(int32_t typesize, int32_t nbytes, const uint8_t* d_src, uint8_t* d_dst, bool inverse, hipStream_t s);
+int bitshuffle_dev(int32_t typesize, int32_t nbytes, const uint8_t* d_src, uint8_t* d_dst, bool inverse,
+                   uint8_t format_version, hipStream_t s);
+
+// Kernel timing hook for bench.py (HIP events around the dominant kernels of the last batch).
+struct KernelTimes { float filter_ms, encode_ms, finalize_ms, decode_ms, unfilter_ms; };
+void enable_timing(bool on);
+KernelTimes last_times();
+
+// Device bookkeeping
+int device_count();
+const char* last_error();
+
+}  // namespace b2h

@@ -1,0 +1,1028 @@
+// b2h_engine.hip -- MI355X (gfx950) batch engine for the Blosc2 chunk pipeline.
+//
+// Compress (one uniform batch of chunks, all device-resident):
+//   [k_copy_work]      only when >= 3 filters are active: the reference rewrites its input in
+//                      place (blosc/blosc2.c:1048, 1173-1176), so we work on a private copy W
+//   k_ffilter x K      forward filters, one launch per active filter, workgroup per block
+//                      (block 0 of every chunk first when DELTA must see a rewritten block 0)
+//   k_encode           one wave per stream: run test, entropy probe, exact BloscLZ parse
+//   k_finalize         one lane per chunk: serial-layout bookkeeping of blosc_c/serial_blosc
+//                      (csize words, bstarts, destsize checks via `peak`, memcpy fallback,
+//                      SPECIAL_ZERO), header
+//   k_scatter          payloads to their final offsets (workgroup per stream)
+//   k_memcpy_chunks    memcpyed chunks
+// Decompress (any chunks, device pointer arrays):
+//   k_dplan_chunks -> k_dscan -> (one sync for totals) -> k_dplan_blocks -> k_decode ->
+//   k_dfilter x K (block 0 first when DELTA is present) ; k_dspecial for memcpyed/special chunks
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "b2h_engine.h"
+#include "b2h_filters.h"
+#include "b2h_format.h"
+#include "b2h_lz.h"
+
+namespace b2h {
+
+// error codes (include/blosc2.h:453-492)
+enum {
+  E_FAILURE = -1, E_DATA = -3, E_MEMORY = -4, E_READ = -5, E_WRITE = -6, E_CODEC = -7, E_VERSION = -10,
+  E_HEADER = -11, E_PARAM = -12, E_RUNLEN = -17, E_FILTER = -18, E_MAXBUF = -35,
+};
+
+static thread_local char g_err[256];
+const char* last_error() { return g_err; }
+
+#define HIPCHK(x)                                                                              \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess) {                                                                    \
+      snprintf(g_err, sizeof g_err, "%s: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+      return E_FAILURE;                                                                        \
+    }                                                                                          \
+  } while (0)
+
+// ------------------------------------------------------------------------------ workspace ----
+// Grow-only per-device scratch.  Never freed while the process runs; buffers carry 256 B of
+// slack because the LZ kernels read a few bytes past a stream's end (ldu32).
+struct Scratch {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t n) {
+    n += 256;
+    if (n <= cap) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, n) != hipSuccess) { snprintf(g_err, sizeof g_err, "hipMalloc(%zu) failed", n); return E_MEMORY; }
+    cap = n;
+    return 0;
+  }
+  template <typename T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct Workspace {
+  Scratch t1, t2, work, sbuf, res, place, mode;                // compress
+  Scratch dchunks, dstreams, dblocks, dtotals, stage, stage2, ptrs;  // decompress
+  std::mutex mu;
+};
+
+static Workspace* ws_for_current_device() {
+  static std::mutex m;
+  static std::vector<Workspace*> all;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  std::lock_guard<std::mutex> g(m);
+  if ((int)all.size() <= dev) all.resize(dev + 1, nullptr);
+  if (!all[dev]) all[dev] = new Workspace();
+  return all[dev];
+}
+
+int device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+// ------------------------------------------------------------------------------- timing -----
+static bool g_timing = false;
+static KernelTimes g_times{};
+void enable_timing(bool on) { g_timing = on; }
+KernelTimes last_times() { return g_times; }
+
+struct EvPair {
+  hipEvent_t a = nullptr, b = nullptr;
+  void start(hipStream_t s) {
+    if (!g_timing) return;
+    if (!a) { (void)hipEventCreate(&a); (void)hipEventCreate(&b); }
+    (void)hipEventRecord(a, s);
+  }
+  void stop(hipStream_t s) { if (g_timing) (void)hipEventRecord(b, s); }
+  float ms() {
+    if (!g_timing || !a) return 0.f;
+    (void)hipEventSynchronize(b);
+    float t = 0.f;
+    (void)hipEventElapsedTime(&t, a, b);
+    return t;
+  }
+};
+static EvPair ev_filter, ev_encode, ev_final, ev_decode, ev_unfilter;
+
+// ================================================================ compression: geometry ====
+struct CGeom {
+  int32_t nbytes, bs, nblocks, leftover, spb, nsc, neblock, ts, destsize, clevel, overhead;
+  int64_t src_stride, wstride, dst_stride;
+};
+
+__device__ __forceinline__ void stream_locate(const CGeom& g, int32_t l, int32_t* off, int32_t* len, int32_t* blk) {
+  const int32_t full = g.nblocks - (g.leftover ? 1 : 0);
+  if (l < full * g.spb) {
+    const int32_t b = l / g.spb, j = l - b * g.spb;
+    *blk = b;
+    *off = b * g.bs + j * g.neblock;
+    *len = g.neblock;
+  } else {
+    *blk = g.nblocks - 1;
+    *off = (g.nblocks - 1) * g.bs;
+    *len = g.leftover;
+  }
+}
+
+__global__ void k_copy_work(const uint8_t* __restrict__ src, int64_t src_stride, uint8_t* __restrict__ dst,
+                            int64_t dst_stride, int32_t nbytes) {
+  const int32_t c = blockIdx.y;
+  const uint8_t* s = src + (int64_t)c * src_stride;
+  uint8_t* d = dst + (int64_t)c * dst_stride;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nbytes; i += (int64_t)gridDim.x * blockDim.x) d[i] = s[i];
+}
+
+// Forward filter stage: grid (blocks_per_launch, nchunks).  pass: 0 all blocks, 1 block 0, 2 blocks >= 1.
+__global__ __launch_bounds__(kBlockThreads) void k_ffilter(CGeom g, int pass, uint8_t filter, uint8_t meta,
+                                                           const uint8_t* __restrict__ in, int64_t in_stride,
+                                                           uint8_t* __restrict__ out, int64_t out_stride,
+                                                           const uint8_t* __restrict__ dref, int64_t dref_stride,
+                                                           int zeroed) {
+  const int32_t c = blockIdx.y;
+  const int32_t b = pass == 2 ? (int32_t)blockIdx.x + 1 : (int32_t)blockIdx.x;
+  if (b >= g.nblocks) return;
+  const int32_t off = b * g.bs;
+  const int32_t bsize = (b == g.nblocks - 1 && g.leftover) ? g.leftover : g.bs;
+  const uint8_t* s = in + (int64_t)c * in_stride + off;
+  uint8_t* d = out + (int64_t)c * out_stride + off;
+  switch (filter) {
+    case kShuffle: block_shuffle(s, d, bsize, meta ? meta : g.ts); break;
+    case kBitshuffle: block_bitshuffle(s, d, bsize, g.ts); break;
+    case kDelta: block_delta_encode(s, dref + (int64_t)c * dref_stride, d, bsize, g.ts, b == 0); break;
+    case kTruncPrec: block_trunc(s, d, bsize, g.ts, zeroed); break;
+    default: break;
+  }
+}
+
+// One wave per stream.  Dynamic LDS: hash table (POS << hashlog) + tag buckets.
+template <typename POS>
+__global__ __launch_bounds__(64) void k_encode(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
+                                               StreamResult* __restrict__ res, int32_t nstreams_total) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int32_t s = blockIdx.x;
+  if (s >= nstreams_total) return;
+  const int32_t c = s / g.nsc, l = s - c * g.nsc;
+  int32_t off, len, blk;
+  stream_locate(g, l, &off, &len, &blk);
+  const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
+  volatile POS* htab = reinterpret_cast<volatile POS*>(smem);
+  volatile uint8_t* tag = smem + (sizeof(POS) << hashlog);
+  const uint8_t* in = filt + (int64_t)c * g.wstride + off;
+  uint8_t* out = sbuf + (int64_t)c * g.wstride + off;
+  StreamResult r = encode_stream<POS>(in, len, g.clevel, out, htab, tag, g.overhead == kHdrExt);
+  if (threadIdx.x == 0) res[s] = r;
+}
+
+struct Place {
+  int32_t off;    // payload offset inside the chunk output (csize word sits at off - 4)
+  int32_t csize;  // csize word
+};
+
+// Serial reference bookkeeping per chunk (blosc/blosc2.c:1277-1466, 2161-2228, 3004-3107).
+// mode: 0 compressed, 1 memcpy fallback, 2 special zero, 3 does not fit.
+__global__ void k_finalize(CGeom g, const StreamResult* __restrict__ res, Place* __restrict__ place,
+                           int32_t* __restrict__ mode, uint8_t* __restrict__ dst, int32_t* __restrict__ cbytes,
+                           int32_t nchunks, const uint8_t* __restrict__ header_template) {
+  const int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nchunks) return;
+  uint8_t* d = dst + (int64_t)c * g.dst_stride;
+  const StreamResult* r = res + (int64_t)c * g.nsc;
+  Place* pl = place + (int64_t)c * g.nsc;
+  const int32_t ovh = g.overhead;
+  int32_t ntbytes = ovh + 4 * g.nblocks;
+  const int32_t destsize = g.destsize;
+  bool ok = true, all_zero = true;
+  int32_t l = 0;
+  for (int32_t b = 0; b < g.nblocks && ok; b++) {
+    const bool lo = (b == g.nblocks - 1) && g.leftover;
+    const int32_t ns = lo ? 1 : g.spb;
+    const int32_t nl = lo ? g.leftover : g.neblock;
+    int32_t bstart = ntbytes;
+    uint8_t* bs = d + ovh + 4 * b;
+    bs[0] = (uint8_t)bstart; bs[1] = (uint8_t)(bstart >> 8); bs[2] = (uint8_t)(bstart >> 16); bs[3] = (uint8_t)(bstart >> 24);
+    for (int32_t j = 0; j < ns; j++, l++) {
+      const StreamResult sr = r[l];
+      ntbytes += 4;
+      if (sr.kind == kStreamZeroRun || sr.kind == kStreamByteRun) {
+        if (ntbytes > destsize) { ok = false; break; }
+        pl[l].off = ntbytes;
+        pl[l].csize = -sr.size;
+        if (sr.size) {
+          all_zero = false;
+          ntbytes += 1;
+          if (ntbytes > destsize) { ok = false; break; }
+        }
+        continue;
+      }
+      all_zero = false;
+      int32_t maxout = nl;
+      if (ntbytes + maxout > destsize) {
+        maxout = destsize - ntbytes;
+        if (maxout <= 0) { ok = false; break; }
+      }
+      int32_t cb = (sr.kind == kStreamLz && maxout >= 66 && sr.peak <= maxout) ? sr.size : 0;
+      if (cb == 0) cb = nl;
+      if (cb == nl && ntbytes + nl > destsize) { ok = false; break; }
+      pl[l].off = ntbytes;
+      pl[l].csize = cb;   // == nl means raw copy
+      ntbytes += cb;
+    }
+  }
+  // header (template already holds flags/typesize/nbytes/blocksize/filters)
+  for (int i = 0; i < ovh; i++) d[i] = header_template[i];
+  int32_t m, cb;
+  if (ok) {
+    const int32_t nstreams = g.nsc;
+    if (all_zero && ntbytes == ovh + 4 * g.nblocks + 4 * nstreams) {
+      m = 2;
+      cb = ovh;
+      d[31] |= (uint8_t)(kSpecialZero << 4);
+    } else {
+      m = 0;
+      cb = ntbytes;
+    }
+  } else if (g.nbytes + ovh <= destsize) {
+    m = 1;
+    cb = g.nbytes + ovh;
+    d[2] |= kFlagMemcpy;
+  } else {
+    m = 3;
+    cb = 0;
+  }
+  d[12] = (uint8_t)cb; d[13] = (uint8_t)(cb >> 8); d[14] = (uint8_t)(cb >> 16); d[15] = (uint8_t)(cb >> 24);
+  mode[c] = m;
+  cbytes[c] = cb;
+}
+
+// Workgroup copy of n bytes to an arbitrarily aligned destination: aligned u32 stores, sources
+// read with ldu32 (unaligned ok, slack guaranteed by the scratch layout).
+__device__ void wg_copy(uint8_t* __restrict__ d, const uint8_t* __restrict__ s, int32_t n) {
+  const int32_t head = (int32_t)((4 - (reinterpret_cast<uintptr_t>(d) & 3)) & 3);
+  const int32_t h = min(head, n);
+  if ((int32_t)threadIdx.x < h) d[threadIdx.x] = s[threadIdx.x];
+  const int32_t body = (n - h) / 4;
+  uint32_t* d4 = reinterpret_cast<uint32_t*>(d + h);
+  const uint8_t* s4 = s + h;
+  if ((reinterpret_cast<uintptr_t>(s4) & 3) == 0) {
+    const uint32_t* a = reinterpret_cast<const uint32_t*>(s4);
+    for (int32_t i = threadIdx.x; i < body; i += blockDim.x) d4[i] = a[i];
+  } else {
+    for (int32_t i = threadIdx.x; i < body; i += blockDim.x) d4[i] = ldu32(s4 + 4 * i);
+  }
+  for (int32_t i = h + body * 4 + threadIdx.x; i < n; i += blockDim.x) d[i] = s[i];
+}
+
+__global__ __launch_bounds__(kBlockThreads) void k_scatter(CGeom g, const Place* __restrict__ place,
+                                                           const int32_t* __restrict__ mode,
+                                                           const StreamResult* __restrict__ res,
+                                                           const uint8_t* __restrict__ filt,
+                                                           const uint8_t* __restrict__ sbuf, uint8_t* __restrict__ dst,
+                                                           int32_t nstreams_total) {
+  const int32_t s = blockIdx.x;
+  if (s >= nstreams_total) return;
+  const int32_t c = s / g.nsc, l = s - c * g.nsc;
+  if (mode[c] != 0) return;
+  int32_t off, len, blk;
+  stream_locate(g, l, &off, &len, &blk);
+  const Place pl = place[s];
+  uint8_t* d = dst + (int64_t)c * g.dst_stride;
+  if (threadIdx.x == 0) {
+    const uint32_t w = (uint32_t)pl.csize;
+    uint8_t* q = d + pl.off - 4;
+    q[0] = (uint8_t)w; q[1] = (uint8_t)(w >> 8); q[2] = (uint8_t)(w >> 16); q[3] = (uint8_t)(w >> 24);
+    if (pl.csize < 0) d[pl.off] = 0x1;   // run-length token
+  }
+  if (pl.csize <= 0) return;
+  const uint8_t* src = (pl.csize == len) ? filt + (int64_t)c * g.wstride + off : sbuf + (int64_t)c * g.wstride + off;
+  wg_copy(d + pl.off, src, pl.csize);
+}
+
+// memcpyed chunks: header + raw bytes.  `only_mode1`: fallback chunks only (mode[] == 1).
+__global__ void k_memcpy_chunks(const uint8_t* __restrict__ src, int64_t src_stride, uint8_t* __restrict__ dst,
+                                int64_t dst_stride, int32_t nbytes, const int32_t* __restrict__ mode,
+                                const uint8_t* __restrict__ header_template, int32_t* __restrict__ cbytes,
+                                int32_t overhead, int32_t destsize) {
+  const int32_t c = blockIdx.y;
+  if (mode && mode[c] != 1) return;
+  const uint8_t* s = src + (int64_t)c * src_stride;
+  uint8_t* d = dst + (int64_t)c * dst_stride;
+  const bool fits = nbytes + overhead <= destsize;
+  if (!mode && blockIdx.x == 0 && (int32_t)threadIdx.x < overhead) {
+    // memcpyed from the start: header written here; cbytes 0 when it cannot fit
+    // (blosc/blosc2.c:3038-3041)
+    uint8_t v = header_template[threadIdx.x];
+    const int32_t cb = fits ? nbytes + overhead : 0;
+    if (threadIdx.x >= 12 && threadIdx.x < 16) v = (uint8_t)(cb >> (8 * (threadIdx.x - 12)));
+    d[threadIdx.x] = v;
+    if (threadIdx.x == 0) cbytes[c] = cb;
+  }
+  if (!fits) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nbytes; i += (int64_t)gridDim.x * blockDim.x)
+    d[overhead + i] = s[i];
+}
+
+// ============================================================ compression: host driver ====
+static int32_t split_block(int32_t splitmode, int compcode, const uint8_t* filters, int32_t ts, int32_t bs) {
+  // blosc/stune.c:186-215
+  if (splitmode == 1) return 1;
+  if (splitmode == 2) return 0;
+  bool shuffle = false;
+  for (int i = 0; i < kMaxFilters; i++) shuffle |= filters[i] == kShuffle;
+  return (compcode == 0 || compcode == 1) && shuffle && ts <= kMaxStreams && (bs / ts) >= kMinBuffer;
+}
+
+int make_compress_plan(CompressPlan* p, int32_t nbytes, int32_t destsize, int clevel, int32_t typesize,
+                       int32_t ctx_blocksize, int32_t splitmode, const uint8_t* filters,
+                       const uint8_t* filters_meta, int32_t* computed_blocksize, bool extended) {
+  memset(p, 0, sizeof *p);
+  p->overhead = extended ? kHdrExt : kHdrMin;
+  if (nbytes > 0x7fffffff - kHdrExt) return E_MAXBUF;
+  if (destsize < kHdrExt) return E_MAXBUF;
+  if (clevel < 0 || clevel > 9) return -8;   // BLOSC2_ERROR_CODEC_PARAM
+  // stune (blosc/stune.c:47-165) with the incoming typesize, before the >255 cap
+  int32_t bs;
+  if (nbytes < typesize) {
+    bs = 1;
+  } else {
+    const int32_t splitmode_nb = split_block(splitmode, 0, filters, typesize, nbytes);
+    bs = nbytes;
+    if (ctx_blocksize) {
+      bs = ctx_blocksize;
+    } else {
+      if (nbytes >= 32 * 1024) {
+        static const int32_t scale[10] = {8 << 10, 16 << 10, 32 << 10, 64 << 10, 128 << 10,
+                                          128 << 10, 256 << 10, 256 << 10, 256 << 10, 256 << 10};
+        bs = scale[clevel];
+      }
+      if (clevel > 0 && splitmode_nb) {
+        static const int32_t per_ts[10] = {0, 32, 32, 32, 64, 64, 64, 128, 256, 512};
+        bs = per_ts[clevel] * 1024 * typesize;
+        if (bs > 4 * 1024 * 1024) bs = 4 * 1024 * 1024;
+        if (bs < 32 * 1024) bs = 32 * 1024;
+      }
+    }
+    if (bs > nbytes) bs = nbytes;
+    if (bs > typesize) bs = bs / typesize * typesize;
+  }
+  *computed_blocksize = bs;
+  const int32_t ts = typesize > 255 ? 1 : typesize;
+  p->nbytes = nbytes;
+  p->typesize = ts;
+  p->clevel = clevel;
+  p->blocksize = bs;
+  p->destsize = destsize;
+  memcpy(p->filters, filters, 6);
+  memcpy(p->filters_meta, filters_meta, 6);
+  const int32_t nblocks = bs ? nbytes / bs + (nbytes % bs ? 1 : 0) : 0;
+  // write_compression_header (blosc/blosc2.c:2911-3001)
+  uint8_t flags = extended ? (kFlagShuffle | kFlagBitshuffle) : 0;
+  bool memcpyed = clevel == 0 || nbytes < kMinBuffer;
+  if (!memcpyed && p->overhead + 4 * nblocks > destsize) memcpyed = true;
+  if (memcpyed) {
+    flags |= kFlagMemcpy;
+  } else {
+    for (int i = 0; i < kMaxFilters; i++) {
+      if (filters[i] == kShuffle) flags |= kFlagShuffle;
+      if (filters[i] == kBitshuffle) flags |= kFlagBitshuffle;
+      if (filters[i] == kDelta) flags |= kFlagDelta;
+    }
+    p->split = split_block(splitmode, 0, filters, ts, bs) != 0;
+    if (!p->split) flags |= kFlagDontSplit;
+  }
+  p->memcpyed = memcpyed;
+  int32_t hb = ctx_blocksize > 0 ? ctx_blocksize : bs;
+  if (nbytes > 0 && hb > nbytes) hb = nbytes;
+  p->header_blocksize = hb;
+  uint8_t* h = p->header;
+  memset(h, 0, 32);
+  h[0] = 5; h[1] = 1; h[2] = flags; h[3] = (uint8_t)ts;
+  for (int k = 0; k < 4; k++) { h[4 + k] = (uint8_t)(nbytes >> (8 * k)); h[8 + k] = (uint8_t)(hb >> (8 * k)); }
+  for (int i = 0; i < 6; i++) { h[16 + i] = filters[i]; h[24 + i] = filters_meta[i]; }
+  h[22] = 0;   // udcompcode = BLOSCLZ
+  return 0;
+}
+
+static bool hostside_trunc_ok(int8_t prec, int32_t ts, int* zeroed) {
+  const int mant = ts == 4 ? 23 : (ts == 8 ? 52 : -1);
+  if (mant < 0) return false;
+  const int pp = prec;
+  if ((pp < 0 ? -pp : pp) > mant) return false;
+  *zeroed = pp >= 0 ? mant - pp : -pp;
+  return *zeroed < mant;
+}
+
+int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stride, int32_t nchunks, uint8_t* d_dst,
+                   int64_t dst_stride, int32_t* d_cbytes, hipStream_t st) {
+  if (nchunks <= 0) return 0;
+  Workspace* ws = ws_for_current_device();
+  std::lock_guard<std::mutex> lock(ws->mu);
+  const int32_t n = P.nbytes;
+  // header template in device memory (tiny; kept in the mode scratch tail)
+  CGeom g{};
+  g.nbytes = n;
+  g.bs = P.blocksize;
+  g.ts = P.typesize;
+  g.clevel = P.clevel;
+  g.destsize = P.destsize;
+  g.overhead = P.overhead;
+  g.src_stride = src_stride;
+  g.dst_stride = dst_stride;
+  g.wstride = ((int64_t)n + 255) / 256 * 256 + 256;
+  if (P.memcpyed) {
+    if (ws->mode.ensure(64) < 0) return E_MEMORY;
+    uint8_t* htpl = ws->mode.as<uint8_t>();
+    HIPCHK(hipMemcpyAsync(htpl, P.header, 32, hipMemcpyHostToDevice, st));
+    dim3 grid(std::max(1, std::min(64, n / (256 * 16) + 1)), nchunks);
+    k_memcpy_chunks<<<grid, 256, 0, st>>>(d_src, src_stride, d_dst, dst_stride, n, nullptr, htpl, d_cbytes,
+                                          P.overhead, P.destsize);
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
+  g.nblocks = n / g.bs + (n % g.bs ? 1 : 0);
+  g.leftover = n % g.bs;
+  g.spb = P.split ? g.ts : 1;
+  g.neblock = g.bs / g.spb;
+  const int32_t full = g.nblocks - (g.leftover ? 1 : 0);
+  g.nsc = full * g.spb + (g.leftover ? 1 : 0);
+  const int64_t ntot = (int64_t)nchunks * g.nsc;
+  if (ntot > 0x7fffffff) { snprintf(g_err, sizeof g_err, "too many streams"); return E_PARAM; }
+
+  // active forward filters and their buffers (ring tmp, tmp2, input -- see header comment)
+  int act[6], nact = 0;
+  for (int i = 0; i < 6; i++) if (P.filters[i] != kNoFilter) act[nact++] = i;
+  for (int k = 0; k < nact; k++) {
+    const uint8_t f = P.filters[act[k]];
+    if (f > kTruncPrec) { snprintf(g_err, sizeof g_err, "filter %d is not a built-in filter", f); return E_FILTER; }
+  }
+  const size_t wbytes = (size_t)g.wstride * nchunks;
+  int rc = 0;
+  if (nact >= 1) rc |= ws->t1.ensure(wbytes);
+  if (nact >= 2) rc |= ws->t2.ensure(wbytes);
+  const bool clobber = nact >= 3;
+  if (clobber) rc |= ws->work.ensure(wbytes);
+  rc |= ws->sbuf.ensure(wbytes);
+  rc |= ws->res.ensure(sizeof(StreamResult) * (size_t)ntot);
+  rc |= ws->place.ensure(sizeof(Place) * (size_t)ntot);
+  rc |= ws->mode.ensure(sizeof(int32_t) * (size_t)nchunks + 64);
+  if (rc) return E_MEMORY;
+  uint8_t* htpl = ws->mode.as<uint8_t>() + sizeof(int32_t) * (size_t)nchunks;
+  htpl = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(htpl) + 15) & ~uintptr_t(15));
+  HIPCHK(hipMemcpyAsync(htpl, P.header, 32, hipMemcpyHostToDevice, st));
+
+  const uint8_t* raw = d_src;
+  int64_t raw_stride = src_stride;
+  if (clobber) {
+    dim3 grid(std::max(1, std::min(256, n / (256 * 16) + 1)), nchunks);
+    k_copy_work<<<grid, 256, 0, st>>>(d_src, src_stride, ws->work.as<uint8_t>(), g.wstride, n);
+    raw = ws->work.as<uint8_t>();
+    raw_stride = g.wstride;
+  }
+  // forward filters
+  ev_filter.start(st);
+  const uint8_t* filt = raw;
+  int64_t filt_stride = raw_stride;
+  uint8_t* ring[3] = {ws->t1.as<uint8_t>(), ws->t2.as<uint8_t>(), ws->work.as<uint8_t>()};
+  bool has_delta = false;
+  for (int k = 0; k < nact; k++) has_delta |= P.filters[act[k]] == kDelta;
+  const bool two_pass = clobber && has_delta && g.nblocks > 1;
+  for (int pass = two_pass ? 1 : 0; pass <= (two_pass ? 2 : 0); pass++) {
+    const uint8_t* cur = raw;
+    int64_t cur_stride = raw_stride;
+    for (int k = 0; k < nact; k++) {
+      const uint8_t f = P.filters[act[k]], meta = P.filters_meta[act[k]];
+      int zeroed = 0;
+      if (f == kTruncPrec && !hostside_trunc_ok((int8_t)meta, g.ts, &zeroed)) return E_FILTER;
+      uint8_t* outb = ring[k % 3];
+      const int64_t out_stride = (k % 3 == 2) ? g.wstride : g.wstride;
+      dim3 grid(pass == 1 ? 1 : (pass == 2 ? g.nblocks - 1 : g.nblocks), nchunks);
+      k_ffilter<<<grid, kBlockThreads, 0, st>>>(g, pass, f, meta, cur, cur_stride, outb, out_stride, raw, raw_stride, zeroed);
+      cur = outb;
+      cur_stride = out_stride;
+    }
+    filt = cur;
+    filt_stride = cur_stride;
+  }
+  ev_filter.stop(st);
+  if (nact > 0 && filt_stride != g.wstride) return E_FAILURE;
+  // encoder reads the filtered streams at c*wstride: if no filter ran, stage the input there
+  if (nact == 0) {
+    rc = ws->t1.ensure(wbytes);
+    if (rc) return rc;
+    dim3 grid(std::max(1, std::min(256, n / (256 * 16) + 1)), nchunks);
+    k_copy_work<<<grid, 256, 0, st>>>(raw, raw_stride, ws->t1.as<uint8_t>(), g.wstride, n);
+    filt = ws->t1.as<uint8_t>();
+  }
+  HIPCHK(hipGetLastError());
+
+  // encode
+  ev_encode.start(st);
+  const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
+  const bool small = std::max(g.neblock, g.leftover) <= 65536;
+  StreamResult* res = ws->res.as<StreamResult>();
+  if (small) {
+    const size_t lds = (sizeof(uint16_t) << hashlog) + kTagBuckets;
+    k_encode<uint16_t><<<(uint32_t)ntot, 64, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot);
+  } else {
+    const size_t lds = (sizeof(uint32_t) << hashlog) + kTagBuckets;   // up to 66 KiB: opt in
+    static bool attr_set = false;
+    if (!attr_set) {
+      HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_encode<uint32_t>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr_set = true;
+    }
+    k_encode<uint32_t><<<(uint32_t)ntot, 64, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot);
+  }
+  ev_encode.stop(st);
+  HIPCHK(hipGetLastError());
+
+  ev_final.start(st);
+  Place* place = ws->place.as<Place>();
+  int32_t* mode = ws->mode.as<int32_t>();
+  k_finalize<<<(nchunks + 63) / 64, 64, 0, st>>>(g, res, place, mode, d_dst, d_cbytes, nchunks, htpl);
+  k_scatter<<<(uint32_t)ntot, kBlockThreads, 0, st>>>(g, place, mode, res, filt, ws->sbuf.as<uint8_t>(), d_dst, (int32_t)ntot);
+  {
+    dim3 grid(std::max(1, std::min(64, n / (256 * 16) + 1)), nchunks);
+    k_memcpy_chunks<<<grid, 256, 0, st>>>(raw, raw_stride, d_dst, dst_stride, n, mode, htpl, d_cbytes,
+                                          P.overhead, P.destsize);
+  }
+  ev_final.stop(st);
+  HIPCHK(hipGetLastError());
+  if (g_timing) {
+    g_times.filter_ms = ev_filter.ms();
+    g_times.encode_ms = ev_encode.ms();
+    g_times.finalize_ms = ev_final.ms();
+  }
+  return 0;
+}
+
+// ============================================================== decompression: planning ====
+__device__ __forceinline__ int32_t rd32(const uint8_t* p) {
+  return (int32_t)((uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24));
+}
+
+// read_chunk_header + initialize_context_decompression (blosc/blosc2.c:738-852, 2688-2909)
+__global__ void k_dplan_chunks(const uint8_t* const* __restrict__ srcs, const int32_t* __restrict__ srcsize,
+                               const int32_t* __restrict__ dstsize, DChunk* __restrict__ ch, int32_t n) {
+  const int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  DChunk d;
+  memset(&d, 0, sizeof d);
+  const uint8_t* s = srcs[c];
+  const int32_t ss = srcsize[c];
+  auto fail = [&](int32_t code) { d.status = code; d.nstreams = 0; d.nblocks = 0; ch[c] = d; };
+  if (ss < kHdrMin) return fail(E_READ);
+  d.version = s[0];
+  d.flags = s[2];
+  d.typesize = s[3];
+  d.nbytes = rd32(s + 4);
+  d.blocksize = rd32(s + 8);
+  const int32_t cb = rd32(s + 12);
+  if (cb < kHdrMin || d.blocksize <= 0 || d.blocksize > 536866816 || d.typesize == 0) return fail(E_HEADER);
+  const bool ext = (d.flags & kFlagShuffle) && (d.flags & kFlagBitshuffle);
+  if (ext) {
+    if (cb < kHdrExt || ss < kHdrExt) return fail(ss < kHdrExt ? E_READ : E_HEADER);
+    for (int i = 0; i < 6; i++) { d.filters[i] = s[16 + i]; d.filters_meta[i] = s[24 + i]; }
+    d.codec = s[22];
+    const uint8_t flags2 = s[30], bflags = s[31];
+    if (flags2 != 0) return fail(E_VERSION);          // VL blocks: not on the device path
+    if (bflags & 0x08) return fail(E_PARAM);            // lazy chunks need a frame
+    if (bflags & 0x01) return fail(E_CODEC);            // dictionaries: LZ4/ZSTD only
+    d.special = (bflags >> 4) & 7;
+    if (d.version == 3) { d.filters[5] = 0; d.filters_meta[5] = 0; }
+    d.overhead = kHdrExt;
+  } else {
+    // flags_to_filters + get_filter_flags (blosc/blosc2.c:704-735)
+    if ((d.flags & kFlagShuffle) && d.typesize > 1) d.filters[5] = kShuffle;
+    if (d.flags & kFlagBitshuffle) d.filters[5] = kBitshuffle;
+    if (d.flags & kFlagDelta) d.filters[4] = kDelta;
+    d.overhead = kHdrMin;
+  }
+  if (d.nbytes > 0 && d.blocksize > d.nbytes) d.blocksize = d.nbytes;
+  if (cb > ss) return fail(E_HEADER);
+  if (d.nbytes > dstsize[c]) return fail(E_WRITE);
+  if (d.special > kSpecialUninit) return fail(E_DATA);
+  const bool memcpyed = d.flags & kFlagMemcpy;
+  if (memcpyed && cb != d.nbytes + d.overhead) return fail(E_DATA);
+  d.status = d.nbytes;
+  d.nblocks = d.nbytes / d.blocksize + (d.nbytes % d.blocksize ? 1 : 0);
+  d.leftover = d.nbytes % d.blocksize;
+  d.dont_split = (d.flags >> 4) & 1;
+  if (d.nbytes == 0 || memcpyed || d.special) {
+    d.nblocks = 0;   // handled by k_dspecial, not by the block table
+    d.nstreams = 0;
+    ch[c] = d;
+    return;
+  }
+  if (ss < d.overhead + 4 * d.nblocks) return fail(E_READ);
+  const int32_t spb = d.dont_split ? 1 : d.typesize;
+  d.nstreams = (d.nblocks - (d.leftover ? 1 : 0)) * spb + (d.leftover ? 1 : 0);
+  // backward pipeline: active filters (not NOFILTER / TRUNC_PREC), applied high slot -> low
+  int k = 0, K = 0;
+  for (int i = 5; i >= 0; i--) if (d.filters[i] != kNoFilter && d.filters[i] != kTruncPrec) K++;
+  for (int i = 5; i >= 0; i--) {
+    const uint8_t f = d.filters[i];
+    if (f == kNoFilter || f == kTruncPrec) continue;
+    if (f > kTruncPrec) return fail(E_FILTER);   // user filters: host path only
+    d.has_delta |= f == kDelta;
+    d.fsrc[i] = (k % 2 == 0) ? 0 : 1;
+    d.fdst[i] = (k == K - 1) ? 2 : ((k % 2 == 0) ? 1 : 0);
+    k++;
+  }
+  d.nfilters_bwd = (uint8_t)K;
+  ch[c] = d;
+}
+
+struct DTotals {
+  int64_t stage_bytes;
+  int32_t nblocks, nstreams;
+  int32_t any_delta, max_filters;
+};
+
+// Single-workgroup exclusive scans (block_base, stream_base, stage_off) + totals.
+__global__ __launch_bounds__(1024) void k_dscan(DChunk* __restrict__ ch, int32_t n, DTotals* __restrict__ tot) {
+  __shared__ int64_t sb[1024];
+  __shared__ int32_t sbk[1024], sst[1024], sdl[1024], smf[1024];
+  const int32_t per = (n + blockDim.x - 1) / blockDim.x;
+  const int32_t lo = min(n, (int32_t)threadIdx.x * per), hi = min(n, lo + per);
+  int64_t a = 0;
+  int32_t bk = 0, st = 0, dl = 0, mf = 0;
+  for (int32_t i = lo; i < hi; i++) {
+    if (ch[i].status < 0) continue;
+    a += ch[i].nstreams ? ch[i].nbytes : 0;
+    bk += ch[i].nblocks;
+    st += ch[i].nstreams;
+    dl |= ch[i].has_delta;
+    mf = max(mf, (int32_t)ch[i].nfilters_bwd);
+  }
+  sb[threadIdx.x] = a; sbk[threadIdx.x] = bk; sst[threadIdx.x] = st; sdl[threadIdx.x] = dl; smf[threadIdx.x] = mf;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t ra = 0;
+    int32_t rb = 0, rs = 0, rd = 0, rm = 0;
+    for (int t = 0; t < (int)blockDim.x; t++) {
+      int64_t va = sb[t]; int32_t vb = sbk[t], vs = sst[t];
+      sb[t] = ra; sbk[t] = rb; sst[t] = rs;
+      ra += va; rb += vb; rs += vs; rd |= sdl[t]; rm = max(rm, smf[t]);
+    }
+    tot->stage_bytes = ra; tot->nblocks = rb; tot->nstreams = rs; tot->any_delta = rd; tot->max_filters = rm;
+  }
+  __syncthreads();
+  int64_t ra = sb[threadIdx.x];
+  int32_t rb = sbk[threadIdx.x], rs = sst[threadIdx.x];
+  for (int32_t i = lo; i < hi; i++) {
+    ch[i].stage_off = ra;
+    ch[i].block_base = rb;
+    ch[i].stream_base = rs;
+    if (ch[i].status < 0) continue;
+    ra += ch[i].nstreams ? ch[i].nbytes : 0;
+    rb += ch[i].nblocks;
+    rs += ch[i].nstreams;
+  }
+}
+
+struct DBlock {
+  int32_t chunk, block;
+};
+
+__device__ int32_t find_chunk(const DChunk* ch, int32_t n, int32_t idx) {
+  int32_t lo = 0, hi = n - 1;   // last chunk with block_base <= idx and nblocks > 0
+  while (lo < hi) {
+    const int32_t mid = (lo + hi + 1) >> 1;
+    if (ch[mid].block_base <= idx) lo = mid; else hi = mid - 1;
+  }
+  while (lo > 0 && (ch[lo].nblocks == 0 || ch[lo].status < 0 || ch[lo].block_base > idx)) lo--;
+  return lo;
+}
+
+// Per block: read bstarts, walk the csize words of its streams (blosc/blosc2.c:1987-2025).
+__global__ void k_dplan_blocks(const uint8_t* const* __restrict__ srcs, const int32_t* __restrict__ srcsize,
+                               DChunk* __restrict__ ch, int32_t n, DBlock* __restrict__ blocks,
+                               DStream* __restrict__ streams, int32_t nblocks_total) {
+  const int32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= nblocks_total) return;
+  const int32_t c = find_chunk(ch, n, idx);
+  const DChunk d = ch[c];
+  const int32_t b = idx - d.block_base;
+  blocks[idx].chunk = c;
+  blocks[idx].block = b;
+  const uint8_t* s = srcs[c];
+  const int32_t ss = srcsize[c];
+  const bool lo = (b == d.nblocks - 1) && d.leftover;
+  const int32_t bsize = lo ? d.leftover : d.blocksize;
+  const int32_t ns = (!d.dont_split && !lo) ? d.typesize : 1;
+  const int32_t neblock = bsize / ns;
+  const int32_t sbase = d.stream_base + b * (d.dont_split ? 1 : d.typesize);
+  int32_t pos = rd32(s + d.overhead + 4 * b);
+  int32_t err = 0;
+  if (pos <= 0 || pos >= ss) err = E_DATA;
+  if (neblock == 0) err = E_WRITE;
+  for (int32_t j = 0; j < ns; j++) {
+    DStream st;
+    st.chunk = c;
+    st.neblock = neblock;
+    st.dst_off = b * d.blocksize + j * neblock;
+    st.csize = 0;
+    st.src = 0;
+    if (!err) {
+      if (ss - pos < 4) { err = E_READ; }
+      else {
+        const int32_t cs = rd32(s + pos);
+        pos += 4;
+        int32_t payload = cs > 0 ? cs : (cs < 0 ? 1 : 0);
+        if (ss - pos < payload) err = E_READ;
+        st.csize = cs;
+        st.src = pos;
+        pos += payload;
+      }
+    }
+    if (err) st.neblock = -1;
+    streams[sbase + j] = st;
+  }
+  if (err) atomicMin(&ch[c].status, err);
+}
+
+// One wave per stream.
+__global__ __launch_bounds__(64) void k_decode(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
+                                               DChunk* __restrict__ ch, const DStream* __restrict__ streams,
+                                               uint8_t* __restrict__ stage, int32_t nstreams_total,
+                                               const uint8_t* __restrict__ maskout) {
+  const int32_t s = blockIdx.x;
+  if (s >= nstreams_total) return;
+  const DStream st = streams[s];
+  const int32_t c = st.chunk;
+  const DChunk d = ch[c];
+  if (d.status < 0 || st.neblock < 0) return;
+  if (maskout && maskout[st.dst_off / d.blocksize]) return;
+  const uint8_t* in = srcs[c] + st.src;
+  uint8_t* out = (d.nfilters_bwd ? stage + d.stage_off : dsts[c]) + st.dst_off;
+  const int32_t nb = st.neblock;
+  const int lane = threadIdx.x;
+  if (st.csize == 0) {
+    for (int32_t i = lane; i < nb; i += 64) out[i] = 0;
+  } else if (st.csize < 0) {
+    const uint8_t token = in[0];
+    if (!(token & 1) || st.csize < -255) { if (lane == 0) atomicMin(&ch[c].status, E_RUNLEN); return; }
+    const uint8_t v = (uint8_t)(-st.csize);
+    for (int32_t i = lane; i < nb; i += 64) out[i] = v;
+  } else if (st.csize == nb) {
+    for (int32_t i = lane; i < nb; i += 64) out[i] = in[i];
+  } else {
+    if ((d.flags >> 5) != 0) { if (lane == 0) atomicMin(&ch[c].status, E_CODEC); return; }
+    const int32_t got = wave_lz_decode(in, st.csize, out, nb);
+    if (got != nb && lane == 0) atomicMin(&ch[c].status, E_DATA);
+  }
+}
+
+// Backward filter for filter slot `slot`; pass 0: all blocks, 1: block 0 only, 2: blocks >= 1.
+__global__ __launch_bounds__(kBlockThreads) void k_dfilter(DChunk* __restrict__ ch, const DBlock* __restrict__ blocks,
+                                                           uint8_t* const* __restrict__ dsts, uint8_t* __restrict__ stage,
+                                                           uint8_t* __restrict__ stage2, int slot, int pass,
+                                                           int32_t nblocks_total, const uint8_t* __restrict__ maskout) {
+  const int32_t idx = blockIdx.x;
+  if (idx >= nblocks_total) return;
+  const DBlock bk = blocks[idx];
+  if (pass == 1 && bk.block != 0) return;
+  if (pass == 2 && bk.block == 0) return;
+  const DChunk d = ch[bk.chunk];
+  if (d.status < 0) return;
+  const uint8_t f = d.filters[slot];
+  if (f == kNoFilter || f == kTruncPrec) return;
+  if (maskout && maskout[bk.block]) return;
+  const bool lo = (bk.block == d.nblocks - 1) && d.leftover;
+  const int32_t bsize = lo ? d.leftover : d.blocksize;
+  const int64_t off = (int64_t)bk.block * d.blocksize;
+  uint8_t* bufs[3] = {stage + d.stage_off + off, stage2 + d.stage_off + off, dsts[bk.chunk] + off};
+  const uint8_t* s = bufs[d.fsrc[slot]];
+  uint8_t* o = bufs[d.fdst[slot]];
+  const uint8_t meta = d.filters_meta[slot];
+  switch (f) {
+    case kShuffle: block_unshuffle(s, o, bsize, meta ? meta : d.typesize); break;
+    case kBitshuffle: block_bitunshuffle(s, o, bsize, d.typesize, d.version); break;
+    case kDelta:
+      for (int32_t i = threadIdx.x; i < bsize; i += blockDim.x) o[i] = s[i];
+      __syncthreads();
+      if (bk.block == 0) block_delta_decode_first(o, bsize, d.typesize);
+      else block_delta_decode_rest(dsts[bk.chunk], o, bsize, d.typesize);
+      break;
+    default: break;
+  }
+}
+
+// memcpyed / special chunks (blosc/blosc2.c:1865-1935): grid (pieces, n).
+__global__ void k_dspecial(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
+                           const DChunk* __restrict__ ch, const int32_t* __restrict__ srcsize) {
+  const int32_t c = blockIdx.y;
+  const DChunk d = ch[c];
+  if (d.status < 0 || d.nstreams != 0 || d.nbytes == 0) return;
+  const bool memcpyed = d.flags & kFlagMemcpy;
+  const uint8_t* s = srcs[c];
+  uint8_t* o = dsts[c];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d.special == kSpecialZero) {
+    for (int64_t i = i0; i < d.nbytes; i += stride) o[i] = 0;
+  } else if (d.special == kSpecialNan) {
+    if (d.typesize == 4) { for (int64_t i = i0; i < d.nbytes / 4; i += stride) reinterpret_cast<uint32_t*>(o)[i] = 0x7fc00000u; }
+    else { for (int64_t i = i0; i < d.nbytes / 8; i += stride) reinterpret_cast<uint64_t*>(o)[i] = 0x7ff8000000000000ull; }
+  } else if (d.special == kSpecialValue) {
+    const int32_t ts = rd32(s + 12) - kHdrExt;
+    for (int64_t i = i0; i < d.nbytes; i += stride) o[i] = s[kHdrExt + (i % ts)];
+  } else if (d.special == kSpecialUninit) {
+    // nothing to write
+  } else if (memcpyed) {
+    for (int64_t i = i0; i < d.nbytes; i += stride) o[i] = s[d.overhead + i];
+  }
+}
+
+__global__ void k_dstatus(const DChunk* __restrict__ ch, int32_t* __restrict__ status, int32_t n) {
+  const int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < n) status[c] = ch[c].status;
+}
+
+int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint8_t* const* d_dst,
+                     const int32_t* d_dstsize, int32_t n, int64_t dst_bound, int32_t* d_status,
+                     const uint8_t* d_maskout, hipStream_t st) {
+  if (n <= 0) return 0;
+  Workspace* ws = ws_for_current_device();
+  std::lock_guard<std::mutex> lock(ws->mu);
+  if (ws->dchunks.ensure(sizeof(DChunk) * (size_t)n) < 0 || ws->dtotals.ensure(sizeof(DTotals)) < 0) return E_MEMORY;
+  DChunk* ch = ws->dchunks.as<DChunk>();
+  DTotals* tot = ws->dtotals.as<DTotals>();
+  k_dplan_chunks<<<(n + 255) / 256, 256, 0, st>>>(d_src, d_srcsize, d_dstsize, ch, n);
+  k_dscan<<<1, 1024, 0, st>>>(ch, n, tot);
+  HIPCHK(hipGetLastError());
+  DTotals h{};
+  HIPCHK(hipMemcpyAsync(&h, tot, sizeof h, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  (void)dst_bound;
+  int rc = 0;
+  if (h.nblocks > 0) {
+    rc |= ws->dblocks.ensure(sizeof(DBlock) * (size_t)h.nblocks);
+    rc |= ws->dstreams.ensure(sizeof(DStream) * (size_t)h.nstreams);
+    rc |= ws->stage.ensure((size_t)h.stage_bytes);
+    if (h.max_filters >= 2) rc |= ws->stage2.ensure((size_t)h.stage_bytes);
+    if (rc) return E_MEMORY;
+    DBlock* blocks = ws->dblocks.as<DBlock>();
+    DStream* streams = ws->dstreams.as<DStream>();
+    k_dplan_blocks<<<(h.nblocks + 255) / 256, 256, 0, st>>>(d_src, d_srcsize, ch, n, blocks, streams, h.nblocks);
+    ev_decode.start(st);
+    k_decode<<<h.nstreams, 64, 0, st>>>(d_src, d_dst, ch, streams, ws->stage.as<uint8_t>(), h.nstreams, d_maskout);
+    ev_decode.stop(st);
+    ev_unfilter.start(st);
+    if (h.max_filters > 0) {
+      const int passes = h.any_delta ? 2 : 1;
+      for (int ps = 0; ps < passes; ps++) {
+        const int pass = h.any_delta ? ps + 1 : 0;
+        for (int slot = 5; slot >= 0; slot--)
+          k_dfilter<<<h.nblocks, kBlockThreads, 0, st>>>(ch, blocks, d_dst, ws->stage.as<uint8_t>(),
+                                                         ws->stage2.as<uint8_t>(), slot, pass, h.nblocks, d_maskout);
+      }
+    }
+    ev_unfilter.stop(st);
+  }
+  {
+    dim3 grid(64, n);
+    k_dspecial<<<grid, 256, 0, st>>>(d_src, d_dst, ch, d_srcsize);
+  }
+  k_dstatus<<<(n + 255) / 256, 256, 0, st>>>(ch, d_status, n);
+  HIPCHK(hipGetLastError());
+  if (g_timing) {
+    g_times.decode_ms = ev_decode.ms();
+    g_times.unfilter_ms = ev_unfilter.ms();
+  }
+  return 0;
+}
+
+__global__ void k_fill_ptrs(const uint8_t* src, int64_t src_stride, const int32_t* cbytes, uint8_t* dst, int64_t dst_stride,
+                            int32_t dst_cap, const uint8_t** sp, int32_t* ss, uint8_t** dp, int32_t* ds, int32_t n) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  sp[i] = src + (int64_t)i * src_stride;
+  ss[i] = cbytes[i];
+  dp[i] = dst + (int64_t)i * dst_stride;
+  ds[i] = dst_cap;
+}
+
+int decompress_batch_strided(const uint8_t* d_src, int64_t src_stride, const int32_t* d_cbytes, int32_t n, uint8_t* d_dst,
+                             int64_t dst_stride, int32_t dst_cap, int32_t* d_status, hipStream_t st) {
+  if (n <= 0) return 0;
+  Workspace* ws = ws_for_current_device();
+  const size_t need = (size_t)n * (2 * sizeof(void*) + 2 * sizeof(int32_t)) + 64;
+  {
+    std::lock_guard<std::mutex> lock(ws->mu);
+    if (ws->ptrs.ensure(need) < 0) return E_MEMORY;
+  }
+  uint8_t* base = ws->ptrs.as<uint8_t>();
+  const uint8_t** sp = reinterpret_cast<const uint8_t**>(base);
+  uint8_t** dp = reinterpret_cast<uint8_t**>(base + sizeof(void*) * (size_t)n);
+  int32_t* ss = reinterpret_cast<int32_t*>(base + 2 * sizeof(void*) * (size_t)n);
+  int32_t* ds = ss + n;
+  k_fill_ptrs<<<(n + 255) / 256, 256, 0, st>>>(d_src, src_stride, d_cbytes, d_dst, dst_stride, dst_cap, sp, ss, dp, ds, n);
+  HIPCHK(hipGetLastError());
+  return decompress_batch(sp, ss, dp, ds, n, (int64_t)n * dst_cap, d_status, nullptr, st);
+}
+
+// ============================================================================ raw filters ====
+__global__ __launch_bounds__(kBlockThreads) void k_raw_shuffle(const uint8_t* __restrict__ s, uint8_t* __restrict__ d,
+                                                               int32_t nbytes, int32_t ts, int inverse) {
+  // one workgroup over the whole buffer is far too slow for 256 MiB; split into planes-major
+  // tiles: every workgroup owns elements [e0, e1) of all planes.
+  const int32_t n = nbytes / ts;
+  const int32_t per = ((n + gridDim.x - 1) / gridDim.x + 3) & ~3;
+  const int32_t e0 = min(n, (int32_t)blockIdx.x * per), e1 = min(n, e0 + per);
+  if (e0 < e1) {
+    const int32_t cnt = e1 - e0;
+    const bool fast = (cnt % 4 == 0) && (n % 4 == 0) && (e0 % 4 == 0) &&
+                      aligned16(s) && aligned16(d) && (ts == 2 || ts == 4 || ts == 8 || ts == 16);
+    if (fast) {
+      for (int32_t q = threadIdx.x; q < cnt / 4; q += blockDim.x) {
+        const int32_t e = e0 + 4 * q;
+        if (!inverse) {
+          for (int plane = 0; plane < ts; plane++) {
+            uint32_t o = 0;
+            for (int k = 0; k < 4; k++) o |= (uint32_t)s[(int64_t)(e + k) * ts + plane] << (8 * k);
+            *reinterpret_cast<uint32_t*>(d + (int64_t)plane * n + e) = o;
+          }
+        } else {
+          for (int plane = 0; plane < ts; plane++) {
+            const uint32_t w = *reinterpret_cast<const uint32_t*>(s + (int64_t)plane * n + e);
+            for (int k = 0; k < 4; k++) d[(int64_t)(e + k) * ts + plane] = (uint8_t)(w >> (8 * k));
+          }
+        }
+      }
+    } else {
+      for (int64_t i = threadIdx.x; i < (int64_t)cnt * ts; i += blockDim.x) {
+        const int32_t e = e0 + (int32_t)(i / ts), plane = (int32_t)(i % ts);
+        if (!inverse) d[(int64_t)plane * n + e] = s[(int64_t)e * ts + plane];
+        else d[(int64_t)e * ts + plane] = s[(int64_t)plane * n + e];
+      }
+    }
+  }
+  if (blockIdx.x == 0)
+    for (int32_t i = n * ts + threadIdx.x; i < nbytes; i += blockDim.x) d[i] = s[i];
+}
+
+int shuffle_dev(int32_t ts, int32_t nbytes, const uint8_t* d_src, uint8_t* d_dst, bool inverse, hipStream_t st) {
+  if (ts < 1 || ts > 256 || nbytes < 0) return E_PARAM;
+  if (nbytes == 0) return 0;
+  const int32_t n = nbytes / ts;
+  const int grid = std::max(1, std::min(4096, n / 1024 + 1));
+  k_raw_shuffle<<<grid, kBlockThreads, 0, st>>>(d_src, d_dst, nbytes, ts, inverse ? 1 : 0);
+  HIPCHK(hipGetLastError());
+  return nbytes;
+}
+
+__global__ __launch_bounds__(kBlockThreads) void k_raw_bitshuffle(const uint8_t* __restrict__ s, uint8_t* __restrict__ d,
+                                                                  int32_t nbytes, int32_t ts, int inverse,
+                                                                  uint8_t version) {
+  const int32_t nel = nbytes / ts;
+  if (inverse && version == 2 && (nel % 8) != 0) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nbytes; i += (int64_t)gridDim.x * blockDim.x) d[i] = s[i];
+    return;
+  }
+  const int32_t m = nel & ~7;
+  const int32_t rowlen = m / 8;
+  for (int32_t gi = blockIdx.x * blockDim.x + threadIdx.x; gi < rowlen; gi += gridDim.x * blockDim.x) {
+    if (!inverse) {
+      const uint8_t* e8 = s + (int64_t)gi * 8 * ts;
+      for (int32_t b = 0; b < ts; b++) {
+        uint64_t x = 0;
+        for (int r = 0; r < 8; r++) x |= (uint64_t)e8[r * ts + b] << (8 * r);
+        x = bit_transpose8(x);
+        for (int k = 0; k < 8; k++) d[(int64_t)(8 * b + k) * rowlen + gi] = (uint8_t)(x >> (8 * k));
+      }
+    } else {
+      uint8_t* e8 = d + (int64_t)gi * 8 * ts;
+      for (int32_t b = 0; b < ts; b++) {
+        uint64_t y = 0;
+        for (int k = 0; k < 8; k++) y |= (uint64_t)s[(int64_t)(8 * b + k) * rowlen + gi] << (8 * k);
+        y = bit_transpose8(y);
+        for (int r = 0; r < 8; r++) e8[r * ts + b] = (uint8_t)(y >> (8 * r));
+      }
+    }
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = (int64_t)m * ts + threadIdx.x; i < nbytes; i += blockDim.x) d[i] = s[i];
+}
+
+int bitshuffle_dev(int32_t ts, int32_t nbytes, const uint8_t* d_src, uint8_t* d_dst, bool inverse, uint8_t version,
+                   hipStream_t st) {
+  if (ts < 1 || ts > 256 || nbytes < 0) return E_PARAM;
+  if (nbytes == 0) return 0;
+  const int32_t rows = (nbytes / ts) / 8;
+  const int grid = std::max(1, std::min(4096, rows / 256 + 1));
+  k_raw_bitshuffle<<<grid, kBlockThreads, 0, st>>>(d_src, d_dst, nbytes, ts, inverse ? 1 : 0, version);
+  HIPCHK(hipGetLastError());
+  return nbytes;
+}
+
+}  // namespace b2h

@@ -1,0 +1,267 @@
+// b2h_filters.h -- workgroup-level block filters for gfx950 (device code, included by
+// b2h_engine.hip).  Each routine transforms ONE block `src -> dst` with the whole workgroup and
+// reproduces the reference filter byte-for-byte:
+//   shuffle / unshuffle      blosc/shuffle-generic.h:34-83, blosc/shuffle.c:416-449
+//   bitshuffle / unshuffle   blosc/bitshuffle-generic.c:147-258, blosc/shuffle.c:454-521
+//   delta encode / decode    blosc/delta.c:18-161
+//   trunc-prec               blosc/trunc-prec.c:23-86
+// Byte transposes move 16 B per lane on the element side and 4 B per lane per plane on the plane
+// side, so both the HBM read and write streams are fully coalesced.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace b2h {
+
+constexpr int kBlockThreads = 256;
+
+__device__ __forceinline__ uint32_t byte_of(uint32_t w, int k) { return (w >> (8 * k)) & 0xffu; }
+
+// ------------------------------------------------------------------------------- shuffle ----
+// Fast path: TS in {2,4,8,16}, n % 4 == 0, 16-byte aligned src/dst.  Thread t owns elements
+// [4t, 4t+4): it reads 4*TS contiguous bytes and writes one u32 into each of the TS planes.
+template <int TS>
+__device__ void shuffle_fast(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t n) {
+  const int32_t quads = n / 4;
+  for (int32_t q = threadIdx.x; q < quads; q += blockDim.x) {
+    uint32_t w[TS];   // 4*TS bytes = elements 4q..4q+3
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + (int64_t)q * 4 * TS);
+    if constexpr (TS % 4 == 0) {
+#pragma unroll
+      for (int k = 0; k < TS / 4; k++) {
+        uint4 v = reinterpret_cast<const uint4*>(s32)[k];
+        w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+      }
+    } else {  // TS == 2
+      uint2 v = *reinterpret_cast<const uint2*>(s32);
+      w[0] = v.x; w[1] = v.y;
+    }
+#pragma unroll
+    for (int plane = 0; plane < TS; plane++) {
+      uint32_t o = 0;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int byte = e * TS + plane;     // byte index inside the 4*TS bytes
+        o |= byte_of(w[byte / 4], byte % 4) << (8 * e);
+      }
+      reinterpret_cast<uint32_t*>(dst + (int64_t)plane * n)[q] = o;
+    }
+  }
+}
+
+template <int TS>
+__device__ void unshuffle_fast(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t n) {
+  const int32_t quads = n / 4;
+  for (int32_t q = threadIdx.x; q < quads; q += blockDim.x) {
+    uint32_t p[TS];
+#pragma unroll
+    for (int plane = 0; plane < TS; plane++) p[plane] = reinterpret_cast<const uint32_t*>(src + (int64_t)plane * n)[q];
+    uint32_t w[TS];
+#pragma unroll
+    for (int k = 0; k < TS; k++) {
+      uint32_t o = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const int byte = 4 * k + b;           // output byte inside the 4*TS bytes
+        o |= byte_of(p[byte % TS], byte / TS) << (8 * b);
+      }
+      w[k] = o;
+    }
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + (int64_t)q * 4 * TS);
+    if constexpr (TS % 4 == 0) {
+#pragma unroll
+      for (int k = 0; k < TS / 4; k++) reinterpret_cast<uint4*>(d32)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+    } else {
+      *reinterpret_cast<uint2*>(d32) = make_uint2(w[0], w[1]);
+    }
+  }
+}
+
+__device__ __forceinline__ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// Whole-block byte shuffle (any typesize 1..256), tail bytes copied verbatim.
+__device__ void block_shuffle(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t bsize, int32_t ts) {
+  const int32_t n = bsize / ts;
+  const bool fast = (n % 4 == 0) && aligned16(src) && aligned16(dst);
+  if (fast && ts == 4) shuffle_fast<4>(src, dst, n);
+  else if (fast && ts == 8) shuffle_fast<8>(src, dst, n);
+  else if (fast && ts == 2) shuffle_fast<2>(src, dst, n);
+  else if (fast && ts == 16) shuffle_fast<16>(src, dst, n);
+  else if (ts == 1) {
+    for (int32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+  } else {
+    for (int64_t i = threadIdx.x; i < (int64_t)n * ts; i += blockDim.x) {
+      const int32_t plane = (int32_t)(i / n), e = (int32_t)(i % n);
+      dst[i] = src[(int64_t)e * ts + plane];
+    }
+  }
+  for (int32_t i = n * ts + threadIdx.x; i < bsize; i += blockDim.x) dst[i] = src[i];
+}
+
+__device__ void block_unshuffle(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t bsize, int32_t ts) {
+  const int32_t n = bsize / ts;
+  const bool fast = (n % 4 == 0) && aligned16(src) && aligned16(dst);
+  if (fast && ts == 4) unshuffle_fast<4>(src, dst, n);
+  else if (fast && ts == 8) unshuffle_fast<8>(src, dst, n);
+  else if (fast && ts == 2) unshuffle_fast<2>(src, dst, n);
+  else if (fast && ts == 16) unshuffle_fast<16>(src, dst, n);
+  else if (ts == 1) {
+    for (int32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+  } else {
+    for (int64_t i = threadIdx.x; i < (int64_t)n * ts; i += blockDim.x) {
+      const int32_t e = (int32_t)(i / ts), plane = (int32_t)(i % ts);
+      dst[i] = src[(int64_t)plane * n + e];
+    }
+  }
+  for (int32_t i = n * ts + threadIdx.x; i < bsize; i += blockDim.x) dst[i] = src[i];
+}
+
+// ---------------------------------------------------------------------------- bitshuffle ----
+// 8x8 bit-matrix transpose of a u64 whose byte r is row r (bit c = column c): afterwards byte c
+// holds column c, i.e. bit r of byte c = bit c of input byte r.  Three swap stages of 1/2/4.
+__device__ __forceinline__ uint64_t bit_transpose8(uint64_t x) {
+  const uint64_t m1 = 0x00AA00AA00AA00AAull, m2 = 0x0000CCCC0000CCCCull, m4 = 0x00000000F0F0F0F0ull;
+  uint64_t t;
+  t = (x ^ (x >> 7)) & m1;  x ^= t ^ (t << 7);
+  t = (x ^ (x >> 14)) & m2; x ^= t ^ (t << 14);
+  t = (x ^ (x >> 28)) & m4; x ^= t ^ (t << 28);
+  return x;
+}
+
+// Output row r = 8*b + k (b: byte of the element, k: bit) has m/8 bytes; byte g of row r packs
+// bit k of byte b of elements 8g..8g+7 (element 8g+i in bit i).  Thread g owns one 8-element group.
+__device__ void block_bitshuffle(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t bsize, int32_t ts) {
+  const int32_t m = (bsize / ts) & ~7;
+  const int32_t rowlen = m / 8;
+  for (int32_t g = threadIdx.x; g < rowlen; g += blockDim.x) {
+    const uint8_t* e8 = src + (int64_t)g * 8 * ts;   // 8 consecutive elements
+    for (int32_t b = 0; b < ts; b++) {
+      uint64_t x = 0;
+#pragma unroll
+      for (int r = 0; r < 8; r++) x |= (uint64_t)e8[r * ts + b] << (8 * r);
+      x = bit_transpose8(x);
+#pragma unroll
+      for (int k = 0; k < 8; k++) dst[(int64_t)(8 * b + k) * rowlen + g] = (uint8_t)(x >> (8 * k));
+    }
+  }
+  for (int32_t i = m * ts + threadIdx.x; i < bsize; i += blockDim.x) dst[i] = src[i];
+}
+
+// Inverse.  format_version == 2 (Blosc1 chunks): un-bitshuffle only if (bsize/ts) % 8 == 0,
+// else plain copy (blosc/shuffle.c:489-505).
+__device__ void block_bitunshuffle(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t bsize, int32_t ts,
+                                   uint8_t format_version) {
+  const int32_t n = bsize / ts;
+  if (format_version == 2 && (n % 8) != 0) {
+    for (int32_t i = threadIdx.x; i < bsize; i += blockDim.x) dst[i] = src[i];
+    return;
+  }
+  const int32_t m = n & ~7;
+  const int32_t rowlen = m / 8;
+  for (int32_t g = threadIdx.x; g < rowlen; g += blockDim.x) {
+    uint8_t* e8 = dst + (int64_t)g * 8 * ts;
+    for (int32_t b = 0; b < ts; b++) {
+      uint64_t y = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) y |= (uint64_t)src[(int64_t)(8 * b + k) * rowlen + g] << (8 * k);
+      y = bit_transpose8(y);
+#pragma unroll
+      for (int r = 0; r < 8; r++) e8[r * ts + b] = (uint8_t)(y >> (8 * r));
+    }
+  }
+  for (int32_t i = m * ts + threadIdx.x; i < bsize; i += blockDim.x) dst[i] = src[i];
+}
+
+// --------------------------------------------------------------------------------- delta ----
+__device__ __forceinline__ int delta_width(int32_t ts) {
+  if (ts == 1 || ts == 2 || ts == 4 || ts == 8) return ts;
+  return (ts % 8 == 0) ? 8 : 1;
+}
+
+// Encoder.  Block 0: d[i] = s[i] ^ s[i-1] over w-byte words (d[0] = s[0]); `cur` is the stage
+// input (the reference passes _src as dref for block 0).  Other blocks: d = s ^ dref where dref is
+// the chunk's block-0 region of the pipeline input (blosc/blosc2.c:1126-1128).  Only
+// (bsize / w) * w bytes are written, as in the reference.
+__device__ void block_delta_encode(const uint8_t* __restrict__ cur, const uint8_t* __restrict__ dref,
+                                   uint8_t* __restrict__ dst, int32_t bsize, int32_t ts, bool first_block) {
+  const int w = delta_width(ts);
+  const int32_t nb = bsize / w * w;
+  if (first_block) {
+    for (int32_t i = threadIdx.x; i < nb; i += blockDim.x) dst[i] = i < w ? cur[i] : (uint8_t)(cur[i] ^ cur[i - w]);
+  } else if ((nb % 16) == 0 && aligned16(cur) && aligned16(dref) && aligned16(dst)) {
+    for (int32_t i = threadIdx.x; i < nb / 16; i += blockDim.x) {
+      uint4 a = reinterpret_cast<const uint4*>(cur)[i], b = reinterpret_cast<const uint4*>(dref)[i];
+      reinterpret_cast<uint4*>(dst)[i] = make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
+    }
+  } else {
+    for (int32_t i = threadIdx.x; i < nb; i += blockDim.x) dst[i] = cur[i] ^ dref[i];
+  }
+}
+
+// Decoder for blocks >= 1 (in place): d ^= decoded block 0.
+__device__ void block_delta_decode_rest(const uint8_t* __restrict__ dref, uint8_t* __restrict__ d, int32_t bsize, int32_t ts) {
+  const int w = delta_width(ts);
+  const int32_t nb = bsize / w * w;
+  if ((nb % 16) == 0 && aligned16(dref) && aligned16(d)) {
+    for (int32_t i = threadIdx.x; i < nb / 16; i += blockDim.x) {
+      uint4 a = reinterpret_cast<uint4*>(d)[i], b = reinterpret_cast<const uint4*>(dref)[i];
+      reinterpret_cast<uint4*>(d)[i] = make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
+    }
+  } else {
+    for (int32_t i = threadIdx.x; i < nb; i += blockDim.x) d[i] ^= dref[i];
+  }
+}
+
+// Decoder for block 0 (in place): running XOR over w-byte words = inclusive XOR-scan.  Each
+// thread scans a contiguous segment, the segment totals are XOR-scanned through LDS, then each
+// segment is re-walked with its carry.  Byte-wise: d[x] ^= d[x - w] serially == XOR of the bytes
+// x, x-w, x-2w, ... so the scan runs on w-byte words.
+__device__ void block_delta_decode_first(uint8_t* __restrict__ d, int32_t bsize, int32_t ts) {
+  __shared__ uint64_t carry[kBlockThreads];
+  const int w = delta_width(ts);
+  const int32_t nw = bsize / w;
+  const int32_t per = (nw + blockDim.x - 1) / blockDim.x;
+  const int32_t lo = min(nw, (int32_t)threadIdx.x * per), hi = min(nw, lo + per);
+  auto ldw = [&](int32_t i) { uint64_t v = 0; for (int k = 0; k < w; k++) v |= (uint64_t)d[(int64_t)i * w + k] << (8 * k); return v; };
+  auto stw = [&](int32_t i, uint64_t v) { for (int k = 0; k < w; k++) d[(int64_t)i * w + k] = (uint8_t)(v >> (8 * k)); };
+  uint64_t acc = 0;
+  for (int32_t i = lo; i < hi; i++) acc ^= ldw(i);
+  carry[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t run = 0;
+    for (int t = 0; t < (int)blockDim.x; t++) { uint64_t v = carry[t]; carry[t] = run; run ^= v; }
+  }
+  __syncthreads();
+  uint64_t run = carry[threadIdx.x];
+  for (int32_t i = lo; i < hi; i++) { run ^= ldw(i); stw(i, run); }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------- trunc-prec ----
+// dst = src & ~((1 << zeroed) - 1) per element; returns false on invalid parameters.
+__device__ __forceinline__ bool trunc_zeroed_bits(int8_t prec, int32_t ts, int* zeroed) {
+  const int mant = ts == 4 ? 23 : (ts == 8 ? 52 : -1);
+  if (mant < 0) return false;
+  const int p = prec;
+  if ((p < 0 ? -p : p) > mant) return false;
+  *zeroed = p >= 0 ? mant - p : -p;
+  return *zeroed < mant;
+}
+
+__device__ void block_trunc(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t bsize, int32_t ts, int zeroed) {
+  const int32_t n = bsize / ts;
+  if (ts == 4) {
+    const uint32_t mask = ~((1u << zeroed) - 1u);
+    for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      uint32_t v; __builtin_memcpy(&v, src + 4 * (int64_t)i, 4); v &= mask; __builtin_memcpy(dst + 4 * (int64_t)i, &v, 4);
+    }
+  } else {
+    const uint64_t mask = ~((1ull << zeroed) - 1ull);
+    for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      uint64_t v; __builtin_memcpy(&v, src + 8 * (int64_t)i, 8); v &= mask; __builtin_memcpy(dst + 8 * (int64_t)i, &v, 8);
+    }
+  }
+}
+
+}  // namespace b2h

@@ -1,0 +1,67 @@
+// b2h_format.h -- chunk-format constants and plan records shared by the HIP engine and the host
+// C-ABI.  Values follow the reference's on-disk format (README_CHUNK_FORMAT.rst and
+// include/blosc2.h:128-300 of c-blosc2); the plan records are this engine's own.
+#pragma once
+#include <stdint.h>
+
+namespace b2h {
+
+constexpr int kHdrMin = 16;        // BLOSC_MIN_HEADER_LENGTH   (include/blosc2.h:177)
+constexpr int kHdrExt = 32;        // BLOSC_EXTENDED_HEADER_LENGTH (include/blosc2.h:180)
+constexpr int kMinBuffer = 32;     // BLOSC_MIN_BUFFERSIZE      (include/blosc2.h:193)
+constexpr int kMaxFilters = 6;     // BLOSC2_MAX_FILTERS
+constexpr int kMaxStreams = 16;    // MAX_STREAMS               (blosc/stune.h:24)
+
+// header flag bits (include/blosc2.h:273-277)
+constexpr uint8_t kFlagShuffle = 0x1, kFlagMemcpy = 0x2, kFlagBitshuffle = 0x4, kFlagDelta = 0x8,
+                  kFlagDontSplit = 0x10;
+// filter ids (include/blosc2.h:248-259)
+constexpr uint8_t kNoFilter = 0, kShuffle = 1, kBitshuffle = 2, kDelta = 3, kTruncPrec = 4;
+constexpr uint8_t kSpecialZero = 1, kSpecialNan = 2, kSpecialValue = 3, kSpecialUninit = 4;
+
+// BloscLZ constants (blosc/blosclz.c:45-47, 442-465)
+constexpr int kLzMaxCopy = 32;
+constexpr uint32_t kLzNear = 8191;
+constexpr uint32_t kLzFar = 65535 + 8191 - 1;
+
+// Result of encoding one stream with maxout == neblock, enough to reproduce the serial
+// reference decision for any smaller maxout (see b2h_lz.h: peak).
+enum StreamKind : int32_t { kStreamZeroRun = 0, kStreamByteRun = 1, kStreamRaw = 2, kStreamLz = 3 };
+
+struct StreamResult {
+  int32_t kind;   // StreamKind
+  int32_t size;   // LZ: encoded bytes; run: the repeated byte
+  int32_t peak;   // LZ: largest `op + k` bound check made while encoding (<= neblock)
+  int32_t pad;
+};
+
+// One chunk of a decompression batch after header parsing (device-side plan).
+struct DChunk {
+  int64_t stage_off;     // offset of this chunk's staging area (sum of previous nbytes)
+  int32_t status;        // >= 0: nbytes; < 0: BLOSC2_ERROR_*
+  int32_t nbytes;
+  int32_t blocksize;
+  int32_t nblocks;
+  int32_t leftover;
+  int32_t nstreams;      // total streams (0 for memcpyed / special chunks)
+  int32_t block_base;    // first block index in the batch block table
+  int32_t stream_base;   // first stream index in the batch stream table
+  uint8_t typesize, flags, version, special;
+  uint8_t overhead, dont_split, nfilters_bwd, has_delta;
+  uint8_t filters[kMaxFilters];
+  uint8_t filters_meta[kMaxFilters];
+  uint8_t fsrc[kMaxFilters];   // per backward slot: buffer the stage reads (0 stage,1 tmp,2 dst)
+  uint8_t fdst[kMaxFilters];   // per backward slot: buffer the stage writes
+  uint8_t codec, pad0, pad1, pad2;
+};
+
+// One LZ/raw/run stream of a decompression batch.
+struct DStream {
+  int64_t src;       // byte offset of the payload inside the chunk (after the csize word)
+  int32_t csize;     // the csize word as written by the encoder
+  int32_t neblock;   // decoded bytes
+  int32_t chunk;
+  int32_t dst_off;   // offset of the decoded bytes inside the chunk's uncompressed image
+};
+
+}  // namespace b2h

@@ -1,0 +1,832 @@
+// blosc2_api.cpp -- the drop-in C ABI (include/blosc2.h) on top of the MI355X batch engine.
+//
+// Host responsibilities only: context state (incl. the reference's sticky context blocksize,
+// blosc/blosc2.c:2414-2416 + stune.c:54-60), environment overrides, header parsing for the
+// inspection API, H<->D staging of caller buffers, and the plugin registry.  Every byte of
+// filter / codec work is done by the HIP kernels in b2h_engine.hip; there is no CPU fallback --
+// without a usable GPU the compute entry points return BLOSC2_ERROR_FAILURE loudly.
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/b2h.h"
+#include "../../include/blosc2.h"
+#include "b2h_engine.h"
+#include "b2h_format.h"
+
+namespace {
+
+bool trace_on() {
+  static int on = -1;
+  if (on < 0) on = getenv("BLOSC_TRACE") != nullptr;
+  return on;
+}
+#define TRACE_ERROR(...)                                                   \
+  do {                                                                     \
+    if (trace_on()) {                                                      \
+      fprintf(stderr, "[error] - ");                                       \
+      fprintf(stderr, __VA_ARGS__);                                        \
+      fprintf(stderr, " (%s:%d)\n", __FILE__, __LINE__);                   \
+    }                                                                      \
+  } while (0)
+
+int32_t rd32(const uint8_t* p) {
+  return (int32_t)((uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24));
+}
+
+// ---------------------------------------------------------------- device staging buffers ----
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t n) {
+    n += 256;
+    if (n <= cap) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, n) != hipSuccess) return false;
+    cap = n;
+    return true;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  uint8_t* u8() const { return static_cast<uint8_t*>(p); }
+};
+
+struct Device {
+  int dev = -1;
+  hipStream_t stream = nullptr;
+  DevBuf in, out, small;
+  bool init() {
+    if (stream) return true;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+      TRACE_ERROR("no HIP device available: the MI355X engine has no CPU fallback");
+      return false;
+    }
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return false;
+    return true;
+  }
+  void release() {
+    in.release();
+    out.release();
+    small.release();
+    if (stream) (void)hipStreamDestroy(stream);
+    stream = nullptr;
+  }
+};
+
+// --------------------------------------------------------------------- plugin registry ----
+std::mutex g_reg_mu;
+std::vector<blosc2_codec> g_codecs;
+std::vector<blosc2_filter> g_filters;
+
+// ------------------------------------------------------------------------ global state ----
+std::mutex g_global_mu;
+bool g_initlib = false;
+int16_t g_nthreads = 1;
+int g_compressor = BLOSC_BLOSCLZ;
+int g_delta = 0;
+int32_t g_force_blocksize = 0;
+int32_t g_splitmode = BLOSC_FORWARD_COMPAT_SPLIT;
+
+}  // namespace
+
+struct blosc2_context_s {
+  int do_compress = 0;
+  // compression parameters (blosc2_cparams)
+  uint8_t compcode = 0, compcode_meta = 0;
+  int clevel = 5;
+  int use_dict = 0;
+  int32_t typesize = 8;
+  int16_t nthreads = 1;
+  int32_t blocksize = 0;     // sticky: overwritten by every compression (see header comment)
+  int32_t splitmode = BLOSC_FORWARD_COMPAT_SPLIT;
+  void* schunk = nullptr;
+  uint8_t filters[6] = {0, 0, 0, 0, 0, BLOSC_SHUFFLE};
+  uint8_t filters_meta[6] = {0};
+  blosc2_prefilter_fn prefilter = nullptr;
+  blosc2_prefilter_params* preparams = nullptr;
+  void* tuner_params = nullptr;
+  int tuner_id = 0;
+  bool instr_codec = false;
+  void* codec_params = nullptr;
+  void* filter_params[6] = {nullptr};
+  // decompression parameters
+  blosc2_dparams dparams = BLOSC2_DPARAMS_DEFAULTS;
+  // block mask for the next decompression (blosc2_set_maskout)
+  std::vector<uint8_t> maskout;
+  // device side
+  Device dev;
+  std::mutex mu;
+};
+
+namespace {
+
+bool env_long(const char* name, long* out) {
+  const char* v = getenv(name);
+  if (!v) return false;
+  errno = 0;
+  long x = strtol(v, nullptr, 10);
+  if (errno == EINVAL) return false;
+  *out = x;
+  return true;
+}
+
+void build_filters(int doshuffle, int delta, int32_t typesize, uint8_t* filters) {
+  // blosc/blosc2.c:3686-3698
+  if (doshuffle == BLOSC_SHUFFLE && typesize > 1) filters[5] = BLOSC_SHUFFLE;
+  if (doshuffle == BLOSC_BITSHUFFLE) filters[5] = BLOSC_BITSHUFFLE;
+  if (doshuffle == BLOSC_NOSHUFFLE) filters[5] = BLOSC_NOSHUFFLE;
+  if (delta) filters[4] = BLOSC_DELTA;
+}
+
+int compname_to_code(const char* name) {
+  if (!name) return -1;
+  if (!strcmp(name, BLOSC_BLOSCLZ_COMPNAME)) return BLOSC_BLOSCLZ;
+  if (!strcmp(name, BLOSC_LZ4_COMPNAME)) return BLOSC_LZ4;
+  if (!strcmp(name, BLOSC_LZ4HC_COMPNAME)) return BLOSC_LZ4HC;
+  if (!strcmp(name, BLOSC_ZLIB_COMPNAME)) return BLOSC_ZLIB;
+  if (!strcmp(name, BLOSC_ZSTD_COMPNAME)) return BLOSC_ZSTD;
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  for (auto& c : g_codecs)
+    if (c.compname && !strcmp(c.compname, name)) return c.compcode;
+  return -1;
+}
+
+// Pipelines the device path executes: built-in filters and BloscLZ.
+int check_supported(const blosc2_context* c) {
+  if (c->compcode != BLOSC_BLOSCLZ) {
+    TRACE_ERROR("codec %d is not implemented by the MI355X engine (BloscLZ only)", c->compcode);
+    return BLOSC2_ERROR_CODEC_SUPPORT;
+  }
+  if (c->use_dict) {
+    TRACE_ERROR("`use_dict` is only supported for ZSTD, LZ4, and LZ4HC codecs.");
+    return BLOSC2_ERROR_CODEC_PARAM;
+  }
+  for (int i = 0; i < 6; i++) {
+    if (c->filters[i] > BLOSC_TRUNC_PREC) {
+      TRACE_ERROR("filter %d runs on host callbacks; not part of the device pipeline", c->filters[i]);
+      return BLOSC2_ERROR_FILTER_PIPELINE;
+    }
+  }
+  if (c->prefilter || c->instr_codec || c->tuner_params || c->tuner_id != 0) {
+    TRACE_ERROR("prefilters / instrumented codecs / tuners are not supported by the device pipeline");
+    return BLOSC2_ERROR_FILTER_PIPELINE;
+  }
+  return 0;
+}
+
+// Compress one host buffer through the engine (n = 1 batch).
+int compress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void* dest, int32_t destsize,
+                  int32_t blocksize_in, bool sticky, bool extended) {
+  if (srcsize < 0) return BLOSC2_ERROR_INVALID_PARAM;
+  b2h::CompressPlan plan;
+  int32_t computed = 0;
+  int rc = b2h::make_compress_plan(&plan, srcsize, destsize, ctx->clevel, ctx->typesize, blocksize_in, ctx->splitmode,
+                                   ctx->filters, ctx->filters_meta, &computed, extended);
+  if (rc < 0) return rc;
+  if (sticky) ctx->blocksize = computed;
+  if ((rc = check_supported(ctx)) < 0) return rc;
+  Device& d = ctx->dev;
+  if (!d.init()) return BLOSC2_ERROR_FAILURE;
+  if (!d.in.ensure((size_t)srcsize) || !d.out.ensure((size_t)destsize) || !d.small.ensure(64)) return BLOSC2_ERROR_MEMORY_ALLOC;
+  if (srcsize && hipMemcpyAsync(d.in.p, src, (size_t)srcsize, hipMemcpyHostToDevice, d.stream) != hipSuccess)
+    return BLOSC2_ERROR_FAILURE;
+  int32_t* d_cb = reinterpret_cast<int32_t*>(d.small.p);
+  rc = b2h::compress_batch(plan, d.in.u8(), 0, 1, d.out.u8(), 0, d_cb, d.stream);
+  if (rc < 0) {
+    TRACE_ERROR("device compression failed: %s", b2h::last_error());
+    return rc;
+  }
+  int32_t cb = 0;
+  if (hipMemcpyAsync(&cb, d_cb, 4, hipMemcpyDeviceToHost, d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+  if (hipStreamSynchronize(d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+  const int32_t ncopy = cb > 0 ? cb : (destsize < plan.overhead ? destsize : plan.overhead);
+  if (hipMemcpy(dest, d.out.p, (size_t)ncopy, hipMemcpyDeviceToHost) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+  return cb;
+}
+
+// Host-side mirror of read_chunk_header's size fields (blosc/blosc2.c:738-777), used for staging.
+int peek_header(const void* src, int32_t srcsize, int32_t* nbytes, int32_t* cbytes, int32_t* blocksize) {
+  if (srcsize < BLOSC_MIN_HEADER_LENGTH) return BLOSC2_ERROR_READ_BUFFER;
+  const uint8_t* s = static_cast<const uint8_t*>(src);
+  *nbytes = rd32(s + 4);
+  *blocksize = rd32(s + 8);
+  *cbytes = rd32(s + 12);
+  if (*cbytes < BLOSC_MIN_HEADER_LENGTH) return BLOSC2_ERROR_INVALID_HEADER;
+  if (*blocksize <= 0 || *blocksize > BLOSC2_MAXBLOCKSIZE || s[3] == 0) return BLOSC2_ERROR_INVALID_HEADER;
+  return 0;
+}
+
+// Decompress one host chunk through the engine.  With a block mask only unmasked blocks are
+// copied back so masked regions of `dest` keep the caller's bytes (blosc/blosc2.c:1734-1737).
+int decompress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void* dest, int32_t destsize,
+                    const std::vector<uint8_t>* mask) {
+  int32_t nbytes, cbytes, bs;
+  int rc = peek_header(src, srcsize, &nbytes, &cbytes, &bs);
+  if (rc < 0) return rc;
+  if (nbytes > destsize) return BLOSC2_ERROR_WRITE_BUFFER;
+  if (cbytes > srcsize) return BLOSC2_ERROR_INVALID_HEADER;
+  if (nbytes > 0 && bs > nbytes) bs = nbytes;
+  const int32_t nblocks = nbytes > 0 ? nbytes / bs + (nbytes % bs ? 1 : 0) : 0;
+  if (mask && (int32_t)mask->size() != nblocks) {
+    TRACE_ERROR("The number of items in block_maskout (%zu) must match the number of blocks in chunk (%d).",
+                mask->size(), nblocks);
+    return BLOSC2_ERROR_DATA;
+  }
+  Device& d = ctx->dev;
+  if (!d.init()) return BLOSC2_ERROR_FAILURE;
+  const size_t mask_bytes = mask ? mask->size() : 0;
+  if (!d.in.ensure((size_t)cbytes) || !d.out.ensure((size_t)(nbytes > 0 ? nbytes : 1)) ||
+      !d.small.ensure(64 + mask_bytes))
+    return BLOSC2_ERROR_MEMORY_ALLOC;
+  struct Ptrs { const uint8_t* s; uint8_t* o; int32_t ss, ds, status, pad; } h;
+  h.s = d.in.u8();
+  h.o = d.out.u8();
+  h.ss = cbytes;
+  h.ds = destsize;
+  uint8_t* sm = d.small.u8();
+  if (hipMemcpyAsync(d.in.p, src, (size_t)cbytes, hipMemcpyHostToDevice, d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+  if (hipMemcpyAsync(sm, &h, sizeof h, hipMemcpyHostToDevice, d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+  const uint8_t* d_mask = nullptr;
+  if (mask) {
+    if (hipMemcpyAsync(sm + 64, mask->data(), mask_bytes, hipMemcpyHostToDevice, d.stream) != hipSuccess)
+      return BLOSC2_ERROR_FAILURE;
+    d_mask = sm + 64;
+  }
+  Ptrs* dp = reinterpret_cast<Ptrs*>(sm);
+  rc = b2h::decompress_batch(reinterpret_cast<const uint8_t* const*>(&dp->s), &dp->ss,
+                             reinterpret_cast<uint8_t* const*>(&dp->o), &dp->ds, 1, nbytes, &dp->status, d_mask,
+                             d.stream);
+  if (rc < 0) {
+    TRACE_ERROR("device decompression failed: %s", b2h::last_error());
+    return rc;
+  }
+  int32_t status = 0;
+  if (hipMemcpyAsync(&status, &dp->status, 4, hipMemcpyDeviceToHost, d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+  if (hipStreamSynchronize(d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+  if (status <= 0) return status;
+  if (!mask) {
+    if (hipMemcpy(dest, d.out.p, (size_t)status, hipMemcpyDeviceToHost) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+  } else {
+    for (int32_t b = 0; b < nblocks; b++) {
+      if ((*mask)[b]) continue;
+      const int64_t off = (int64_t)b * bs;
+      const int64_t len = std::min<int64_t>(bs, nbytes - off);
+      if (hipMemcpy(static_cast<uint8_t*>(dest) + off, d.out.u8() + off, (size_t)len, hipMemcpyDeviceToHost) != hipSuccess)
+        return BLOSC2_ERROR_FAILURE;
+    }
+  }
+  return status;
+}
+
+blosc2_context* g_global_cctx = nullptr;
+blosc2_context* g_global_dctx = nullptr;
+
+}  // namespace
+
+extern "C" {
+
+void blosc2_init(void) {
+  std::lock_guard<std::mutex> g(g_global_mu);
+  if (g_initlib) return;
+  g_initlib = true;
+}
+
+void blosc2_destroy(void) {
+  std::lock_guard<std::mutex> g(g_global_mu);
+  if (g_global_cctx) { g_global_cctx->dev.release(); delete g_global_cctx; g_global_cctx = nullptr; }
+  if (g_global_dctx) { g_global_dctx->dev.release(); delete g_global_dctx; g_global_dctx = nullptr; }
+  g_initlib = false;
+}
+
+const char* blosc2_get_version_string(void) { return BLOSC2_VERSION_STRING; }
+
+// blosc/blosc2.c:6040-6251 (validation + environment overrides)
+blosc2_context* blosc2_create_cctx(blosc2_cparams cparams) {
+  blosc2_context* c = new blosc2_context_s();
+  c->do_compress = 1;
+  c->use_dict = cparams.use_dict;
+  c->instr_codec = cparams.instr_codec;
+  for (int i = 0; i < 6; i++) {
+    c->filters[i] = cparams.filters[i];
+    c->filters_meta[i] = cparams.filters_meta[i];
+    const uint8_t f = c->filters[i];
+    if ((f >= BLOSC_LAST_FILTER && f <= BLOSC2_DEFINED_FILTERS_STOP) ||
+        (f > BLOSC_LAST_REGISTERED_FILTER && f <= BLOSC2_GLOBAL_REGISTERED_FILTERS_STOP)) {
+      TRACE_ERROR("filter (%d) is not yet defined", f);
+      delete c;
+      return nullptr;
+    }
+  }
+  int doshuffle = -1, dodelta = BLOSC_NOFILTER;
+  if (const char* v = getenv("BLOSC_SHUFFLE")) {
+    if (!strcmp(v, "NOSHUFFLE")) doshuffle = BLOSC_NOSHUFFLE;
+    else if (!strcmp(v, "SHUFFLE")) doshuffle = BLOSC_SHUFFLE;
+    else if (!strcmp(v, "BITSHUFFLE")) doshuffle = BLOSC_BITSHUFFLE;
+  }
+  if (const char* v = getenv("BLOSC_DELTA")) {
+    if (!strcmp(v, "1")) dodelta = BLOSC_DELTA;
+    else if (!strcmp(v, "0")) dodelta = BLOSC_NOFILTER;
+  }
+  long x;
+  c->typesize = cparams.typesize;
+  if (env_long("BLOSC_TYPESIZE", &x) && x > 0) c->typesize = (int32_t)x;
+  build_filters(doshuffle, dodelta, c->typesize, c->filters);
+  c->clevel = cparams.clevel;
+  if (env_long("BLOSC_CLEVEL", &x) && x >= 0) c->clevel = (int)x;
+  c->compcode = cparams.compcode;
+  if (const char* v = getenv("BLOSC_COMPRESSOR")) {
+    const int code = compname_to_code(v);
+    if (code >= BLOSC_LAST_CODEC) {
+      TRACE_ERROR("User defined codecs cannot be set here. Use Blosc2 mechanism instead.");
+      delete c;
+      return nullptr;
+    }
+    c->compcode = (uint8_t)code;
+  }
+  c->compcode_meta = cparams.compcode_meta;
+  c->blocksize = cparams.blocksize;
+  if (env_long("BLOSC_BLOCKSIZE", &x) && x > 0) c->blocksize = (int32_t)x;
+  c->nthreads = cparams.nthreads;
+  if (env_long("BLOSC_NTHREADS", &x) && x > 0) c->nthreads = (int16_t)x;
+  c->splitmode = cparams.splitmode;
+  if (const char* v = getenv("BLOSC_SPLITMODE")) {
+    if (!strcmp(v, "ALWAYS")) c->splitmode = BLOSC_ALWAYS_SPLIT;
+    else if (!strcmp(v, "NEVER")) c->splitmode = BLOSC_NEVER_SPLIT;
+    else if (!strcmp(v, "AUTO")) c->splitmode = BLOSC_AUTO_SPLIT;
+    else if (!strcmp(v, "FORWARD_COMPAT")) c->splitmode = BLOSC_FORWARD_COMPAT_SPLIT;
+  }
+  c->schunk = cparams.schunk;
+  c->prefilter = cparams.prefilter;
+  c->preparams = cparams.preparams;
+  c->tuner_params = cparams.tuner_params;
+  c->tuner_id = cparams.tuner_id;
+  c->codec_params = cparams.codec_params;
+  for (int i = 0; i < 6; i++) c->filter_params[i] = cparams.filter_params[i];
+  return c;
+}
+
+blosc2_context* blosc2_create_dctx(blosc2_dparams dparams) {
+  blosc2_context* c = new blosc2_context_s();
+  c->do_compress = 0;
+  c->dparams = dparams;
+  c->nthreads = dparams.nthreads;
+  long x;
+  if (env_long("BLOSC_NTHREADS", &x) && x > 0) c->nthreads = (int16_t)x;
+  c->schunk = dparams.schunk;
+  return c;
+}
+
+void blosc2_free_ctx(blosc2_context* context) {
+  if (!context) return;
+  context->dev.release();
+  delete context;
+}
+
+int blosc2_ctx_get_cparams(blosc2_context* ctx, blosc2_cparams* cparams) {
+  if (!ctx || !cparams) return BLOSC2_ERROR_NULL_POINTER;
+  *cparams = BLOSC2_CPARAMS_DEFAULTS;
+  cparams->compcode = ctx->compcode;
+  cparams->compcode_meta = ctx->compcode_meta;
+  cparams->clevel = (uint8_t)ctx->clevel;
+  cparams->use_dict = ctx->use_dict;
+  cparams->instr_codec = ctx->instr_codec;
+  cparams->typesize = ctx->typesize;
+  cparams->nthreads = ctx->nthreads;
+  cparams->blocksize = ctx->blocksize;
+  cparams->splitmode = ctx->splitmode;
+  cparams->schunk = ctx->schunk;
+  for (int i = 0; i < 6; i++) {
+    cparams->filters[i] = ctx->filters[i];
+    cparams->filters_meta[i] = ctx->filters_meta[i];
+    cparams->filter_params[i] = ctx->filter_params[i];
+  }
+  cparams->prefilter = ctx->prefilter;
+  cparams->preparams = ctx->preparams;
+  cparams->tuner_id = ctx->tuner_id;
+  cparams->tuner_params = ctx->tuner_params;
+  cparams->codec_params = ctx->codec_params;
+  return BLOSC2_ERROR_SUCCESS;
+}
+
+int blosc2_ctx_get_dparams(blosc2_context* ctx, blosc2_dparams* dparams) {
+  if (!ctx || !dparams) return BLOSC2_ERROR_NULL_POINTER;
+  *dparams = ctx->dparams;
+  dparams->nthreads = ctx->nthreads;
+  dparams->schunk = ctx->schunk;
+  return BLOSC2_ERROR_SUCCESS;
+}
+
+int blosc2_set_maskout(blosc2_context* ctx, bool* maskout, int nblocks) {
+  if (!ctx) return BLOSC2_ERROR_NULL_POINTER;
+  ctx->maskout.assign(maskout, maskout + nblocks);
+  return 0;
+}
+
+// blosc/blosc2.c:3121-3148
+int blosc2_compress_ctx(blosc2_context* context, const void* src, int32_t srcsize, void* dest, int32_t destsize) {
+  if (!context) return BLOSC2_ERROR_NULL_POINTER;
+  if (context->do_compress != 1) {
+    TRACE_ERROR("Context is not meant for compression.  Giving up.");
+    return BLOSC2_ERROR_INVALID_PARAM;
+  }
+  std::lock_guard<std::mutex> g(context->mu);
+  return compress_host(context, src, srcsize, dest, destsize, context->blocksize, true, true);
+}
+
+// blosc/blosc2.c:3943-3962
+int blosc2_decompress_ctx(blosc2_context* context, const void* src, int32_t srcsize, void* dest, int32_t destsize) {
+  if (!context) return BLOSC2_ERROR_NULL_POINTER;
+  if (context->do_compress != 0) {
+    TRACE_ERROR("Context is not meant for decompression.  Giving up.");
+    return BLOSC2_ERROR_INVALID_PARAM;
+  }
+  std::lock_guard<std::mutex> g(context->mu);
+  std::vector<uint8_t> mask;
+  const bool has_mask = !context->maskout.empty();
+  if (has_mask) mask.swap(context->maskout);   // a mask applies to one call (blosc2.c:3954-3959)
+  return decompress_host(context, src, srcsize, dest, destsize, has_mask ? &mask : nullptr);
+}
+
+// blosc/blosc2.c:4265-4474 / 4541-4550: decode only the blocks overlapping [start, start+nitems)
+int blosc2_getitem_ctx(blosc2_context* context, const void* src, int32_t srcsize, int start, int nitems, void* dest,
+                       int32_t destsize) {
+  if (!context) return BLOSC2_ERROR_NULL_POINTER;
+  int32_t nbytes, cbytes, bs;
+  int rc = peek_header(src, srcsize, &nbytes, &cbytes, &bs);
+  if (rc < 0) return rc;
+  const uint8_t* s = static_cast<const uint8_t*>(src);
+  const int64_t ts = s[3];
+  if ((s[2] & BLOSC_DOSHUFFLE) && (s[2] & BLOSC_DOBITSHUFFLE) && srcsize >= 32 && (s[30] & BLOSC2_VL_BLOCKS)) {
+    TRACE_ERROR("getitem is not supported for VL-block chunks.");
+    return BLOSC2_ERROR_INVALID_PARAM;
+  }
+  if (nitems == 0) return 0;
+  if (nitems < 0) return BLOSC2_ERROR_INVALID_PARAM;
+  const int64_t nib = (int64_t)nitems * ts;
+  if (nib > INT32_MAX || nib > destsize) return BLOSC2_ERROR_WRITE_BUFFER;
+  const int64_t sb = (int64_t)start * ts;
+  if (start < 0 || sb > nbytes) return BLOSC2_ERROR_INVALID_PARAM;
+  const int64_t stop = (int64_t)start + nitems;
+  if (stop > INT32_MAX || stop * ts > nbytes) return BLOSC2_ERROR_INVALID_PARAM;
+  if (nbytes > 0 && bs > nbytes) bs = nbytes;
+  const int32_t nblocks = nbytes > 0 ? nbytes / bs + (nbytes % bs ? 1 : 0) : 0;
+  std::vector<uint8_t> mask((size_t)nblocks, 1);
+  const bool delta = (s[2] & BLOSC_DODELTA) != 0;
+  for (int32_t b = 0; b < nblocks; b++) {
+    const int64_t lo = (int64_t)b * bs, hi = lo + bs;
+    if (hi > sb && lo < stop * ts) mask[b] = 0;
+  }
+  if (delta && nblocks) mask[0] = 0;   // later blocks XOR against decoded block 0
+  std::vector<uint8_t> full((size_t)std::max(nbytes, 1));
+  std::lock_guard<std::mutex> g(context->mu);
+  rc = decompress_host(context, src, srcsize, full.data(), nbytes, &mask);
+  if (rc < 0) return rc;
+  memcpy(dest, full.data() + sb, (size_t)nib);
+  return (int)nib;
+}
+
+int blosc2_getitem(const void* src, int32_t srcsize, int start, int nitems, void* dest, int32_t destsize) {
+  blosc2_context* c = blosc2_create_dctx(BLOSC2_DPARAMS_DEFAULTS);
+  const int r = blosc2_getitem_ctx(c, src, srcsize, start, nitems, dest, destsize);
+  blosc2_free_ctx(c);
+  return r;
+}
+
+int blosc1_getitem(const void* src, int start, int nitems, void* dest) {
+  return blosc2_getitem(src, INT32_MAX, start, nitems, dest, INT32_MAX);
+}
+
+// blosc/blosc2.c:3701-3897 (environment overrides, global context)
+int blosc2_compress(int clevel, int doshuffle, int32_t typesize, const void* src, int32_t srcsize, void* dest,
+                    int32_t destsize) {
+  if (!g_initlib) blosc2_init();
+  long x;
+  if (env_long("BLOSC_CLEVEL", &x) && x >= 0) clevel = (int)x;
+  if (const char* v = getenv("BLOSC_SHUFFLE")) {
+    if (!strcmp(v, "NOSHUFFLE")) doshuffle = BLOSC_NOSHUFFLE;
+    else if (!strcmp(v, "SHUFFLE")) doshuffle = BLOSC_SHUFFLE;
+    else if (!strcmp(v, "BITSHUFFLE")) doshuffle = BLOSC_BITSHUFFLE;
+  }
+  if (const char* v = getenv("BLOSC_DELTA")) {
+    if (!strcmp(v, "1")) blosc2_set_delta(1);
+    else if (!strcmp(v, "0")) blosc2_set_delta(0);
+  }
+  if (env_long("BLOSC_TYPESIZE", &x) && x > 0) typesize = (int32_t)x;
+  if (const char* v = getenv("BLOSC_COMPRESSOR")) (void)blosc1_set_compressor(v);
+  if (env_long("BLOSC_BLOCKSIZE", &x) && x > 0) blosc1_set_blocksize((size_t)x);
+  if (env_long("BLOSC_NTHREADS", &x) && x > 0) (void)blosc2_set_nthreads((int16_t)x);
+  if (const char* v = getenv("BLOSC_SPLITMODE")) {
+    int sm = -1;
+    if (!strcmp(v, "ALWAYS")) sm = BLOSC_ALWAYS_SPLIT;
+    else if (!strcmp(v, "NEVER")) sm = BLOSC_NEVER_SPLIT;
+    else if (!strcmp(v, "AUTO")) sm = BLOSC_AUTO_SPLIT;
+    else if (!strcmp(v, "FORWARD_COMPAT")) sm = BLOSC_FORWARD_COMPAT_SPLIT;
+    if (sm >= 0) blosc1_set_splitmode(sm);
+  }
+  std::lock_guard<std::mutex> g(g_global_mu);
+  if (!g_global_cctx) {
+    g_global_cctx = new blosc2_context_s();
+    g_global_cctx->do_compress = 1;
+  }
+  blosc2_context* c = g_global_cctx;
+  memset(c->filters, 0, 6);
+  memset(c->filters_meta, 0, 6);
+  build_filters(doshuffle, g_delta, typesize, c->filters);
+  c->clevel = clevel;
+  c->typesize = typesize;
+  c->compcode = (uint8_t)g_compressor;
+  c->splitmode = g_splitmode;
+  c->nthreads = g_nthreads;
+  const bool blosc1_compat = getenv("BLOSC_BLOSC1_COMPAT") != nullptr && getenv("BLOSC_NOLOCK") == nullptr;
+  // the global path passes g_force_blocksize every call (no sticky blocksize)
+  return compress_host(c, src, srcsize, dest, destsize, g_force_blocksize, false, !blosc1_compat);
+}
+
+int blosc2_decompress(const void* src, int32_t srcsize, void* dest, int32_t destsize) {
+  if (!g_initlib) blosc2_init();
+  std::lock_guard<std::mutex> g(g_global_mu);
+  if (!g_global_dctx) g_global_dctx = new blosc2_context_s();
+  return decompress_host(g_global_dctx, src, srcsize, dest, destsize, nullptr);
+}
+
+int blosc1_compress(int clevel, int doshuffle, size_t typesize, size_t nbytes, const void* src, void* dest,
+                    size_t destsize) {
+  return blosc2_compress(clevel, doshuffle, (int32_t)typesize, src, (int32_t)nbytes, dest, (int32_t)destsize);
+}
+
+int blosc1_decompress(const void* src, void* dest, size_t destsize) {
+  return blosc2_decompress(src, INT32_MAX, dest, (int32_t)destsize);
+}
+
+int16_t blosc2_get_nthreads(void) { return g_nthreads; }
+int16_t blosc2_set_nthreads(int16_t nthreads) {
+  const int16_t old = g_nthreads;
+  if (nthreads <= 0) return BLOSC2_ERROR_INVALID_PARAM;
+  g_nthreads = nthreads;   // only recorded: the device path has no host worker pool
+  return old;
+}
+
+const char* blosc1_get_compressor(void) {
+  const char* name = nullptr;
+  blosc2_compcode_to_compname(g_compressor, &name);
+  return name;
+}
+
+int blosc1_set_compressor(const char* compname) {
+  const int code = compname_to_code(compname);
+  if (code >= BLOSC_LAST_CODEC) {
+    TRACE_ERROR("User defined codecs cannot be set here. Use Blosc2 mechanism instead.");
+    return BLOSC2_ERROR_CODEC_SUPPORT;
+  }
+  if (code >= 0) g_compressor = code;
+  if (!g_initlib) blosc2_init();
+  return code;
+}
+
+void blosc2_set_delta(int dodelta) { g_delta = dodelta; }
+int blosc1_get_blocksize(void) { return g_force_blocksize; }
+void blosc1_set_blocksize(size_t blocksize) { g_force_blocksize = (int32_t)blocksize; }
+void blosc1_set_splitmode(int splitmode) { g_splitmode = splitmode; }
+
+int blosc2_compcode_to_compname(int compcode, const char** compname) {
+  const char* name = nullptr;
+  switch (compcode) {
+    case BLOSC_BLOSCLZ: name = BLOSC_BLOSCLZ_COMPNAME; break;
+    case BLOSC_LZ4: name = BLOSC_LZ4_COMPNAME; break;
+    case BLOSC_LZ4HC: name = BLOSC_LZ4HC_COMPNAME; break;
+    case BLOSC_ZLIB: name = BLOSC_ZLIB_COMPNAME; break;
+    case BLOSC_ZSTD: name = BLOSC_ZSTD_COMPNAME; break;
+    default: {
+      std::lock_guard<std::mutex> g(g_reg_mu);
+      for (auto& c : g_codecs)
+        if (c.compcode == compcode) name = c.compname;
+    }
+  }
+  *compname = name;
+  if (compcode == BLOSC_BLOSCLZ) return compcode;
+  // other built-in codecs exist in the format but are not implemented by this engine
+  return name ? (compcode < BLOSC_LAST_CODEC ? -1 : compcode) : -1;
+}
+
+int blosc2_compname_to_compcode(const char* compname) { return compname_to_code(compname); }
+
+const char* blosc2_list_compressors(void) { return BLOSC_BLOSCLZ_COMPNAME; }
+
+int blosc2_get_complib_info(const char* compname, char** complib, char** version) {
+  const int code = compname_to_code(compname);
+  if (code != BLOSC_BLOSCLZ) {
+    if (complib) *complib = nullptr;
+    if (version) *version = nullptr;
+    return -1;
+  }
+  if (complib) *complib = strdup(BLOSC_BLOSCLZ_LIBNAME);
+  if (version) *version = strdup("2.5.3");
+  return BLOSC_BLOSCLZ_LIB;
+}
+
+// blosc/blosc2.c:4702-4760 (cbuffer inspection)
+int blosc2_cbuffer_sizes(const void* cbuffer, int32_t* nbytes, int32_t* cbytes, int32_t* blocksize) {
+  const uint8_t* s = static_cast<const uint8_t*>(cbuffer);
+  int32_t nb = rd32(s + 4), bs = rd32(s + 8), cb = rd32(s + 12);
+  if (cb < BLOSC_MIN_HEADER_LENGTH || bs <= 0 || bs > BLOSC2_MAXBLOCKSIZE || s[3] == 0) {
+    if (nbytes) *nbytes = 0;
+    if (cbytes) *cbytes = 0;
+    if (blocksize) *blocksize = 0;
+    return BLOSC2_ERROR_INVALID_HEADER;
+  }
+  if (nb > 0 && bs > nb) bs = nb;
+  if (nbytes) *nbytes = nb;
+  if (cbytes) *cbytes = cb;
+  if (blocksize) *blocksize = bs;
+  return 0;
+}
+
+void blosc1_cbuffer_sizes(const void* cbuffer, size_t* nbytes, size_t* cbytes, size_t* blocksize) {
+  int32_t nb = 0, cb = 0, bs = 0;
+  blosc2_cbuffer_sizes(cbuffer, &nb, &cb, &bs);
+  if (nbytes) *nbytes = (size_t)nb;
+  if (cbytes) *cbytes = (size_t)cb;
+  if (blocksize) *blocksize = (size_t)bs;
+}
+
+int blosc1_cbuffer_validate(const void* cbuffer, size_t cbytes, size_t* nbytes) {
+  int32_t header_cbytes, nb, bs;
+  if (cbytes < BLOSC_MIN_HEADER_LENGTH) { *nbytes = 0; return BLOSC2_ERROR_WRITE_BUFFER; }
+  int rc = blosc2_cbuffer_sizes(cbuffer, &nb, &header_cbytes, &bs);
+  if (rc < 0) { *nbytes = 0; return rc; }
+  *nbytes = (size_t)nb;
+  if ((size_t)header_cbytes != cbytes) return BLOSC2_ERROR_INVALID_HEADER;
+  if (nb > BLOSC2_MAX_BUFFERSIZE) return BLOSC2_ERROR_MEMORY_ALLOC;
+  return 0;
+}
+
+void blosc1_cbuffer_metainfo(const void* cbuffer, size_t* typesize, int* flags) {
+  const uint8_t* s = static_cast<const uint8_t*>(cbuffer);
+  if (typesize) *typesize = s[3];
+  if (flags) *flags = s[2];
+}
+
+void blosc2_cbuffer_versions(const void* cbuffer, int* version, int* versionlz) {
+  const uint8_t* s = static_cast<const uint8_t*>(cbuffer);
+  if (version) *version = s[0];
+  if (versionlz) *versionlz = s[1];
+}
+
+const char* blosc2_cbuffer_complib(const void* cbuffer) {
+  const uint8_t* s = static_cast<const uint8_t*>(cbuffer);
+  switch (s[2] >> 5) {
+    case BLOSC_BLOSCLZ_FORMAT: return BLOSC_BLOSCLZ_LIBNAME;
+    case BLOSC_LZ4_FORMAT: return BLOSC_LZ4_LIBNAME;
+    case BLOSC_ZLIB_FORMAT: return BLOSC_ZLIB_LIBNAME;
+    case BLOSC_ZSTD_FORMAT: return BLOSC_ZSTD_LIBNAME;
+    case BLOSC_UDCODEC_FORMAT: return "User-defined";
+    default: return "Unknown";
+  }
+}
+
+// blosc/blosc2.c:6692-6737 (register_codec_private + blosc2_register_codec)
+int blosc2_register_codec(blosc2_codec* codec) {
+  if (!codec) return BLOSC2_ERROR_NULL_POINTER;
+  if (codec->compcode < BLOSC2_USER_REGISTERED_CODECS_START) {
+    TRACE_ERROR("The id must be greater or equal to %d", BLOSC2_USER_REGISTERED_CODECS_START);
+    return BLOSC2_ERROR_FAILURE;
+  }
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  if (g_codecs.size() >= 256) return BLOSC2_ERROR_CODEC_SUPPORT;
+  for (auto& c : g_codecs)
+    if (c.compcode == codec->compcode) {
+      if (c.compname && codec->compname && !strcmp(c.compname, codec->compname)) return 0;
+      TRACE_ERROR("The codec is already registered!");
+      return BLOSC2_ERROR_CODEC_PARAM;
+    }
+  g_codecs.push_back(*codec);
+  return 0;
+}
+
+// blosc/blosc2.c:6642-6687 (register_filter_private + blosc2_register_filter)
+int blosc2_register_filter(blosc2_filter* filter) {
+  if (!filter) return BLOSC2_ERROR_NULL_POINTER;
+  if (filter->id < BLOSC2_USER_REGISTERED_FILTERS_START) {
+    TRACE_ERROR("The id must be greater or equal to %d", BLOSC2_USER_REGISTERED_FILTERS_START);
+    return BLOSC2_ERROR_FAILURE;
+  }
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  if (g_filters.size() >= 256) return BLOSC2_ERROR_CODEC_SUPPORT;
+  for (auto& f : g_filters)
+    if (f.id == filter->id) {
+      if (f.name && filter->name && !strcmp(f.name, filter->name)) return 0;
+      TRACE_ERROR("The filter is already registered!");
+      return BLOSC2_ERROR_FAILURE;
+    }
+  g_filters.push_back(*filter);
+  return 0;
+}
+
+// ------------------------------------------------------------------- raw filter API ----
+static int32_t raw_filter(int kind, int32_t typesize, int32_t blocksize, const void* src, void* dest) {
+  if (typesize < 1 || typesize > 256 || blocksize < 0) return BLOSC2_ERROR_INVALID_PARAM;
+  if (blocksize == 0) return 0;
+  static blosc2_context* ctx = nullptr;
+  static std::mutex m;
+  std::lock_guard<std::mutex> g(m);
+  if (!ctx) ctx = new blosc2_context_s();
+  Device& d = ctx->dev;
+  if (!d.init()) return BLOSC2_ERROR_FAILURE;
+  if (!d.in.ensure((size_t)blocksize) || !d.out.ensure((size_t)blocksize)) return BLOSC2_ERROR_MEMORY_ALLOC;
+  if (hipMemcpyAsync(d.in.p, src, (size_t)blocksize, hipMemcpyHostToDevice, d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+  int rc;
+  switch (kind) {
+    case 0: rc = b2h::shuffle_dev(typesize, blocksize, d.in.u8(), d.out.u8(), false, d.stream); break;
+    case 1: rc = b2h::shuffle_dev(typesize, blocksize, d.in.u8(), d.out.u8(), true, d.stream); break;
+    case 2: rc = b2h::bitshuffle_dev(typesize, blocksize, d.in.u8(), d.out.u8(), false, 0, d.stream); break;
+    default: rc = b2h::bitshuffle_dev(typesize, blocksize, d.in.u8(), d.out.u8(), true, BLOSC2_VERSION_FORMAT, d.stream); break;
+  }
+  if (rc < 0) return rc;
+  if (hipMemcpyAsync(dest, d.out.p, (size_t)blocksize, hipMemcpyDeviceToHost, d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+  if (hipStreamSynchronize(d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+  return blocksize;
+}
+
+int32_t blosc2_shuffle(int32_t typesize, int32_t blocksize, const void* src, void* dest) {
+  return raw_filter(0, typesize, blocksize, src, dest);
+}
+int32_t blosc2_unshuffle(int32_t typesize, int32_t blocksize, const void* src, void* dest) {
+  return raw_filter(1, typesize, blocksize, src, dest);
+}
+int32_t blosc2_bitshuffle(int32_t typesize, int32_t blocksize, const void* src, void* dest) {
+  return raw_filter(2, typesize, blocksize, src, dest);
+}
+int32_t blosc2_bitunshuffle(int32_t typesize, int32_t blocksize, const void* src, void* dest) {
+  return raw_filter(3, typesize, blocksize, src, dest);
+}
+
+// ------------------------------------------------------------------ b2h batch C-ABI ----
+int b2h_compress_batch(const blosc2_cparams* cp, const void* d_src, int32_t chunk_nbytes, int32_t nchunks,
+                       int64_t src_stride, void* d_dst, int64_t dst_stride, int32_t dst_capacity, int32_t* d_cbytes,
+                       void* stream) {
+  if (!cp) return BLOSC2_ERROR_NULL_POINTER;
+  blosc2_context tmp;
+  tmp.compcode = cp->compcode;
+  tmp.use_dict = cp->use_dict;
+  tmp.filters[5] = 0;
+  for (int i = 0; i < 6; i++) { tmp.filters[i] = cp->filters[i]; tmp.filters_meta[i] = cp->filters_meta[i]; }
+  tmp.prefilter = cp->prefilter;
+  tmp.instr_codec = cp->instr_codec;
+  tmp.tuner_params = cp->tuner_params;
+  tmp.tuner_id = cp->tuner_id;
+  int rc = check_supported(&tmp);
+  if (rc < 0) return rc;
+  b2h::CompressPlan plan;
+  int32_t computed = 0;
+  rc = b2h::make_compress_plan(&plan, chunk_nbytes, dst_capacity, cp->clevel, cp->typesize, cp->blocksize,
+                               cp->splitmode, cp->filters, cp->filters_meta, &computed, true);
+  if (rc < 0) return rc;
+  return b2h::compress_batch(plan, static_cast<const uint8_t*>(d_src), src_stride, nchunks,
+                             static_cast<uint8_t*>(d_dst), dst_stride, d_cbytes, static_cast<hipStream_t>(stream));
+}
+
+int b2h_decompress_batch(const void* d_src, int64_t src_stride, const int32_t* d_cbytes, int32_t nchunks, void* d_dst,
+                         int64_t dst_stride, int32_t dst_capacity, int32_t* d_status, void* stream) {
+  return b2h::decompress_batch_strided(static_cast<const uint8_t*>(d_src), src_stride, d_cbytes, nchunks,
+                                       static_cast<uint8_t*>(d_dst), dst_stride, dst_capacity, d_status,
+                                       static_cast<hipStream_t>(stream));
+}
+
+int b2h_decompress_ptrs(const void* const* d_srcs, const int32_t* d_srcsizes, void* const* d_dsts,
+                        const int32_t* d_dstsizes, int32_t n, int64_t dst_bound, int32_t* d_status, void* stream) {
+  return b2h::decompress_batch(reinterpret_cast<const uint8_t* const*>(d_srcs), d_srcsizes,
+                               reinterpret_cast<uint8_t* const*>(d_dsts), d_dstsizes, n, dst_bound, d_status, nullptr,
+                               static_cast<hipStream_t>(stream));
+}
+
+int32_t b2h_shuffle(int32_t typesize, int32_t nbytes, const void* d_src, void* d_dst, int inverse, void* stream) {
+  return b2h::shuffle_dev(typesize, nbytes, static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst),
+                          inverse != 0, static_cast<hipStream_t>(stream));
+}
+
+int32_t b2h_bitshuffle(int32_t typesize, int32_t nbytes, const void* d_src, void* d_dst, int inverse, void* stream) {
+  return b2h::bitshuffle_dev(typesize, nbytes, static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst),
+                             inverse != 0, BLOSC2_VERSION_FORMAT, static_cast<hipStream_t>(stream));
+}
+
+void b2h_enable_timing(int on) { b2h::enable_timing(on != 0); }
+void b2h_last_times(float out[5]) {
+  const b2h::KernelTimes t = b2h::last_times();
+  out[0] = t.filter_ms; out[1] = t.encode_ms; out[2] = t.finalize_ms; out[3] = t.decode_ms; out[4] = t.unfilter_ms;
+}
+const char* b2h_last_error(void) { return b2h::last_error(); }
+int b2h_device_count(void) { return b2h::device_count(); }
+
+}  // extern "C"

@@ -1,0 +1,400 @@
+/*
+ * blosc2.h -- drop-in C ABI of the MI355X-native Blosc2 chunk engine (libblosc2.so from
+ * c-blosc2_amd/).  Binary compatible with the c-blosc2 3.3.3 entry points listed here: same
+ * names, same struct layouts, same argument meaning, same return / error conventions.  Each
+ * declaration cites the reference declaration it replaces (c-blosc2 include/blosc2.h:line).
+ *
+ * What runs where: every built-in filter (SHUFFLE, BITSHUFFLE, DELTA, TRUNC_PREC) and the BloscLZ
+ * codec execute as HIP kernels on the GPU; host code only parses/writes headers, stages buffers
+ * and keeps context state.  Chunks needing another codec (LZ4, ZLIB, ZSTD, user codecs) or user
+ * filters / pre- / postfilters return BLOSC2_ERROR_CODEC_SUPPORT / BLOSC2_ERROR_FILTER_PIPELINE
+ * ("Out of scope").
+ */
+#ifndef BLOSC2_AMD_BLOSC2_H
+#define BLOSC2_AMD_BLOSC2_H
+
+#include <limits.h>
+#include <stdbool.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BLOSC_EXPORT __attribute__((visibility("default")))
+
+/* ---- version (include/blosc2.h:84-89) ---- */
+#define BLOSC2_VERSION_MAJOR 3
+#define BLOSC2_VERSION_MINOR 3
+#define BLOSC2_VERSION_RELEASE 3
+#define BLOSC2_VERSION_STRING "3.3.3.dev"
+#define BLOSC2_VERSION_DATE "$Date:: 2026-08-06 #$"
+
+/* ---- format constants (include/blosc2.h:128-196) ---- */
+enum {
+  BLOSC1_VERSION_FORMAT_PRE1 = 1,
+  BLOSC1_VERSION_FORMAT = 2,
+  BLOSC2_VERSION_FORMAT_ALPHA = 3,
+  BLOSC2_VERSION_FORMAT_BETA1 = 4,
+  BLOSC2_VERSION_FORMAT_STABLE = 5,
+  BLOSC2_VERSION_FORMAT_VL_BLOCKS = 6,
+  BLOSC2_VERSION_FORMAT = BLOSC2_VERSION_FORMAT_VL_BLOCKS,
+};
+
+enum {
+  BLOSC_MIN_HEADER_LENGTH = 16,
+  BLOSC_EXTENDED_HEADER_LENGTH = 32,
+  BLOSC2_MAX_OVERHEAD = BLOSC_EXTENDED_HEADER_LENGTH,
+  BLOSC2_MAX_BUFFERSIZE = (INT_MAX - BLOSC2_MAX_OVERHEAD),
+  BLOSC_MAX_TYPESIZE = UINT8_MAX,
+  BLOSC_MIN_BUFFERSIZE = 32,
+};
+#define BLOSC_MAX_OVERHEAD BLOSC2_MAX_OVERHEAD
+#define BLOSC_MAX_BUFFERSIZE BLOSC2_MAX_BUFFERSIZE
+
+/* filters (include/blosc2.h:221-264) */
+enum {
+  BLOSC2_DEFINED_FILTERS_START = 0,
+  BLOSC2_DEFINED_FILTERS_STOP = 31,
+  BLOSC2_GLOBAL_REGISTERED_FILTERS_START = 32,
+  BLOSC2_GLOBAL_REGISTERED_FILTERS_STOP = 159,
+  BLOSC2_GLOBAL_REGISTERED_FILTERS = 5,
+  BLOSC2_USER_REGISTERED_FILTERS_START = 160,
+  BLOSC2_USER_REGISTERED_FILTERS_STOP = 255,
+  BLOSC2_MAX_FILTERS = 6,
+  BLOSC2_MAX_UDFILTERS = 16,
+};
+enum {
+  BLOSC_NOSHUFFLE = 0,
+  BLOSC_NOFILTER = 0,
+  BLOSC_SHUFFLE = 1,
+  BLOSC_BITSHUFFLE = 2,
+  BLOSC_DELTA = 3,
+  BLOSC_TRUNC_PREC = 4,
+  BLOSC_LAST_FILTER = 5,
+  BLOSC_LAST_REGISTERED_FILTER = BLOSC2_GLOBAL_REGISTERED_FILTERS_START + BLOSC2_GLOBAL_REGISTERED_FILTERS - 1,
+};
+
+/* header flags (include/blosc2.h:270-295) */
+enum {
+  BLOSC_DOSHUFFLE = 0x1,
+  BLOSC_MEMCPYED = 0x2,
+  BLOSC_DOBITSHUFFLE = 0x4,
+  BLOSC_DODELTA = 0x8,
+};
+enum {
+  BLOSC2_USEDICT = 0x1,
+  BLOSC2_BIGENDIAN = 0x2,
+  BLOSC2_INSTR_CODEC = 0x80,
+};
+enum {
+  BLOSC2_VL_BLOCKS = 0x1,
+};
+enum {
+  BLOSC2_MAXDICTSIZE = 128 * 1024,
+  BLOSC2_MINUSEFULDICT = 256,
+  BLOSC2_MAXBLOCKSIZE = 536866816,
+  BLOSC2_MAXTYPESIZE = BLOSC2_MAXBLOCKSIZE,
+};
+
+/* codecs (include/blosc2.h:306-400) */
+enum {
+  BLOSC2_DEFINED_CODECS_START = 0,
+  BLOSC2_DEFINED_CODECS_STOP = 31,
+  BLOSC2_GLOBAL_REGISTERED_CODECS_START = 32,
+  BLOSC2_GLOBAL_REGISTERED_CODECS_STOP = 159,
+  BLOSC2_GLOBAL_REGISTERED_CODECS = 5,
+  BLOSC2_USER_REGISTERED_CODECS_START = 160,
+  BLOSC2_USER_REGISTERED_CODECS_STOP = 255,
+};
+enum {
+  BLOSC_BLOSCLZ = 0,
+  BLOSC_LZ4 = 1,
+  BLOSC_LZ4HC = 2,
+  BLOSC_ZLIB = 4,
+  BLOSC_ZSTD = 5,
+  BLOSC_LAST_CODEC = 6,
+  BLOSC_LAST_REGISTERED_CODEC = BLOSC2_GLOBAL_REGISTERED_CODECS_START + BLOSC2_GLOBAL_REGISTERED_CODECS - 1,
+};
+#define BLOSC_BLOSCLZ_COMPNAME "blosclz"
+#define BLOSC_LZ4_COMPNAME "lz4"
+#define BLOSC_LZ4HC_COMPNAME "lz4hc"
+#define BLOSC_ZLIB_COMPNAME "zlib"
+#define BLOSC_ZSTD_COMPNAME "zstd"
+enum {
+  BLOSC_BLOSCLZ_LIB = 0,
+  BLOSC_LZ4_LIB = 1,
+  BLOSC_ZLIB_LIB = 3,
+  BLOSC_ZSTD_LIB = 4,
+  BLOSC_UDCODEC_LIB = 6,
+  BLOSC_SCHUNK_LIB = 7,
+};
+#define BLOSC_BLOSCLZ_LIBNAME "BloscLZ"
+#define BLOSC_LZ4_LIBNAME "LZ4"
+#define BLOSC_ZLIB_LIBNAME "Zlib"
+#define BLOSC_ZSTD_LIBNAME "Zstd"
+enum {
+  BLOSC_BLOSCLZ_FORMAT = BLOSC_BLOSCLZ_LIB,
+  BLOSC_LZ4_FORMAT = BLOSC_LZ4_LIB,
+  BLOSC_LZ4HC_FORMAT = BLOSC_LZ4_LIB,
+  BLOSC_ZLIB_FORMAT = BLOSC_ZLIB_LIB,
+  BLOSC_ZSTD_FORMAT = BLOSC_ZSTD_LIB,
+  BLOSC_UDCODEC_FORMAT = BLOSC_UDCODEC_LIB,
+};
+enum {
+  BLOSC_BLOSCLZ_VERSION_FORMAT = 1,
+  BLOSC_LZ4_VERSION_FORMAT = 1,
+  BLOSC_LZ4HC_VERSION_FORMAT = 1,
+  BLOSC_ZLIB_VERSION_FORMAT = 1,
+  BLOSC_ZSTD_VERSION_FORMAT = 1,
+  BLOSC_UDCODEC_VERSION_FORMAT = 1,
+};
+/* split modes (include/blosc2.h:410-415) */
+enum {
+  BLOSC_ALWAYS_SPLIT = 1,
+  BLOSC_NEVER_SPLIT = 2,
+  BLOSC_AUTO_SPLIT = 3,
+  BLOSC_FORWARD_COMPAT_SPLIT = 4,
+};
+/* chunk header offsets (include/blosc2.h:420-433) */
+enum {
+  BLOSC2_CHUNK_VERSION = 0x0,
+  BLOSC2_CHUNK_VERSIONLZ = 0x1,
+  BLOSC2_CHUNK_FLAGS = 0x2,
+  BLOSC2_CHUNK_TYPESIZE = 0x3,
+  BLOSC2_CHUNK_NBYTES = 0x4,
+  BLOSC2_CHUNK_BLOCKSIZE = 0x8,
+  BLOSC2_CHUNK_CBYTES = 0xc,
+  BLOSC2_CHUNK_FILTER_CODES = 0x10,
+  BLOSC2_CHUNK_FILTER_META = 0x18,
+  BLOSC2_CHUNK_BLOSC2_FLAGS2 = 0x1e,
+  BLOSC2_CHUNK_BLOSC2_FLAGS = 0x1F,
+};
+/* special values (include/blosc2.h:438-446) */
+enum {
+  BLOSC2_NO_SPECIAL = 0x0,
+  BLOSC2_SPECIAL_ZERO = 0x1,
+  BLOSC2_SPECIAL_NAN = 0x2,
+  BLOSC2_SPECIAL_VALUE = 0x3,
+  BLOSC2_SPECIAL_UNINIT = 0x4,
+  BLOSC2_SPECIAL_LASTID = 0x4,
+  BLOSC2_SPECIAL_MASK = 0x7,
+};
+/* error codes (include/blosc2.h:453-492) */
+enum {
+  BLOSC2_ERROR_SUCCESS = 0,
+  BLOSC2_ERROR_FAILURE = -1,
+  BLOSC2_ERROR_STREAM = -2,
+  BLOSC2_ERROR_DATA = -3,
+  BLOSC2_ERROR_MEMORY_ALLOC = -4,
+  BLOSC2_ERROR_READ_BUFFER = -5,
+  BLOSC2_ERROR_WRITE_BUFFER = -6,
+  BLOSC2_ERROR_CODEC_SUPPORT = -7,
+  BLOSC2_ERROR_CODEC_PARAM = -8,
+  BLOSC2_ERROR_CODEC_DICT = -9,
+  BLOSC2_ERROR_VERSION_SUPPORT = -10,
+  BLOSC2_ERROR_INVALID_HEADER = -11,
+  BLOSC2_ERROR_INVALID_PARAM = -12,
+  BLOSC2_ERROR_FILE_READ = -13,
+  BLOSC2_ERROR_FILE_WRITE = -14,
+  BLOSC2_ERROR_FILE_OPEN = -15,
+  BLOSC2_ERROR_NOT_FOUND = -16,
+  BLOSC2_ERROR_RUN_LENGTH = -17,
+  BLOSC2_ERROR_FILTER_PIPELINE = -18,
+  BLOSC2_ERROR_CHUNK_INSERT = -19,
+  BLOSC2_ERROR_CHUNK_APPEND = -20,
+  BLOSC2_ERROR_CHUNK_UPDATE = -21,
+  BLOSC2_ERROR_2GB_LIMIT = -22,
+  BLOSC2_ERROR_SCHUNK_COPY = -23,
+  BLOSC2_ERROR_FRAME_TYPE = -24,
+  BLOSC2_ERROR_FILE_TRUNCATE = -25,
+  BLOSC2_ERROR_THREAD_CREATE = -26,
+  BLOSC2_ERROR_POSTFILTER = -27,
+  BLOSC2_ERROR_FRAME_SPECIAL = -28,
+  BLOSC2_ERROR_SCHUNK_SPECIAL = -29,
+  BLOSC2_ERROR_PLUGIN_IO = -30,
+  BLOSC2_ERROR_FILE_REMOVE = -31,
+  BLOSC2_ERROR_NULL_POINTER = -32,
+  BLOSC2_ERROR_INVALID_INDEX = -33,
+  BLOSC2_ERROR_METALAYER_NOT_FOUND = -34,
+  BLOSC2_ERROR_MAX_BUFSIZE_EXCEEDED = -35,
+  BLOSC2_ERROR_TUNER = -36,
+  BLOSC2_ERROR_LOCK = -37,
+};
+
+/* ---- context and parameter structs (ABI-identical to include/blosc2.h:1125-1248) ---- */
+typedef struct blosc2_context_s blosc2_context;
+
+typedef struct {
+  void *user_data;
+  const uint8_t *input;
+  uint8_t *output;
+  int32_t output_size;
+  int32_t output_typesize;
+  int32_t output_offset;
+  int64_t nchunk;
+  int32_t nblock;
+  int32_t tid;
+  uint8_t *ttmp;
+  size_t ttmp_nbytes;
+  blosc2_context *ctx;
+  bool output_is_disposable;
+} blosc2_prefilter_params;
+
+typedef struct {
+  void *user_data;
+  const uint8_t *input;
+  uint8_t *output;
+  int32_t size;
+  int32_t typesize;
+  int32_t offset;
+  int64_t nchunk;
+  int32_t nblock;
+  int32_t tid;
+  uint8_t *ttmp;
+  size_t ttmp_nbytes;
+  blosc2_context *ctx;
+} blosc2_postfilter_params;
+
+typedef int (*blosc2_prefilter_fn)(blosc2_prefilter_params *params);
+typedef int (*blosc2_postfilter_fn)(blosc2_postfilter_params *params);
+
+/* include/blosc2.h:1173-1211 */
+typedef struct {
+  uint8_t compcode;
+  uint8_t compcode_meta;
+  uint8_t clevel;
+  int use_dict;
+  int32_t typesize;
+  int16_t nthreads;
+  int32_t blocksize;
+  int32_t splitmode;
+  void *schunk;
+  uint8_t filters[BLOSC2_MAX_FILTERS];
+  uint8_t filters_meta[BLOSC2_MAX_FILTERS];
+  blosc2_prefilter_fn prefilter;
+  blosc2_prefilter_params *preparams;
+  void *tuner_params;
+  int tuner_id;
+  bool instr_codec;
+  void *codec_params;
+  void *filter_params[BLOSC2_MAX_FILTERS];
+} blosc2_cparams;
+
+/* include/blosc2.h:1216-1223 */
+static const blosc2_cparams BLOSC2_CPARAMS_DEFAULTS = {
+    BLOSC_BLOSCLZ, 0, 5, 0, 8, 1, 0, BLOSC_FORWARD_COMPAT_SPLIT, NULL,
+    {0, 0, 0, 0, 0, BLOSC_SHUFFLE}, {0, 0, 0, 0, 0, 0},
+    NULL, NULL, NULL, 0, 0, NULL, {NULL, NULL, NULL, NULL, NULL, NULL}};
+
+/* include/blosc2.h:1232-1243 */
+typedef struct {
+  int16_t nthreads;
+  void *schunk;
+  blosc2_postfilter_fn postfilter;
+  blosc2_postfilter_params *postparams;
+  int32_t typesize;
+} blosc2_dparams;
+
+/* include/blosc2.h:1248 */
+static const blosc2_dparams BLOSC2_DPARAMS_DEFAULTS = {1, NULL, NULL, NULL, 8};
+
+/* ---- codec / filter plugin registry (include/blosc2.h:2698-2762) ---- */
+typedef int (*blosc2_codec_encoder_cb)(const uint8_t *input, int32_t input_len, uint8_t *output, int32_t output_len,
+                                       uint8_t meta, blosc2_cparams *cparams, const void *chunk);
+typedef int (*blosc2_codec_decoder_cb)(const uint8_t *input, int32_t input_len, uint8_t *output, int32_t output_len,
+                                       uint8_t meta, blosc2_dparams *dparams, const void *chunk);
+typedef struct {
+  uint8_t compcode;
+  char *compname;
+  uint8_t complib;
+  uint8_t version;
+  blosc2_codec_encoder_cb encoder;
+  blosc2_codec_decoder_cb decoder;
+} blosc2_codec;
+
+typedef int (*blosc2_filter_forward_cb)(const uint8_t *, uint8_t *, int32_t, uint8_t, blosc2_cparams *, uint8_t);
+typedef int (*blosc2_filter_backward_cb)(const uint8_t *, uint8_t *, int32_t, uint8_t, blosc2_dparams *, uint8_t);
+typedef struct {
+  uint8_t id;
+  char *name;
+  uint8_t version;
+  blosc2_filter_forward_cb forward;
+  blosc2_filter_backward_cb backward;
+} blosc2_filter;
+
+/* ================================================================ entry points ========= */
+/* library lifetime: include/blosc2.h:540 (blosc2_init), 551 (blosc2_destroy) */
+BLOSC_EXPORT void blosc2_init(void);
+BLOSC_EXPORT void blosc2_destroy(void);
+/* include/blosc2.h:843 (blosc2_get_version_string) */
+BLOSC_EXPORT const char *blosc2_get_version_string(void);
+
+/* contexts: include/blosc2.h:1263-1328 */
+BLOSC_EXPORT blosc2_context *blosc2_create_cctx(blosc2_cparams cparams);
+BLOSC_EXPORT blosc2_context *blosc2_create_dctx(blosc2_dparams dparams);
+BLOSC_EXPORT void blosc2_free_ctx(blosc2_context *context);
+BLOSC_EXPORT int blosc2_ctx_get_cparams(blosc2_context *ctx, blosc2_cparams *cparams);
+BLOSC_EXPORT int blosc2_ctx_get_dparams(blosc2_context *ctx, blosc2_dparams *dparams);
+BLOSC_EXPORT int blosc2_set_maskout(blosc2_context *ctx, bool *maskout, int nblocks);
+
+/* the hot path: include/blosc2.h:1482-1484 and 1538-1539 */
+BLOSC_EXPORT int blosc2_compress_ctx(blosc2_context *context, const void *src, int32_t srcsize, void *dest,
+                                     int32_t destsize);
+BLOSC_EXPORT int blosc2_decompress_ctx(blosc2_context *context, const void *src, int32_t srcsize, void *dest,
+                                       int32_t destsize);
+/* partial decode: include/blosc2.h:1698 (blosc2_getitem_ctx), 722 (blosc2_getitem) */
+BLOSC_EXPORT int blosc2_getitem_ctx(blosc2_context *context, const void *src, int32_t srcsize, int start, int nitems,
+                                    void *dest, int32_t destsize);
+BLOSC_EXPORT int blosc2_getitem(const void *src, int32_t srcsize, int start, int nitems, void *dest,
+                                int32_t destsize);
+
+/* global-context API: include/blosc2.h:1413 (blosc2_compress), 1459 (blosc2_decompress),
+ * 638-704 (blosc1_compress / blosc1_decompress / blosc1_getitem) */
+BLOSC_EXPORT int blosc2_compress(int clevel, int doshuffle, int32_t typesize, const void *src, int32_t srcsize,
+                                 void *dest, int32_t destsize);
+BLOSC_EXPORT int blosc2_decompress(const void *src, int32_t srcsize, void *dest, int32_t destsize);
+BLOSC_EXPORT int blosc1_compress(int clevel, int doshuffle, size_t typesize, size_t nbytes, const void *src,
+                                 void *dest, size_t destsize);
+BLOSC_EXPORT int blosc1_decompress(const void *src, void *dest, size_t destsize);
+BLOSC_EXPORT int blosc1_getitem(const void *src, int start, int nitems, void *dest);
+
+/* global settings: include/blosc2.h:751-797, 2649-2679 */
+BLOSC_EXPORT int16_t blosc2_get_nthreads(void);
+BLOSC_EXPORT int16_t blosc2_set_nthreads(int16_t nthreads);
+BLOSC_EXPORT const char *blosc1_get_compressor(void);
+BLOSC_EXPORT int blosc1_set_compressor(const char *compname);
+BLOSC_EXPORT void blosc2_set_delta(int dodelta);
+BLOSC_EXPORT int blosc1_get_blocksize(void);
+BLOSC_EXPORT void blosc1_set_blocksize(size_t blocksize);
+BLOSC_EXPORT void blosc1_set_splitmode(int splitmode);
+
+/* codec names: include/blosc2.h:809-861 */
+BLOSC_EXPORT int blosc2_compcode_to_compname(int compcode, const char **compname);
+BLOSC_EXPORT int blosc2_compname_to_compcode(const char *compname);
+BLOSC_EXPORT const char *blosc2_list_compressors(void);
+BLOSC_EXPORT int blosc2_get_complib_info(const char *compname, char **complib, char **version);
+
+/* chunk inspection: include/blosc2.h:893-988 */
+BLOSC_EXPORT int blosc2_cbuffer_sizes(const void *cbuffer, int32_t *nbytes, int32_t *cbytes, int32_t *blocksize);
+BLOSC_EXPORT void blosc1_cbuffer_sizes(const void *cbuffer, size_t *nbytes, size_t *cbytes, size_t *blocksize);
+BLOSC_EXPORT int blosc1_cbuffer_validate(const void *cbuffer, size_t cbytes, size_t *nbytes);
+BLOSC_EXPORT void blosc2_cbuffer_versions(const void *cbuffer, int *version, int *versionlz);
+BLOSC_EXPORT const char *blosc2_cbuffer_complib(const void *cbuffer);
+BLOSC_EXPORT void blosc1_cbuffer_metainfo(const void *cbuffer, size_t *typesize, int *flags);
+
+/* plugin registry: include/blosc2.h:2727 (codec), 2762 (filter) */
+BLOSC_EXPORT int blosc2_register_codec(blosc2_codec *codec);
+BLOSC_EXPORT int blosc2_register_filter(blosc2_filter *filter);
+
+/* raw filters on host buffers (executed by the GPU kernels): include/blosc2.h:2845-2900 */
+BLOSC_EXPORT int32_t blosc2_shuffle(int32_t typesize, int32_t blocksize, const void *src, void *dest);
+BLOSC_EXPORT int32_t blosc2_unshuffle(int32_t typesize, int32_t blocksize, const void *src, void *dest);
+BLOSC_EXPORT int32_t blosc2_bitshuffle(int32_t typesize, int32_t blocksize, const void *src, void *dest);
+BLOSC_EXPORT int32_t blosc2_bitunshuffle(int32_t typesize, int32_t blocksize, const void *src, void *dest);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BLOSC2_AMD_BLOSC2_H */

@@ -22,7 +22,7 @@ enum {
   SPLIT_ALWAYS = 1, SPLIT_NEVER = 2, SPLIT_AUTO = 3, SPLIT_FWD = 4,
   SPECIAL_ZERO = 1, SPECIAL_NAN = 2, SPECIAL_VALUE = 3, SPECIAL_UNINIT = 4,
   ERR_DATA = -3, ERR_READ = -5, ERR_WRITE = -6, ERR_PARAM = -12, ERR_CODEC = -7,
-  ERR_RUNLEN = -33, ERR_FILTER = -8, ERR_HEADER = -39,
+  ERR_RUNLEN = -17, ERR_FILTER = -18, ERR_HEADER = -11,
 };
 
 static inline uint32_t ld32(const uint8_t *p) {

@@ -1,0 +1,96 @@
+"""CPU tier: the C-ABI library loads and exports every entry point include/*.h declares, and the
+host-only logic (header inspection, registry rules) behaves like the reference.  No compute calls:
+there is no GPU here, and the compute entry points must fail loudly without one."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from b2ctypes import REPO
+
+import sys
+sys.path.insert(0, os.path.join(REPO, "c-blosc2_amd"))
+import blosc2_amd as B  # noqa: E402
+
+GOLD = os.path.join(REPO, "tests", "golden")
+
+
+def declared_symbols():
+    names = []
+    for h in ("blosc2.h", "b2h.h"):
+        txt = open(os.path.join(REPO, "include", h)).read()
+        names += re.findall(r"^BLOSC_EXPORT[^;(]*?\b(\w+)\s*\(", txt, flags=re.M)
+    return sorted(set(names))
+
+
+def test_all_declared_symbols_exported():
+    lib = C.CDLL(B.LIB_PATH)
+    names = declared_symbols()
+    assert len(names) >= 50
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_header_inspection_matches_reference_fields():
+    L = B.lib()
+    gold = np.fromfile(os.path.join(GOLD, "blosc-blosclz-3.0.0.cdata"), np.uint8)
+    nb, cb, bs = C.c_int32(), C.c_int32(), C.c_int32()
+    assert L.blosc2_cbuffer_sizes(B._p(gold), C.byref(nb), C.byref(cb), C.byref(bs)) == 0
+    assert (nb.value, cb.value, bs.value) == (4_000_000, 16910, 2 * 1024 * 1024)
+    v, vlz = C.c_int(), C.c_int()
+    L.blosc2_cbuffer_versions(B._p(gold), C.byref(v), C.byref(vlz))
+    assert (v.value, vlz.value) == (5, 1)
+    L.blosc2_cbuffer_complib.restype = C.c_char_p
+    assert L.blosc2_cbuffer_complib(B._p(gold)) == b"BloscLZ"
+    ts, fl = C.c_size_t(), C.c_int()
+    L.blosc1_cbuffer_metainfo(B._p(gold), C.byref(ts), C.byref(fl))
+    assert (ts.value, fl.value) == (4, 5)
+    n = C.c_size_t()
+    assert L.blosc1_cbuffer_validate(B._p(gold), C.c_size_t(16910), C.byref(n)) == 0 and n.value == 4_000_000
+    assert L.blosc2_get_version_string() == b"3.3.3.dev"
+
+
+def test_registry_id_rules():
+    """blosc2_register_codec/filter only accept user ids >= 160 (blosc/blosc2.c:6680-6737)."""
+    L = B.lib()
+
+    class Codec(C.Structure):
+        _fields_ = [("compcode", C.c_uint8), ("compname", C.c_char_p), ("complib", C.c_uint8),
+                    ("version", C.c_uint8), ("encoder", C.c_void_p), ("decoder", C.c_void_p)]
+
+    class Filter(C.Structure):
+        _fields_ = [("id", C.c_uint8), ("name", C.c_char_p), ("version", C.c_uint8),
+                    ("forward", C.c_void_p), ("backward", C.c_void_p)]
+    assert L.blosc2_register_codec(C.byref(Codec(100, b"low", 0, 1, None, None))) < 0
+    assert L.blosc2_register_codec(C.byref(Codec(200, b"mine", 0, 1, None, None))) == 0
+    assert L.blosc2_register_filter(C.byref(Filter(40, b"low", 1, None, None))) < 0
+    assert L.blosc2_register_filter(C.byref(Filter(201, b"mine", 1, None, None))) == 0
+    L.blosc2_compname_to_compcode.argtypes = [C.c_char_p]
+    assert L.blosc2_compname_to_compcode(b"mine") == 200
+    assert L.blosc2_compname_to_compcode(b"blosclz") == 0
+
+
+def test_context_params_roundtrip():
+    L = B.lib()
+    L.blosc2_ctx_get_cparams.argtypes = [C.c_void_p, C.POINTER(B.CParams)]
+    cp = B.cparams(clevel=7, typesize=4, filters=(0, 0, 0, 0, 3, 2), blocksize=65536)
+    ctx = L.blosc2_create_cctx(cp)
+    out = B.CParams()
+    assert L.blosc2_ctx_get_cparams(ctx, C.byref(out)) == 0
+    assert (out.clevel, out.typesize, out.blocksize, list(out.filters)) == (7, 4, 65536, [0, 0, 0, 0, 3, 2])
+    L.blosc2_free_ctx(ctx)
+    # an undefined built-in filter id is rejected at context creation (blosc/blosc2.c:6052-6066)
+    assert L.blosc2_create_cctx(B.cparams(filters=(0, 0, 0, 0, 0, 7))) is None
+
+
+@pytest.mark.skipif(B.lib().b2h_device_count() > 0, reason="a GPU is present")
+def test_no_gpu_fails_loudly():
+    """Without a GPU the compute entry points return an error: there is no CPU fallback."""
+    L = B.lib()
+    src = np.arange(1000, dtype=np.int32)
+    ctx = L.blosc2_create_cctx(B.cparams(typesize=4))
+    out = np.zeros(src.nbytes + 64, np.uint8)
+    assert L.blosc2_compress_ctx(ctx, B._p(src), src.nbytes, B._p(out), out.nbytes) < 0
+    L.blosc2_free_ctx(ctx)

@@ -1,0 +1,258 @@
+"""GPU tier: the HIP path (through the drop-in C ABI and the device batch ABI) against the oracle
+restatement, the reference library built from its sources (oracle/_ref, when present) and the
+reference's own golden vectors.  Bar: byte-identical chunks, exact round trips."""
+import ctypes as C
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from b2ctypes import REPO
+from datagen import gen_f32, int64_ramp, mixed_bytes
+from oracle_lib import oracle, oracle_compress, oracle_decompress, p, ref, ref_compress
+
+sys.path.insert(0, os.path.join(REPO, "c-blosc2_amd"))
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(REPO, "tests", "golden")
+RAMP = np.arange(1_000_000, dtype=np.int32)
+
+
+@pytest.fixture(scope="module")
+def B():
+    import torch  # noqa: F401  (same HIP runtime as bench.py: torch first, then the engine)
+    import blosc2_amd
+    L = blosc2_amd.lib()
+    assert L.b2h_device_count() > 0
+    return blosc2_amd
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def test_shuffle_kats(B):
+    L = B.lib()
+    out = np.zeros(RAMP.nbytes, np.uint8)
+    assert L.blosc2_shuffle(4, RAMP.nbytes, B._p(RAMP), B._p(out)) == RAMP.nbytes
+    assert sha(out) == "40e1351bba9155c3d765d66b5b4d25cb104aa2ad4b844b0a5d20af40cab2b920"
+    back = np.zeros_like(out)
+    L.blosc2_unshuffle(4, RAMP.nbytes, B._p(out), B._p(back))
+    assert np.array_equal(back.view(np.int32), RAMP)
+    L.blosc2_bitshuffle(4, RAMP.nbytes, B._p(RAMP), B._p(out))
+    assert sha(out) == "a1bba6ced356ddca157010f340b8b5a39a5cd43a77b7c99cd1cb8896e853169d"
+    L.blosc2_bitunshuffle(4, RAMP.nbytes, B._p(out), B._p(back))
+    assert np.array_equal(back.view(np.int32), RAMP)
+
+
+@pytest.mark.parametrize("ts", [1, 2, 3, 4, 7, 8, 16, 17, 80])
+@pytest.mark.parametrize("nelem", [7, 192, 500, 1792, 8000, 100000])
+def test_shuffle_grid_vs_oracle(B, ts, nelem):
+    """test_shuffle_roundtrip_*.csv grid: GPU vs oracle, byte-exact, both directions."""
+    L, O = B.lib(), oracle()
+    src = np.random.default_rng(ts * 7 + nelem).integers(0, 256, ts * nelem + 3, dtype=np.uint8)
+    n = src.nbytes
+    g, o = np.zeros(n, np.uint8), np.zeros(n, np.uint8)
+    for fg, fo in (("blosc2_shuffle", "or_shuffle"), ("blosc2_unshuffle", "or_unshuffle"),
+                   ("blosc2_bitshuffle", "or_bitshuffle")):
+        getattr(L, fg)(ts, n, B._p(src), B._p(g))
+        getattr(O, fo)(ts, n, p(src), p(o))
+        assert np.array_equal(g, o), fg
+    L.blosc2_bitunshuffle(ts, n, B._p(src), B._p(g))
+    O.or_bitunshuffle(ts, n, p(src), p(o), 6)
+    assert np.array_equal(g, o)
+
+
+def test_blosclz_chunk_kat(B):
+    """compat/blosc-blosclz-3.0.0.cdata == blosc1_compress(9, SHUFFLE, 4, ramp)."""
+    L = B.lib()
+    gold = np.fromfile(os.path.join(GOLD, "blosc-blosclz-3.0.0.cdata"), np.uint8)
+    L.blosc1_set_compressor(b"blosclz")
+    out = np.zeros(RAMP.nbytes, np.uint8)
+    n = L.blosc1_compress(9, 1, 4, RAMP.nbytes, B._p(RAMP), B._p(out), RAMP.nbytes)
+    assert n == gold.nbytes
+    assert np.array_equal(out[:n], gold)
+    dec = np.zeros(RAMP.nbytes, np.uint8)
+    assert L.blosc1_decompress(B._p(gold), B._p(dec), RAMP.nbytes) == RAMP.nbytes
+    assert np.array_equal(dec.view(np.int32), RAMP)
+
+
+@pytest.mark.parametrize("name", ["blosc-1.3.0-blosclz.cdata", "blosc-1.7.0-blosclz.cdata",
+                                  "blosc-1.11.1-blosclz.cdata", "blosc-1.14.0-blosclz.cdata"])
+def test_blosc1_decode_kats(B, name):
+    gold = np.fromfile(os.path.join(GOLD, name), np.uint8)
+    dec = B.decompress(gold, RAMP.nbytes)
+    assert isinstance(dec, np.ndarray), dec
+    assert np.array_equal(dec.view(np.int32), RAMP)
+
+
+def test_golden_chunks(B):
+    """Reference-produced chunks (tests/golden/make_golden.py): GPU compress is byte-identical,
+    GPU decompress restores the input."""
+    man = json.load(open(os.path.join(GOLD, "chunks.json")))
+    data = np.load(os.path.join(GOLD, "chunks.npz"))
+    for i, case in enumerate(man):
+        src, want = data[f"in_{i}"], data[f"out_{i}"]
+        kw = {k: case[k] for k in ("clevel", "typesize", "filters", "filters_meta", "blocksize", "splitmode")}
+        got = B.compress(src, **kw)
+        assert isinstance(got, np.ndarray) and np.array_equal(got, want), (i, case)
+        dec = B.decompress(want, src.nbytes)
+        assert isinstance(dec, np.ndarray), (i, dec)
+        assert np.array_equal(dec, oracle_decompress(want, src.nbytes)), (i, case)
+        if case.get("lossless", True):
+            assert np.array_equal(dec, src), (i, case)
+
+
+def _cases(seed, count):
+    rng = np.random.default_rng(seed)
+    for _ in range(count):
+        ts = int(rng.choice([1, 2, 4, 8, 16]))
+        kind = int(rng.integers(0, 4))
+        n = int(rng.integers(1, 600_000)) // ts * ts or ts
+        if kind == 0:
+            src = gen_f32(int(rng.integers(0, 1 << 30)), max(1, n // 4))
+            ts = 4
+        elif kind == 1:
+            src = int64_ramp(int(rng.integers(0, 1 << 40)), max(1, n // 8))
+            ts = 8
+        else:
+            src = mixed_bytes(int(rng.integers(0, 1 << 30)), n)
+        f5 = int(rng.choice([0, 1, 2]))
+        f4 = int(rng.choice([0, 3])) if kind != 2 or ts in (1, 2, 4, 8) else 0
+        yield src, dict(clevel=int(rng.integers(1, 10)), typesize=ts, filters=(0, 0, 0, 0, f4, f5),
+                        blocksize=int(rng.choice([0, 0, 16384, 131072])),
+                        splitmode=int(rng.choice([1, 2, 4])))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_chunks_vs_oracle(B, seed):
+    for src, kw in _cases(seed, 10):
+        want = oracle_compress(src, **kw)
+        got = B.compress(src, **kw)
+        assert isinstance(want, np.ndarray)
+        assert isinstance(got, np.ndarray) and np.array_equal(got, want), kw
+        if ref() is not None:
+            assert np.array_equal(ref_compress(src, **kw), want), kw
+        dec = B.decompress(got, src.nbytes)
+        assert np.array_equal(dec, src.view(np.uint8).reshape(-1)), kw
+
+
+@pytest.mark.parametrize("slack", [-200_000, -70_000, -5000, -300, -40, 0, 32])
+def test_tight_destsize_serial_semantics(B, slack):
+    """destsize below nbytes+32 exercises the serial maxout reduction (blosc/blosc2.c:1343-1350),
+    the memcpy fallback and the 'does not fit' (0) return."""
+    L = B.lib()
+    for src, ts in ((mixed_bytes(11, 400_000), 1), (gen_f32(3, 100_000), 4)):
+        destsize = src.nbytes + 32 + slack
+        cp = B.cparams(clevel=5, typesize=ts)
+        ctx = L.blosc2_create_cctx(cp)
+        got = B.compress_ctx(ctx, src, destsize=destsize)
+        L.blosc2_free_ctx(ctx)
+        oc = oracle()
+        from oracle_lib import or_cparams
+        ocp = or_cparams(clevel=5, typesize=ts)
+        raw = src.view(np.uint8).reshape(-1)
+        out = np.zeros(raw.nbytes + 64, np.uint8)
+        n = oc.or_compress_chunk(C.byref(ocp), p(raw), raw.nbytes, p(out), destsize)
+        if n > 0:
+            assert isinstance(got, np.ndarray) and np.array_equal(got, out[:n]), (slack, ts)
+        else:
+            assert got == n, (slack, ts, got, n)
+
+
+def test_context_blocksize_is_sticky(B):
+    """A compression context keeps the blocksize of its previous call (blosc/blosc2.c:2414)."""
+    L = B.lib()
+    ctx = L.blosc2_create_cctx(B.cparams(clevel=5, typesize=4))
+    small, big = np.arange(1000, dtype=np.int32), np.arange(1 << 20, dtype=np.int32)
+    outs = [B.compress_ctx(ctx, x) for x in (small, big)]
+    L.blosc2_free_ctx(ctx)
+    assert outs[1][8:12].view(np.int32)[0] == 4000
+    if ref() is not None:
+        R = ref()
+        from b2ctypes import cparams as rcp
+        rctx = R.blosc2_create_cctx(rcp(clevel=5, typesize=4))
+        for x, g in zip((small, big), outs):
+            o = np.zeros(x.nbytes + 64, np.uint8)
+            n = R.blosc2_compress_ctx(rctx, p(x), x.nbytes, p(o), x.nbytes + 32)
+            assert np.array_equal(o[:n], g)
+        R.blosc2_free_ctx(rctx)
+
+
+def test_maskout_and_getitem(B):
+    L = B.lib()
+    src = gen_f32(0, 1 << 18)
+    chunk = B.compress(src, clevel=5, typesize=4, blocksize=65536)
+    nblocks = src.nbytes // 65536
+    mask = (C.c_bool * nblocks)(*[i % 3 == 1 for i in range(nblocks)])
+    ctx = L.blosc2_create_dctx(B.dparams())
+    L.blosc2_set_maskout(ctx, mask, nblocks)
+    out = np.full(src.nbytes, 0xEE, np.uint8)
+    assert L.blosc2_decompress_ctx(ctx, B._p(chunk), chunk.nbytes, B._p(out), out.nbytes) == src.nbytes
+    raw = src.view(np.uint8)
+    for b in range(nblocks):
+        blk = slice(b * 65536, (b + 1) * 65536)
+        if b % 3 == 1:
+            assert np.all(out[blk] == 0xEE)
+        else:
+            assert np.array_equal(out[blk], raw[blk])
+    # getitem: items [70000, 70000+5000)
+    item = np.zeros(5000 * 4, np.uint8)
+    assert L.blosc2_getitem_ctx(ctx, B._p(chunk), chunk.nbytes, 70000, 5000, B._p(item), item.nbytes) == item.nbytes
+    assert np.array_equal(item.view(np.float32), src[70000:75000])
+    L.blosc2_free_ctx(ctx)
+
+
+def test_device_batch_matches_per_chunk(B):
+    """b2h_compress_batch over many chunks == per-chunk oracle bytes; batch decompress restores."""
+    import torch
+    nchunks, chunk = 48, 1 << 20
+    host = gen_f32(0, nchunks * chunk // 4)
+    cases = [dict(clevel=5, typesize=4, filters=(0, 0, 0, 0, 0, 1)),
+             dict(clevel=5, typesize=4, filters=(0, 0, 0, 0, 0, 2), blocksize=262144),
+             dict(clevel=9, typesize=4, filters=(0, 0, 0, 0, 3, 1)),
+             dict(clevel=1, typesize=4, filters=(0, 0, 0, 4, 3, 1), filters_meta=(0, 0, 0, 20, 0, 0))]
+    dsrc = torch.from_numpy(host.view(np.uint8)).cuda()
+    cap = chunk + 32
+    stride = (cap + 255) // 256 * 256
+    ddst = torch.zeros(nchunks * stride, dtype=torch.uint8, device="cuda")
+    dcb = torch.zeros(nchunks, dtype=torch.int32, device="cuda")
+    for kw in cases:
+        cp = B.cparams(**kw)
+        B.compress_batch(cp, dsrc.data_ptr(), chunk, nchunks, chunk, ddst.data_ptr(), stride, cap, dcb.data_ptr())
+        torch.cuda.synchronize()
+        cbytes = dcb.cpu().numpy()
+        out = ddst.cpu().numpy()
+        for i in range(nchunks):
+            want = oracle_compress(host[i * chunk // 4:(i + 1) * chunk // 4], **kw)
+            assert cbytes[i] == want.nbytes and np.array_equal(out[i * stride:i * stride + cbytes[i]], want), (kw, i)
+        dout = torch.zeros(nchunks * chunk, dtype=torch.uint8, device="cuda")
+        dst = torch.zeros(nchunks, dtype=torch.int32, device="cuda")
+        B.decompress_batch(ddst.data_ptr(), stride, dcb.data_ptr(), nchunks, dout.data_ptr(), chunk, chunk,
+                           dst.data_ptr())
+        torch.cuda.synchronize()
+        assert (dst.cpu().numpy() == chunk).all()
+        if kw["filters"][3] != 4:   # trunc-prec is lossy
+            assert torch.equal(dout, dsrc)
+
+
+@pytest.mark.slow
+def test_c2_shuffle_256mib_roundtrip(B):
+    """C2 at full size: 256 MiB float32 shuffle ts=4 on device vs a numpy transpose (bit-exact)."""
+    import torch
+    n = 256 << 20
+    host = gen_f32(0, n // 4)
+    d = torch.from_numpy(host.view(np.uint8)).cuda()
+    o = torch.empty_like(d)
+    L = B.lib()
+    assert L.b2h_shuffle(4, n, C.c_void_p(d.data_ptr()), C.c_void_p(o.data_ptr()), 0, None) == n
+    torch.cuda.synchronize()
+    want = host.view(np.uint8).reshape(-1, 4).T.reshape(-1)
+    assert np.array_equal(o.cpu().numpy(), want)
+    back = torch.empty_like(d)
+    L.b2h_shuffle(4, n, C.c_void_p(o.data_ptr()), C.c_void_p(back.data_ptr()), 1, None)
+    torch.cuda.synchronize()
+    assert torch.equal(back, d)
