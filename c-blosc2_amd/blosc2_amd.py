@@ -96,6 +96,14 @@ def lib():
     """Load the HIP library (raises if it was not built: there is no fallback)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch bundles its own libamdhip64 (SONAME libamdhip64.so.7).
+        # Loading torch first lets our library bind to that same copy; loading ours first would
+        # pull /opt/rocm's copy and torch would then add a second runtime.
+        if os.environ.get("B2H_NO_TORCH") is None:
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} missing: build it with `make -C c-blosc2_amd` "
                                "(the MI355X engine has no CPU fallback)")

@@ -61,6 +61,8 @@ struct Scratch {
     cap = 0;
     if (hipMalloc(&p, n) != hipSuccess) { snprintf(g_err, sizeof g_err, "hipMalloc(%zu) failed", n); return E_MEMORY; }
     cap = n;
+    static const bool poison = getenv("B2H_POISON") != nullptr;   // debug: expose unwritten bytes
+    if (poison) (void)hipMemset(p, 0xA5, n);
     return 0;
   }
   template <typename T> T* as() const { return static_cast<T*>(p); }

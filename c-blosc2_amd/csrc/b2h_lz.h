@@ -96,6 +96,9 @@ __device__ LzPassOut lz_pass(const uint8_t* __restrict__ in, int32_t length, int
     uint4* h4 = (uint4*)(htab);
     const int32_t n16 = (int32_t)((sizeof(POS) << hashlog) / 16);
     for (int32_t i = lane; i < n16; i += 64) h4[i] = make_uint4(0, 0, 0, 0);
+    // the clear goes through a uint4 view: keep the compiler from sinking it below the
+    // (differently typed) table reads that follow
+    asm volatile("" ::: "memory");
   }
   LzPassOut r;
   r.peak = 0;

@@ -51,6 +51,8 @@ struct DevBuf {
     cap = 0;
     if (hipMalloc(&p, n) != hipSuccess) return false;
     cap = n;
+    static const bool poison = getenv("B2H_POISON") != nullptr;   // debug: expose unwritten bytes
+    if (poison) (void)hipMemset(p, 0xA5, n);
     return true;
   }
   void release() {
