@@ -95,6 +95,15 @@ int device_count() {
 static bool g_timing = false;
 static KernelTimes g_times{};
 void enable_timing(bool on) { g_timing = on; }
+
+// Diagnostics: copy the per-stream encoder results of the last compression batch to the host.
+int debug_stream_results(void* host, int32_t n) {
+  Workspace* ws = ws_for_current_device();
+  std::lock_guard<std::mutex> lock(ws->mu);
+  if (!ws->res.p || (size_t)n * sizeof(StreamResult) > ws->res.cap) return E_PARAM;
+  HIPCHK(hipMemcpy(host, ws->res.p, (size_t)n * sizeof(StreamResult), hipMemcpyDeviceToHost));
+  return n;
+}
 KernelTimes last_times() { return g_times; }
 
 struct EvPair {
@@ -176,11 +185,14 @@ __global__ __launch_bounds__(64) void k_encode(CGeom g, const uint8_t* __restric
   int32_t off, len, blk;
   stream_locate(g, l, &off, &len, &blk);
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
-  volatile POS* htab = reinterpret_cast<volatile POS*>(smem);
-  volatile uint8_t* tag = smem + (sizeof(POS) << hashlog);
-  const uint8_t* in = filt + (int64_t)c * g.wstride + off;
-  uint8_t* out = sbuf + (int64_t)c * g.wstride + off;
-  StreamResult r = encode_stream<POS>(in, len, g.clevel, out, htab, tag, g.overhead == kHdrExt);
+  volatile B2H_LDS POS* htab = (volatile B2H_LDS POS*)(smem);
+  volatile B2H_LDS uint32_t* tagm = (volatile B2H_LDS uint32_t*)(smem + (sizeof(POS) << hashlog));
+  for (int i = threadIdx.x; i < kTagBuckets; i += 64) tagm[i] = 64u;
+  gin_t in = (gin_t)(filt + (int64_t)c * g.wstride + off);
+  gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  StreamResult r = encode_stream<POS>(in, len, g.clevel, out, htab, tagm, g.overhead == kHdrExt);
+  r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
   if (threadIdx.x == 0) res[s] = r;
 }
 
@@ -278,7 +290,7 @@ __device__ void wg_copy(uint8_t* __restrict__ d, const uint8_t* __restrict__ s, 
     const uint32_t* a = reinterpret_cast<const uint32_t*>(s4);
     for (int32_t i = threadIdx.x; i < body; i += blockDim.x) d4[i] = a[i];
   } else {
-    for (int32_t i = threadIdx.x; i < body; i += blockDim.x) d4[i] = ldu32(s4 + 4 * i);
+    for (int32_t i = threadIdx.x; i < body; i += blockDim.x) d4[i] = ldu32((gin_t)(s4 + 4 * i));
   }
   for (int32_t i = h + body * 4 + threadIdx.x; i < n; i += blockDim.x) d[i] = s[i];
 }
@@ -531,10 +543,10 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
   const bool small = std::max(g.neblock, g.leftover) <= 65536;
   StreamResult* res = ws->res.as<StreamResult>();
   if (small) {
-    const size_t lds = (sizeof(uint16_t) << hashlog) + kTagBuckets;
+    const size_t lds = (sizeof(uint16_t) << hashlog) + 4 * kTagBuckets;
     k_encode<uint16_t><<<(uint32_t)ntot, 64, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot);
   } else {
-    const size_t lds = (sizeof(uint32_t) << hashlog) + kTagBuckets;   // up to 66 KiB: opt in
+    const size_t lds = (sizeof(uint32_t) << hashlog) + 4 * kTagBuckets;   // up to 72 KiB: opt in
     static bool attr_set = false;
     if (!attr_set) {
       HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_encode<uint32_t>),
@@ -764,19 +776,18 @@ __global__ __launch_bounds__(64) void k_decode(const uint8_t* const* __restrict_
   const DChunk d = ch[c];
   if (d.status < 0 || st.neblock < 0) return;
   if (maskout && maskout[st.dst_off / d.blocksize]) return;
-  const uint8_t* in = srcs[c] + st.src;
-  uint8_t* out = (d.nfilters_bwd ? stage + d.stage_off : dsts[c]) + st.dst_off;
+  gin_t in = (gin_t)(srcs[c] + st.src);
+  gout_t out = (gout_t)((d.nfilters_bwd ? stage + d.stage_off : dsts[c]) + st.dst_off);
   const int32_t nb = st.neblock;
   const int lane = threadIdx.x;
   if (st.csize == 0) {
-    for (int32_t i = lane; i < nb; i += 64) out[i] = 0;
+    wave_fill(out, 0, nb);
   } else if (st.csize < 0) {
     const uint8_t token = in[0];
     if (!(token & 1) || st.csize < -255) { if (lane == 0) atomicMin(&ch[c].status, E_RUNLEN); return; }
-    const uint8_t v = (uint8_t)(-st.csize);
-    for (int32_t i = lane; i < nb; i += 64) out[i] = v;
+    wave_fill(out, (uint8_t)(-st.csize), nb);
   } else if (st.csize == nb) {
-    for (int32_t i = lane; i < nb; i += 64) out[i] = in[i];
+    wave_copy(out, in, nb);
   } else {
     if ((d.flags >> 5) != 0) { if (lane == 0) atomicMin(&ch[c].status, E_CODEC); return; }
     const int32_t got = wave_lz_decode(in, st.csize, out, nb);

@@ -32,7 +32,8 @@ struct StreamResult {
   int32_t kind;   // StreamKind
   int32_t size;   // LZ: encoded bytes; run: the repeated byte
   int32_t peak;   // LZ: largest `op + k` bound check made while encoding (<= neblock)
-  int32_t pad;
+  int32_t windows;   // diagnostics: parse windows executed (probe + main pass)
+  int64_t cycles;    // diagnostics: s_memtime ticks spent on this stream
 };
 
 // One chunk of a decompression batch after header parsing (device-side plan).

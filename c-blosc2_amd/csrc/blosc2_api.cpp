@@ -829,6 +829,7 @@ void b2h_last_times(float out[5]) {
   out[0] = t.filter_ms; out[1] = t.encode_ms; out[2] = t.finalize_ms; out[3] = t.decode_ms; out[4] = t.unfilter_ms;
 }
 const char* b2h_last_error(void) { return b2h::last_error(); }
+int b2h_debug_stream_results(void* host, int32_t n) { return b2h::debug_stream_results(host, n); }
 int b2h_device_count(void) { return b2h::device_count(); }
 
 }  // extern "C"

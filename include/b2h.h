@@ -54,6 +54,9 @@ BLOSC_EXPORT void b2h_enable_timing(int on);
 BLOSC_EXPORT void b2h_last_times(float out[5]);
 
 BLOSC_EXPORT const char *b2h_last_error(void);
+/* Diagnostics: per-stream encoder records of the last compression batch on this device
+ * ({kind, size, peak, windows, int64 cycles} x n). Returns n or < 0. Synchronous. */
+BLOSC_EXPORT int b2h_debug_stream_results(void *host, int32_t n);
 BLOSC_EXPORT int b2h_device_count(void);
 
 #ifdef __cplusplus
