@@ -69,7 +69,7 @@ struct Scratch {
 };
 
 struct Workspace {
-  Scratch t1, t2, work, sbuf, res, place, mode;                // compress
+  Scratch t1, t2, work, sbuf, res, place, mode, qctr;          // compress
   Scratch dchunks, dstreams, dblocks, dtotals, stage, stage2, ptrs;  // decompress
   std::mutex mu;
 };
@@ -174,26 +174,39 @@ __global__ __launch_bounds__(kBlockThreads) void k_ffilter(CGeom g, int pass, ui
   }
 }
 
-// One wave per stream.  Dynamic LDS: hash table (POS << hashlog) + tag buckets.
+// Persistent encoder: one wave per workgroup, as many workgroups as fit on the chip (LDS-bound),
+// each pulling stream indices from a device counter until the batch is exhausted.  Stream cost
+// varies ~100x (a float32 mantissa plane vs an all-zero exponent plane) and the hardware deals
+// workgroups to XCDs / shader engines by index, so one-workgroup-per-stream left most slots
+// waiting behind the expensive planes; pulling keeps every resident wave busy.  Every wave exits
+// once the counter passes `nstreams_total`.  Dynamic LDS: hash table (POS << hashlog) + tags.
 template <typename POS>
-__global__ __launch_bounds__(64) void k_encode(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
-                                               StreamResult* __restrict__ res, int32_t nstreams_total) {
+__global__ __launch_bounds__(64) void k_encode(CGeom g, const uint8_t* __restrict__ filt,
+                                               uint8_t* __restrict__ sbuf, StreamResult* __restrict__ res,
+                                               int32_t nstreams_total, int32_t* __restrict__ next) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int32_t s = blockIdx.x;
-  if (s >= nstreams_total) return;
-  const int32_t c = s / g.nsc, l = s - c * g.nsc;
-  int32_t off, len, blk;
-  stream_locate(g, l, &off, &len, &blk);
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
   volatile B2H_LDS POS* htab = (volatile B2H_LDS POS*)(smem);
   volatile B2H_LDS uint32_t* tagm = (volatile B2H_LDS uint32_t*)(smem + (sizeof(POS) << hashlog));
-  for (int i = threadIdx.x; i < kTagBuckets; i += 64) tagm[i] = 64u;
-  gin_t in = (gin_t)(filt + (int64_t)c * g.wstride + off);
-  gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
-  const uint64_t t0 = __builtin_amdgcn_s_memtime();
-  StreamResult r = encode_stream<POS>(in, len, g.clevel, out, htab, tagm, g.overhead == kHdrExt);
-  r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
-  if (threadIdx.x == 0) res[s] = r;
+  for (;;) {
+    // branch-free grab: every lane takes part (lane 0 adds 1, the others 0), so no divergent
+    // region sits between the atomic and the broadcast -- with a lane-0 branch the structurizer
+    // let lanes 1..63 run ahead into the next iteration and re-read a stale index.
+    const int32_t s = __builtin_amdgcn_readfirstlane(atomicAdd(next, lane_id() == 0 ? 1 : 0));
+    if (s >= nstreams_total) return;
+    const int32_t c = s / g.nsc, l = s - c * g.nsc;
+    int32_t off, len, blk;
+    stream_locate(g, l, &off, &len, &blk);
+    for (int i = lane_id(); i < kTagBuckets; i += 64) tagm[i] = 64u;
+    gin_t in = (gin_t)(filt + (int64_t)c * g.wstride + off);
+    gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide time base
+    StreamResult r = encode_stream<POS>(in, len, g.clevel, out, htab, tagm, g.overhead == kHdrExt);
+    r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
+    r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
+    if (lane_id() == 0) res[s] = r;
+  }
 }
 
 struct Place {
@@ -542,18 +555,35 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
   const bool small = std::max(g.neblock, g.leftover) <= 65536;
   StreamResult* res = ws->res.as<StreamResult>();
-  if (small) {
-    const size_t lds = (sizeof(uint16_t) << hashlog) + 4 * kTagBuckets;
-    k_encode<uint16_t><<<(uint32_t)ntot, 64, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot);
-  } else {
-    const size_t lds = (sizeof(uint32_t) << hashlog) + 4 * kTagBuckets;   // up to 72 KiB: opt in
+  rc = ws->qctr.ensure(16);
+  if (rc) return rc;
+  int32_t* next = ws->qctr.as<int32_t>();
+  HIPCHK(hipMemsetAsync(next, 0, sizeof(int32_t), st));
+  {
+    const void* fn = small ? reinterpret_cast<const void*>(&k_encode<uint16_t>)
+                           : reinterpret_cast<const void*>(&k_encode<uint32_t>);
+    const size_t lds = ((small ? sizeof(uint16_t) : sizeof(uint32_t)) << hashlog) + 4 * kTagBuckets;
     static bool attr_set = false;
-    if (!attr_set) {
+    if (!attr_set) {   // > 64 KiB of dynamic LDS per workgroup: opt in once
       HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_encode<uint32_t>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
       attr_set = true;
     }
-    k_encode<uint32_t><<<(uint32_t)ntot, 64, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot);
+    // resident workgroups per CU for this LDS size (cached per size) x CUs
+    static int cached_lds = -1, cached_slots = 0;
+    if ((int)lds != cached_lds) {
+      int dev = 0, per_cu = 0, ncu = 0;
+      HIPCHK(hipGetDevice(&dev));
+      HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, lds));
+      cached_slots = std::max(1, per_cu) * std::max(1, ncu);
+      cached_lds = (int)lds;
+    }
+    const uint32_t grid = (uint32_t)std::min<int64_t>(ntot, cached_slots);
+    if (small)
+      k_encode<uint16_t><<<grid, 64, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next);
+    else
+      k_encode<uint32_t><<<grid, 64, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next);
   }
   ev_encode.stop(st);
   HIPCHK(hipGetLastError());

@@ -34,6 +34,7 @@ struct StreamResult {
   int32_t peak;   // LZ: largest `op + k` bound check made while encoding (<= neblock)
   int32_t windows;   // diagnostics: parse windows executed (probe + main pass)
   int64_t cycles;    // diagnostics: s_memtime ticks spent on this stream
+  int64_t t_start;   // diagnostics: s_memtime at start (occupancy reconstruction)
 };
 
 // One chunk of a decompression batch after header parsing (device-side plan).

@@ -22,7 +22,7 @@ for _ in range(2):
 torch.cuda.synchronize()
 print("times", B.last_times())
 ns = nch * 16 * 4
-rec = np.zeros(ns, dtype=[("kind", "i4"), ("size", "i4"), ("peak", "i4"), ("windows", "i4"), ("cycles", "i8")])
+rec = np.zeros(ns, dtype=[("kind", "i4"), ("size", "i4"), ("peak", "i4"), ("windows", "i4"), ("cycles", "i8"), ("t0", "i8")])
 L.b2h_debug_stream_results.argtypes = [C.c_void_p, C.c_int32]
 assert L.b2h_debug_stream_results(rec.ctypes.data, ns) == ns
 plane = np.arange(ns) % 4
@@ -31,3 +31,28 @@ for p in range(4):
     print(f"plane {p}: kinds {np.bincount(r['kind'], minlength=4).tolist()} size mean {r['size'].mean():.0f} "
           f"windows mean {r['windows'].mean():.0f} max {r['windows'].max()} cycles mean {r['cycles'].mean():.0f} "
           f"max {r['cycles'].max()} cyc/window {r['cycles'].sum() / max(1, r['windows'].sum()):.0f}")
+
+# occupancy reconstruction from start/end stamps (s_memtime is chip-global on gfx950)
+rec2 = np.zeros(ns, dtype=[("kind", "i4"), ("size", "i4"), ("peak", "i4"), ("windows", "i4"), ("cycles", "i8"), ("t0", "i8")])
+assert L.b2h_debug_stream_results(rec2.ctypes.data, ns) == ns
+
+# occupancy from 100 MHz realtime stamps: t_start = (rt0 << 24) | duration
+raw = rec2["t0"].astype(np.uint64)
+rt0 = (raw >> np.uint64(24)).astype(np.int64)
+dur = (raw & np.uint64(0xffffff)).astype(np.int64)
+s0 = rt0 - rt0.min(); s1 = s0 + dur
+ev = np.concatenate([np.stack([s0, np.ones(ns)], 1), np.stack([s1, -np.ones(ns)], 1)])
+ev = ev[np.lexsort((ev[:, 1], ev[:, 0]))]
+act = np.cumsum(ev[:, 1])
+print(f"realtime span {s1.max()/100:.0f} us, max concurrent {act.max():.0f}, avg concurrent {dur.sum()/s1.max():.1f}")
+for p in range(4):
+    print(f"plane {p} mean duration {dur[plane == p].mean()/100:.1f} us")
+bins = 20
+edges = np.linspace(0, s1.max(), bins + 1)
+conc = [int(((s0 < edges[i + 1]) & (s1 > edges[i])).sum()) for i in range(bins)]
+started = [int(((s0 >= edges[i]) & (s0 < edges[i + 1])).sum()) for i in range(bins)]
+print("overlapping per bin:", conc)
+print("started per bin:", started)
+order = np.argsort(s0)
+print("first 8 starts (us):", (s0[order[:8]] / 100).tolist(), "stream ids", order[:8].tolist())
+print("start of stream id quantiles:", [int(s0[min(ns - 1, q)] / 100) for q in (0, 1024, 2048, 4096, 8192, 12288, ns - 1)])
