@@ -55,52 +55,77 @@ def gen_f32_device(start, count, device):
     return out
 
 
-def cpu_baseline(nchunks_sample, chunk_nbytes, threads):
+def _cpu_roundtrip(R, raw, nchunks, chunk_nbytes, threads, reps):
+    """Median-of-`reps` compress and decompress seconds of the reference library over `nchunks`
+    chunks of `raw` with blosc2_compress_ctx / blosc2_decompress_ctx (nthreads = threads)."""
+    import oracle_lib
+    out = np.zeros(chunk_nbytes + 64, np.uint8)
+    tc, td = [], []
+    for _ in range(reps):
+        outs = []
+        if R is not None:
+            from b2ctypes import cparams as rcp, dparams as rdp
+            cctx = R.blosc2_create_cctx(rcp(clevel=5, typesize=4, nthreads=threads))
+            dctx = R.blosc2_create_dctx(rdp(nthreads=threads))
+            t0 = time.perf_counter()
+            for i in range(nchunks):
+                n = R.blosc2_compress_ctx(cctx, C.c_void_p(raw.ctypes.data + i * chunk_nbytes), chunk_nbytes,
+                                          C.c_void_p(out.ctypes.data), chunk_nbytes + 32)
+                outs.append(out[:n].copy())
+            t1 = time.perf_counter()
+            dec = np.empty(chunk_nbytes, np.uint8)
+            for ch in outs:
+                R.blosc2_decompress_ctx(dctx, C.c_void_p(ch.ctypes.data), ch.nbytes,
+                                        C.c_void_p(dec.ctypes.data), chunk_nbytes)
+            t2 = time.perf_counter()
+            R.blosc2_free_ctx(cctx)
+            R.blosc2_free_ctx(dctx)
+        else:
+            src = raw.view(np.float32)
+            t0 = time.perf_counter()
+            for i in range(nchunks):
+                outs.append(oracle_lib.oracle_compress(src[i * chunk_nbytes // 4:(i + 1) * chunk_nbytes // 4],
+                                                       clevel=5, typesize=4))
+            t1 = time.perf_counter()
+            for ch in outs:
+                oracle_lib.oracle_decompress(ch, chunk_nbytes)
+            t2 = time.perf_counter()
+        tc.append(t1 - t0)
+        td.append(t2 - t1)
+    return float(np.median(tc)), float(np.median(td))
+
+
+def cpu_baseline(nchunks_sample, chunk_nbytes, threads, reps=5):
     """The reference library (oracle/_ref, built from /root/reference sources) timed on the host
-    cores on a bounded sample of the same workload.  Falls back to the oracle port if the
-    reference build is absent.  Returns dict for the JSON line."""
+    cores on a bounded sample of the same workload (median of `reps`), at nthreads = threads
+    (the headline `value`) and at nthreads = 1 on a smaller sample.  Falls back to the oracle
+    port (single thread) if the reference build is absent.  Returns dict for the JSON line."""
     from datagen import gen_f32
     import oracle_lib
     R = oracle_lib.ref()
-    src = gen_f32(0, nchunks_sample * chunk_nbytes // 4)
-    raw = src.view(np.uint8)
-    out = np.zeros(chunk_nbytes + 64, np.uint8)
-    outs = []
-    if R is not None:
-        from b2ctypes import cparams as rcp, dparams as rdp
-        cctx = R.blosc2_create_cctx(rcp(clevel=5, typesize=4, nthreads=threads))
-        dctx = R.blosc2_create_dctx(rdp(nthreads=threads))
-        t0 = time.perf_counter()
-        for i in range(nchunks_sample):
-            n = R.blosc2_compress_ctx(cctx, C.c_void_p(raw.ctypes.data + i * chunk_nbytes), chunk_nbytes,
-                                      C.c_void_p(out.ctypes.data), chunk_nbytes + 32)
-            outs.append(out[:n].copy())
-        t1 = time.perf_counter()
-        dec = np.empty(chunk_nbytes, np.uint8)
-        for ch in outs:
-            R.blosc2_decompress_ctx(dctx, C.c_void_p(ch.ctypes.data), ch.nbytes, C.c_void_p(dec.ctypes.data),
-                                    chunk_nbytes)
-        t2 = time.perf_counter()
-        R.blosc2_free_ctx(cctx)
-        R.blosc2_free_ctx(dctx)
-        kind = "reference"
-    else:
+    if R is None:
         threads = 1
-        t0 = time.perf_counter()
-        for i in range(nchunks_sample):
-            outs.append(oracle_lib.oracle_compress(src[i * chunk_nbytes // 4:(i + 1) * chunk_nbytes // 4],
-                                                   clevel=5, typesize=4))
-        t1 = time.perf_counter()
-        for ch in outs:
-            oracle_lib.oracle_decompress(ch, chunk_nbytes)
-        t2 = time.perf_counter()
-        kind = "port"
+    raw = gen_f32(0, nchunks_sample * chunk_nbytes // 4).view(np.uint8)
     nbytes = nchunks_sample * chunk_nbytes
-    return {"value": round(nbytes / ((t1 - t0) + (t2 - t1)) / 2 ** 30, 4), "unit": "GiB/s",
-            "cores": threads, "kind": kind,
-            "sample": f"{nchunks_sample} x {chunk_nbytes >> 20} MiB gen_f32 chunks, compress "
-                      f"{nbytes / (t1 - t0) / 2**30:.3f} GiB/s + decompress {nbytes / (t2 - t1) / 2**30:.3f} GiB/s, "
-                      f"blosc2_*_ctx nthreads={threads}"}
+    tc, td = _cpu_roundtrip(R, raw, nchunks_sample, chunk_nbytes, threads, reps)
+    n1 = max(1, nchunks_sample // 16)
+    tc1, td1 = _cpu_roundtrip(R, raw, n1, chunk_nbytes, 1, max(1, reps // 2))
+    b1 = n1 * chunk_nbytes
+    cpu = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(nbytes / (tc + td) / 2 ** 30, 4), "unit": "GiB/s",
+            "cores": threads, "kind": "reference" if R is not None else "port",
+            "sample": f"{nchunks_sample} x {chunk_nbytes >> 20} MiB gen_f32 chunks (same cparams), median of "
+                      f"{reps}: compress {nbytes / tc / 2**30:.3f} GiB/s + decompress {nbytes / td / 2**30:.3f} GiB/s "
+                      f"at nthreads={threads}; nthreads=1 on {n1} chunks: "
+                      f"{b1 / (tc1 + td1) / 2**30:.3f} GiB/s (c {b1 / tc1 / 2**30:.3f}, d {b1 / td1 / 2**30:.3f}); "
+                      f"host CPU: {cpu}"}
 
 
 def main():
@@ -112,7 +137,7 @@ def main():
     ap.add_argument("--chunk-mib", type=int, default=4)
     ap.add_argument("--clevel", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-chunks", type=int, default=64)
+    ap.add_argument("--cpu-sample-chunks", type=int, default=256)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
