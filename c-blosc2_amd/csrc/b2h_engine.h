@@ -60,6 +60,7 @@ int bitshuffle_dev(int32_t typesize, int32_t nbytes, const uint8_t* d_src, uint8
 struct KernelTimes { float filter_ms, encode_ms, finalize_ms, decode_ms, unfilter_ms; };
 void enable_timing(bool on);
 int debug_stream_results(void* host, int32_t n);
+int debug_decode_cycles(void* host, int32_t n);
 KernelTimes last_times();
 
 // Device bookkeeping

@@ -70,7 +70,7 @@ struct Scratch {
 
 struct Workspace {
   Scratch t1, t2, work, sbuf, res, place, mode, qctr;          // compress
-  Scratch dchunks, dstreams, dblocks, dtotals, stage, stage2, ptrs;  // decompress
+  Scratch dchunks, dstreams, dblocks, dtotals, stage, stage2, ptrs, dqctr, ddbg;  // decompress
   std::mutex mu;
 };
 
@@ -105,6 +105,33 @@ int debug_stream_results(void* host, int32_t n) {
   return n;
 }
 KernelTimes last_times() { return g_times; }
+
+// Diagnostics: per-stream decoder cycles of the last decompression batch (B2H_DECODE_DEBUG=1).
+static const bool g_ddebug = getenv("B2H_DECODE_DEBUG") != nullptr;
+int debug_decode_cycles(void* host, int32_t n) {
+  Workspace* ws = ws_for_current_device();
+  std::lock_guard<std::mutex> lock(ws->mu);
+  if (!g_ddebug || !ws->ddbg.p || (size_t)n * 2 * sizeof(int64_t) > ws->ddbg.cap) return E_PARAM;
+  HIPCHK(hipMemcpy(host, ws->ddbg.p, (size_t)n * 2 * sizeof(int64_t), hipMemcpyDeviceToHost));
+  return n;
+}
+
+// Resident single-wave workgroups of `fn` with `lds` bytes of dynamic LDS (the grid size of the
+// persistent work-pulling kernels), cached per (fn, lds).
+static int resident_slots(const void* fn, size_t lds) {
+  static std::mutex m;
+  static std::vector<std::pair<std::pair<const void*, size_t>, int>> cache;
+  std::lock_guard<std::mutex> g(m);
+  for (auto& e : cache)
+    if (e.first.first == fn && e.first.second == lds) return e.second;
+  int dev = 0, per_cu = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, lds) != hipSuccess) per_cu = 1;
+  const int slots = std::max(1, per_cu) * std::max(1, ncu);
+  cache.push_back({{fn, lds}, slots});
+  return slots;
+}
 
 struct EvPair {
   hipEvent_t a = nullptr, b = nullptr;
@@ -569,17 +596,7 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
       attr_set = true;
     }
-    // resident workgroups per CU for this LDS size (cached per size) x CUs
-    static int cached_lds = -1, cached_slots = 0;
-    if ((int)lds != cached_lds) {
-      int dev = 0, per_cu = 0, ncu = 0;
-      HIPCHK(hipGetDevice(&dev));
-      HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-      HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, lds));
-      cached_slots = std::max(1, per_cu) * std::max(1, ncu);
-      cached_lds = (int)lds;
-    }
-    const uint32_t grid = (uint32_t)std::min<int64_t>(ntot, cached_slots);
+    const uint32_t grid = (uint32_t)std::min<int64_t>(ntot, resident_slots(fn, lds));
     if (small)
       k_encode<uint16_t><<<grid, 64, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next);
     else
@@ -794,14 +811,17 @@ __global__ void k_dplan_blocks(const uint8_t* const* __restrict__ srcs, const in
   if (err) atomicMin(&ch[c].status, err);
 }
 
-// One wave per stream.
-__global__ __launch_bounds__(64) void k_decode(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
-                                               DChunk* __restrict__ ch, const DStream* __restrict__ streams,
-                                               uint8_t* __restrict__ stage, int32_t nstreams_total,
-                                               const uint8_t* __restrict__ maskout) {
-  const int32_t s = blockIdx.x;
-  if (s >= nstreams_total) return;
-  const DStream st = streams[s];
+// Decoder: one wave per stream, persistent (as many single-wave workgroups as the LDS ring
+// allows), streams pulled from a device counter -- stream cost ranges from a 64 KiB memset to
+// thousands of LZ tokens, and a blockIdx-based mapping parks the expensive byte planes on a
+// fraction of the chip (workgroups are dealt to XCDs / shader engines by index).
+constexpr int kRingLog = 15;   // 32 KiB LDS output ring per wave: 5 waves per CU
+
+__device__ __forceinline__ void decode_stream(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
+                                              DChunk* __restrict__ ch, const DStream& st, uint8_t* __restrict__ stage,
+                                              const uint8_t* __restrict__ maskout, B2H_LDS uint8_t* ring,
+                                              int32_t* kind_out) {
+  const int lane = lane_id();
   const int32_t c = st.chunk;
   const DChunk d = ch[c];
   if (d.status < 0 || st.neblock < 0) return;
@@ -809,19 +829,46 @@ __global__ __launch_bounds__(64) void k_decode(const uint8_t* const* __restrict_
   gin_t in = (gin_t)(srcs[c] + st.src);
   gout_t out = (gout_t)((d.nfilters_bwd ? stage + d.stage_off : dsts[c]) + st.dst_off);
   const int32_t nb = st.neblock;
-  const int lane = threadIdx.x;
   if (st.csize == 0) {
     wave_fill(out, 0, nb);
   } else if (st.csize < 0) {
     const uint8_t token = in[0];
-    if (!(token & 1) || st.csize < -255) { if (lane == 0) atomicMin(&ch[c].status, E_RUNLEN); return; }
-    wave_fill(out, (uint8_t)(-st.csize), nb);
+    if (!(token & 1) || st.csize < -255) {
+      if (lane == 0) atomicMin(&ch[c].status, E_RUNLEN);
+    } else {
+      wave_fill(out, (uint8_t)(-st.csize), nb);
+      *kind_out = 1;
+    }
   } else if (st.csize == nb) {
     wave_copy(out, in, nb);
+    *kind_out = 2;
+  } else if ((d.flags >> 5) != 0) {
+    if (lane == 0) atomicMin(&ch[c].status, E_CODEC);
   } else {
-    if ((d.flags >> 5) != 0) { if (lane == 0) atomicMin(&ch[c].status, E_CODEC); return; }
-    const int32_t got = wave_lz_decode(in, st.csize, out, nb);
+    const int32_t got = wave_lz_decode_par<kRingLog>(in, st.csize, out, nb, ring);
     if (got != nb && lane == 0) atomicMin(&ch[c].status, E_DATA);
+    *kind_out = 3;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_decode(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
+                                               DChunk* __restrict__ ch, const DStream* __restrict__ streams,
+                                               uint8_t* __restrict__ stage, int32_t nstreams_total,
+                                               const uint8_t* __restrict__ maskout, int32_t* __restrict__ next,
+                                               int64_t* __restrict__ dbg) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  B2H_LDS uint8_t* ring = (B2H_LDS uint8_t*)smem;
+  for (;;) {
+    // branch-free grab (see k_encode)
+    const int32_t s = __builtin_amdgcn_readfirstlane(atomicAdd(next, lane_id() == 0 ? 1 : 0));
+    if (s >= nstreams_total) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    int32_t kind = 0;
+    decode_stream(srcs, dsts, ch, streams[s], stage, maskout, ring, &kind);
+    if (dbg && lane_id() == 0) {
+      dbg[2 * s] = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
+      dbg[2 * s + 1] = kind;
+    }
   }
 }
 
@@ -917,8 +964,22 @@ int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint
     DBlock* blocks = ws->dblocks.as<DBlock>();
     DStream* streams = ws->dstreams.as<DStream>();
     k_dplan_blocks<<<(h.nblocks + 255) / 256, 256, 0, st>>>(d_src, d_srcsize, ch, n, blocks, streams, h.nblocks);
+    if (ws->dqctr.ensure(16)) return E_MEMORY;
+    int32_t* next = ws->dqctr.as<int32_t>();
     ev_decode.start(st);
-    k_decode<<<h.nstreams, 64, 0, st>>>(d_src, d_dst, ch, streams, ws->stage.as<uint8_t>(), h.nstreams, d_maskout);
+    HIPCHK(hipMemsetAsync(next, 0, sizeof(int32_t), st));
+    {
+      const size_t lds = size_t(1) << kRingLog;
+      const int slots = resident_slots(reinterpret_cast<const void*>(&k_decode), lds);
+      const uint32_t grid = (uint32_t)std::min<int64_t>(h.nstreams, slots);
+      int64_t* dbg = nullptr;
+      if (g_ddebug) {
+        if (ws->ddbg.ensure(sizeof(int64_t) * 2 * (size_t)h.nstreams)) return E_MEMORY;
+        dbg = ws->ddbg.as<int64_t>();
+      }
+      k_decode<<<grid, 64, lds, st>>>(d_src, d_dst, ch, streams, ws->stage.as<uint8_t>(), h.nstreams, d_maskout,
+                                      next, dbg);
+    }
     ev_decode.stop(st);
     ev_unfilter.start(st);
     if (h.max_filters > 0) {

@@ -417,79 +417,459 @@ __device__ __forceinline__ void wave_fill(gout_t o, uint8_t v, int32_t n) {
   for (int32_t i = h + n16 * 16 + lane; i < n; i += 64) o[i] = v;
 }
 
-// dst any alignment: aligned u32 stores, sources via ldu32 (8 readable slack bytes assumed).
+// dst any alignment: 16-byte aligned stores of 16 funnel-shifted source bytes per lane, four
+// 1 KiB rows in flight per step (the source is read with aligned dwords: never past the last
+// dword that holds a source byte).
 __device__ __forceinline__ void wave_copy(gout_t o, gin_t s, int32_t n) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const int lane = lane_id();
-  const int32_t head = (int32_t)((4 - (reinterpret_cast<uintptr_t>(o) & 3)) & 3);
+  const int32_t head = (int32_t)((16 - (reinterpret_cast<uintptr_t>(o) & 15)) & 15);
   const int32_t h = min(head, n);
   if (lane < h) o[lane] = s[lane];
-  B2H_GLB uint32_t* o4 = reinterpret_cast<B2H_GLB uint32_t*>(o + h);
-  const int32_t n4 = (n - h) / 4;
-  for (int32_t i = lane; i < n4; i += 64) o4[i] = ldu32(s + h + 4 * i);
-  for (int32_t i = h + n4 * 4 + lane; i < n; i += 64) o[i] = s[i];
+  const int32_t n16 = (n - h) / 16;
+  gin_t s1 = s + h;
+  B2H_GLB u32x4* o16 = reinterpret_cast<B2H_GLB u32x4*>(o + h);
+  const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(s1) & 3);
+  const B2H_GLB uint32_t* q0 = align4(s1);
+  // the 5th dword of the last 16-byte piece exists only if the source is misaligned
+  int32_t i = lane;
+  for (; i + 192 < n16; i += 256) {
+    uint32_t w[4][5];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const B2H_GLB uint32_t* q = q0 + 4 * (i + 64 * u);
+#pragma unroll
+      for (int k = 0; k < 4; k++) w[u][k] = q[k];
+      w[u][4] = sh ? q[4] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      u32x4 v;
+      v.x = funnel(w[u][0], w[u][1], sh);
+      v.y = funnel(w[u][1], w[u][2], sh);
+      v.z = funnel(w[u][2], w[u][3], sh);
+      v.w = funnel(w[u][3], w[u][4], sh);
+      o16[i + 64 * u] = v;
+    }
+  }
+  for (; i < n16; i += 64) {
+    const B2H_GLB uint32_t* q = q0 + 4 * i;
+    const uint32_t a = q[0], b = q[1], c = q[2], d = q[3], e = sh ? q[4] : 0u;
+    u32x4 v;
+    v.x = funnel(a, b, sh);
+    v.y = funnel(b, c, sh);
+    v.z = funnel(c, d, sh);
+    v.w = funnel(d, e, sh);
+    o16[i] = v;
+  }
+  for (int32_t j = h + n16 * 16 + lane; j < n; j += 64) o[j] = s[j];
 }
 
 // ------------------------------------------------------------------------------- decoder ----
-// Returns decoded bytes, or 0 on any violation (same conditions as the reference).  `out` is
-// global memory written and re-read by this wave: every token that reads earlier output first
-// waits for the wave's previous stores (workgroup-scope fence).
-__device__ __forceinline__ int32_t wave_lz_decode(gin_t in, int32_t length, gout_t out, int32_t maxout) {
+// Double-buffered register window over the compressed stream.  w0 holds stream bytes
+// [wpos, wpos + 256) (lane l: the aligned dword at wpos + 4 l), w1 the next 256; wpos is chosen so
+// that in + wpos is 4-byte aligned (it may be -1..-3).  Token bytes are read with readlane (no
+// memory round trip per token), literal runs with bpermute; w1 is loaded one window ahead.
+// Dwords at or past the stream end read as 0; an aligned dword holding a stream byte never
+// crosses a page, so the partial first/last dwords are safe to load.
+struct InWin {
+  uint32_t w0, w1;
+  int32_t wpos;
+};
+
+__device__ __forceinline__ uint32_t inwin_dword(gin_t in, int32_t length, int32_t pos) {
+  const int32_t mine = pos + 4 * lane_id();
+  return mine < length ? *reinterpret_cast<const B2H_GLB uint32_t*>(in + mine) : 0u;
+}
+
+__device__ __forceinline__ void inwin_reload(InWin& W, gin_t in, int32_t length, int32_t pos) {
+  W.wpos = pos - (int32_t)(reinterpret_cast<uintptr_t>(in + pos) & 3);
+  W.w0 = inwin_dword(in, length, W.wpos);
+  W.w1 = inwin_dword(in, length, W.wpos + 256);
+}
+
+// Make stream offset `pos` fall inside w0; returns its offset in w0 (0..255).
+__device__ __forceinline__ int32_t inwin_seek(InWin& W, gin_t in, int32_t length, int32_t pos) {
+  int32_t k = pos - W.wpos;
+  if (k >= 256) {
+    if (k < 512) {
+      W.w0 = W.w1;
+      W.wpos += 256;
+      W.w1 = inwin_dword(in, length, W.wpos + 256);
+    } else {
+      inwin_reload(W, in, length, pos);
+    }
+    k = pos - W.wpos;
+  }
+  return k;
+}
+
+// Four stream bytes starting at w0 offset k (0..255), little-endian.
+__device__ __forceinline__ uint32_t inwin_peek4(const InWin& W, int32_t k) {
+  const int li = k >> 2;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)W.w0, li);
+  const uint32_t hi = li < 63 ? (uint32_t)__builtin_amdgcn_readlane((int)W.w0, li + 1)
+                              : (uint32_t)__builtin_amdgcn_readlane((int)W.w1, 0);
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (k & 3)));
+}
+
+__device__ __forceinline__ uint32_t inwin_byte(InWin& W, gin_t in, int32_t length, int32_t pos) {
+  const int32_t k = inwin_seek(W, in, length, pos);
+  return ((uint32_t)__builtin_amdgcn_readlane((int)W.w0, k >> 2) >> (8 * (k & 3))) & 0xffu;
+}
+
+// Move output bytes [from, to) of the LDS ring to global memory (positions are stream offsets;
+// ring slot = position mod R).  16 B per lane when both sides are 16-byte aligned.
+template <int RLOG>
+__device__ __forceinline__ void ring_flush(const B2H_LDS uint8_t* ring, gout_t out, int32_t from, int32_t to) {
+  constexpr int32_t RM = (1 << RLOG) - 1;
+  const int lane = lane_id();
+  int32_t x = from;
+  if (((reinterpret_cast<uintptr_t>(out + x) & 15) == 0) && ((x & 15) == 0)) {
+    for (; x + 1024 <= to; x += 1024) {
+      const int32_t y = x + lane * 16;
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = *reinterpret_cast<const B2H_LDS u32x4*>(ring + (y & RM));
+      *reinterpret_cast<B2H_GLB u32x4*>(out + y) = v;
+    }
+  }
+  for (int32_t y = x + lane; y < to; y += 64) out[y] = ring[y & RM];
+}
+
+
+// Slow paths of the decoder, kept out of line on purpose: inlined, their loops and the flushes
+// made the token loop irreducible (the backend then wraps every token in a guard-variable
+// state machine, ~4x the instructions).  Called for copies longer than 64 bytes, sources older
+// than the ring, and ring flushes.  Returns the new flush frontier F.
+template <int RLOG>
+__device__ __noinline__ int32_t copy_general(B2H_LDS uint8_t* ring, gout_t out, int32_t op, int32_t src, int32_t len, int32_t dist, int32_t F) {
+  constexpr int32_t R = 1 << RLOG, RM = R - 1, PIECE = 4096, STEP = 1024;
+  const int lane = lane_id();
+  const bool overlap = dist < len;
+  const int32_t step = overlap ? 64 % dist : 0;
+  int32_t r = overlap ? lane % dist : 0;
+  for (int32_t done = 0; done < len; done += STEP) {
+    const int32_t n = min(len - done, STEP);
+    while (op + done + n - F > R) { ring_flush<RLOG>(ring, out, F, F + PIECE); F += PIECE; }
+    if (src < F) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    for (int32_t i = done + lane; i < done + n; i += 64) {
+      const int32_t y = overlap ? src + r : src + i;
+      const uint8_t b = y >= F ? ring[y & RM] : out[y];
+      ring[(op + i) & RM] = b;
+      if (overlap) { r += step; if (r >= dist) r -= dist; }
+    }
+  }
+  return F;
+}
+// Flush 4 KiB pieces until end - F <= ring size.
+template <int RLOG>
+__device__ __noinline__ int32_t flush_to(B2H_LDS uint8_t* ring, gout_t out, int32_t end, int32_t F) {
+  constexpr int32_t R = 1 << RLOG, PIECE = 4096;
+  while (end - F > R) { ring_flush<RLOG>(ring, out, F, F + PIECE); F += PIECE; }
+  return F;
+}
+// BloscLZ stream decode (blosc/blosclz.c:685-795).  Returns decoded bytes, or 0 on any violation
+// (same conditions and order as the reference).  Output goes through an LDS ring of 2^RLOG bytes:
+// matches read their source from the ring (in-order LDS per wave: no fences), and bytes leave for
+// `out` in 4 KiB pieces once they are more than one ring behind.  A source older than the ring
+// (distance > ring, rare) is read back from `out` after a fence.  One register peek per token;
+// matches up to 64 bytes and literal runs are one LDS read + write per lane.
+template <int RLOG>
+__device__ __forceinline__ int32_t wave_lz_decode_ring(gin_t in, int32_t length, gout_t out, int32_t maxout,
+                                                       B2H_LDS uint8_t* ring) {
+  constexpr int32_t R = 1 << RLOG, RM = R - 1;
   const int lane = lane_id();
   if (length == 0) return 0;
-  int32_t ip = 0, op = 0;
-  uint32_t ctrl = in[ip++] & 31u;
+  InWin W;
+  inwin_reload(W, in, length, 0);
+  int32_t ip = 0, op = 0, F = 0;   // ip: the current ctrl byte; output [0, F) already in `out`
+  // the first ctrl is read as byte0 & 31 (blosc/blosclz.c:694): clear its top bits in the
+  // register window (ip never returns to 0) instead of carrying a first-token flag, which the
+  // compiler would thread into a second loop entry (irreducible -> state machine)
+  if (lane == 0) W.w0 &= ~(0xe0u << (8 * (-W.wpos)));
+  // make the entry values opaque: with ip = 0 known on the entry edge the compiler threads that
+  // edge past the window check into the loop body (a second loop entry -> irreducible loop ->
+  // guard-variable state machine around every token)
+  asm volatile("" : "+s"(ip), "+s"(W.wpos));
   for (;;) {
+    const int32_t k = inwin_seek(W, in, length, ip);
+    const uint32_t t = inwin_peek4(W, k);
+    const uint32_t ctrl = t & 0xffu;
+    int32_t p = ip + 1;   // the reference's ip after reading ctrl
     if (ctrl >= 32) {
-      int32_t len = (int32_t)(ctrl >> 5) - 1;
+      int32_t len = (int32_t)(ctrl >> 5) + 2;
       const int32_t ofs = (int32_t)(ctrl & 31u) << 8;
-      uint32_t code;
-      if (len == 6) {
+      int32_t dist;
+      if (len == 9) {   // length extension bytes
+        uint32_t code;
+        len = 6;
         do {
-          if (ip + 1 >= length) return 0;
-          code = in[ip++];
+          if (p + 1 >= length) return 0;
+          code = inwin_byte(W, in, length, p++);
           len += (int32_t)code;
         } while (code == 255);
-      } else if (ip + 1 >= length) {
-        return 0;
-      }
-      code = in[ip++];
-      len += 3;
-      int32_t dist = ofs + (int32_t)code + 1;   // op - ref after the reference's ref--
-      if (code == 255 && ofs == (31 << 8)) {
-        if (ip + 1 >= length) return 0;
-        dist = (((int32_t)in[ip] << 8) | in[ip + 1]) + (int32_t)kLzNear + 1;
-        ip += 2;
+        code = inwin_byte(W, in, length, p++);
+        len += 3;
+        dist = ofs + (int32_t)code + 1;
+        if (code == 255 && ofs == (31 << 8)) {
+          if (p + 1 >= length) return 0;
+          const uint32_t hi = inwin_byte(W, in, length, p), lo = inwin_byte(W, in, length, p + 1);
+          dist = (int32_t)((hi << 8) | lo) + (int32_t)kLzNear + 1;
+          p += 2;
+        }
+      } else {
+        if (p + 1 >= length) return 0;
+        const uint32_t code = (t >> 8) & 0xffu;
+        p += 1;
+        dist = ofs + (int32_t)code + 1;   // op - ref after the reference's ref--
+        if (code == 255 && ofs == (31 << 8)) {
+          if (p + 1 >= length) return 0;
+          dist = (int32_t)((((t >> 16) & 0xffu) << 8) | (t >> 24)) + (int32_t)kLzNear + 1;
+          p += 2;
+        }
       }
       if (op + len > maxout) return 0;
       if (op - dist < 0) return 0;
-      if (ip >= length) break;   // a trailing match is dropped (blosc/blosclz.c:742)
-      ctrl = in[ip++];
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      if (p >= length) break;   // a trailing match is dropped (blosc/blosclz.c:742)
       const int32_t src = op - dist;
-      if (dist >= len) {
-        for (int32_t i = lane; i < len; i += 64) out[op + i] = out[src + i];
+      if (len <= 64 && src >= F && op + len - F <= R) {
+        // overlapping copies replicate the period `dist`: every source byte precedes this token
+        const int32_t yl = dist < len ? lane % dist : lane;
+        if (lane < len) ring[(op + lane) & RM] = ring[(src + yl) & RM];
       } else {
-        // overlapping: period `dist`, every source byte precedes this token
-        const int32_t step = 64 % dist;
-        int32_t r = lane % dist;
-        for (int32_t i = lane; i < len; i += 64) {
-          out[op + i] = out[src + r];
-          r += step;
-          if (r >= dist) r -= dist;
-        }
+        F = copy_general<RLOG>(ring, out, op, src, len, dist, F);
       }
       op += len;
     } else {
       const int32_t run = (int32_t)ctrl + 1;
       if (op + run > maxout) return 0;
-      if (ip + run > length) return 0;
-      if (lane < run) out[op + lane] = in[ip + lane];
+      if (p + run > length) return 0;
+      if (op + run - F > R) F = flush_to<RLOG>(ring, out, op + run, F);
+      // bytes [p, p + run) sit at w0 offsets k + 1 .. k + run (< 288): w0, spilling into w1
+      const int32_t idx = k + 1 + lane;
+      uint32_t v = (uint32_t)__shfl((int)W.w0, idx >> 2);
+      if (k + 1 + run > 256) {
+        const uint32_t v1 = (uint32_t)__shfl((int)W.w1, (idx >> 2) & 63);
+        v = idx >= 256 ? v1 : v;
+      }
+      if (lane < run) ring[(op + lane) & RM] = (uint8_t)(v >> (8 * (idx & 3)));
       op += run;
-      ip += run;
-      if (ip >= length) break;
-      ctrl = in[ip++];
+      p += run;
+      if (p >= length) break;
+    }
+    ip = p;
+  }
+  ring_flush<RLOG>(ring, out, F, op);
+  return op;
+}
+
+// ------------------------------------------------------------- window-parallel decoder ----
+// Wave64 inclusive scans with DPP (row shifts inside 16-lane rows, then row broadcasts 15/31).
+// `id` is the identity of the operation: lanes whose DPP source is masked or out of row read it.
+__device__ __forceinline__ int32_t wave_scan_add(int32_t v) {
+  int32_t r = v;
+  r += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+  r += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+  r += __builtin_amdgcn_update_dpp(0, v, 0x113, 0xf, 0xf, false);   // row_shr:3
+  r += __builtin_amdgcn_update_dpp(0, r, 0x114, 0xf, 0xe, false);   // row_shr:4, banks 1-3
+  r += __builtin_amdgcn_update_dpp(0, r, 0x118, 0xf, 0xc, false);   // row_shr:8, banks 2-3
+  r += __builtin_amdgcn_update_dpp(0, r, 0x142, 0xa, 0xf, false);   // row_bcast:15, rows 1,3
+  r += __builtin_amdgcn_update_dpp(0, r, 0x143, 0xc, 0xf, false);   // row_bcast:31, rows 2,3
+  return r;
+}
+__device__ __forceinline__ int32_t wave_scan_max(int32_t v) {   // values >= -1
+  int32_t r = v;
+  r = max(r, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));
+  r = max(r, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));
+  r = max(r, __builtin_amdgcn_update_dpp(-1, v, 0x113, 0xf, 0xf, false));
+  r = max(r, __builtin_amdgcn_update_dpp(-1, r, 0x114, 0xf, 0xe, false));
+  r = max(r, __builtin_amdgcn_update_dpp(-1, r, 0x118, 0xf, 0xc, false));
+  r = max(r, __builtin_amdgcn_update_dpp(-1, r, 0x142, 0xa, 0xf, false));
+  r = max(r, __builtin_amdgcn_update_dpp(-1, r, 0x143, 0xc, 0xf, false));
+  return r;
+}
+
+// Four bytes at (lane-varying) offset q of the 512-byte register window w0|w1 (q <= 504).
+__device__ __forceinline__ uint32_t win_dword(const InWin& W, int32_t q) {
+  const int32_t d = q >> 2;
+  const uint32_t a = (uint32_t)__shfl((int)W.w0, d), a1 = (uint32_t)__shfl((int)W.w1, d & 63);
+  const uint32_t b = (uint32_t)__shfl((int)W.w0, (d + 1) & 63), b1 = (uint32_t)__shfl((int)W.w1, (d + 1) & 63);
+  return funnel(d < 64 ? a : a1, d + 1 < 64 ? b : b1, (uint32_t)(q & 3));
+}
+
+// BloscLZ stream decode, window-parallel (same results and rejections as wave_lz_decode_ring,
+// blosc/blosclz.c:685-795).  Per window of 64 candidate token starts ip + lane:
+//   1. every lane parses the token that would start at its byte (2..5 header bytes from the
+//      register window) -> kind, size, output length, distance;
+//   2. the true token chain from ip is walked with one readlane per token (s += size[s]);
+//   3. a DPP scan over the chain gives every token's output offset; bound violations (maxout,
+//      distance before the output start), tokens near the stream end and multi-byte length
+//      extensions end the batch and are decoded one at a time by the serial token code;
+//   4. all literal bytes of the batch are written at once (each byte lane finds its token with a
+//      max-scan), then the matches are copied in order (sources always precede the token, so
+//      literals-first is safe).
+template <int RLOG>
+__device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, gout_t out, int32_t maxout,
+                                                      B2H_LDS uint8_t* ring) {
+  constexpr int32_t R = 1 << RLOG, RM = R - 1, WMAX = 8192;
+  const int lane = lane_id();
+  if (length == 0) return 0;
+  InWin W;
+  inwin_reload(W, in, length, 0);
+  int32_t ip = 0, op = 0, F = 0;
+  int32_t result = -1;   // -1 running, 0 rejected
+  if (lane == 0) W.w0 &= ~(0xe0u << (8 * (-W.wpos)));   // first ctrl is byte0 & 31
+  asm volatile("" : "+s"(ip), "+s"(W.wpos));
+  for (;;) {
+    const int32_t k = inwin_seek(W, in, length, ip);
+    // ---- 1. parse every candidate start ----
+    const int32_t P = ip + lane;
+    const uint32_t lo32 = win_dword(W, k + lane), hi32 = win_dword(W, k + lane + 4);
+    const uint32_t ctrl = lo32 & 0xffu, b1 = (lo32 >> 8) & 0xffu, b2 = (lo32 >> 16) & 0xffu,
+                   b3 = lo32 >> 24, b4 = hi32 & 0xffu;
+    const bool lit = ctrl < 32;
+    const bool ext = (ctrl >> 5) == 7;
+    const uint32_t code = ext ? b2 : b1;
+    const uint32_t ofs = (ctrl & 31u) << 8;
+    const bool far = !lit && code == 255 && ofs == (31u << 8);
+    const int32_t mlen = ext ? 9 + (int32_t)b1 : (int32_t)(ctrl >> 5) + 2;
+    const int32_t dist = far ? (int32_t)(((ext ? b3 : b2) << 8) | (ext ? b4 : b3)) + (int32_t)kLzNear + 1
+                             : (int32_t)(ofs + code) + 1;
+    const int32_t size = lit ? (int32_t)ctrl + 2 : 2 + (ext ? 1 : 0) + (far ? 2 : 0);
+    const int32_t olen = lit ? (int32_t)ctrl + 1 : mlen;
+    const bool special = (ext && b1 == 255) || (P + 8 > length) || (P + size >= length);
+    // ---- 2. chain walk ----
+    const int32_t step = special ? 128 : size;
+    uint64_t chain = 0;
+    int32_t s = 0;
+    do {
+      chain |= 1ull << s;
+      s += __builtin_amdgcn_readlane(step, s);
+    } while (s < 64);
+    const uint64_t spec = chain & __ballot(special);
+    int32_t st = spec ? __builtin_ctzll(spec) : 64;   // first token for the serial path
+    uint64_t batch = chain & (st < 64 ? (1ull << st) - 1 : ~0ull);
+    // ---- 3. output offsets and bound checks ----
+    const bool inb = (batch >> lane) & 1ull;
+    const int32_t v = inb ? olen : 0;
+    const int32_t ex = wave_scan_add(v) - v;   // exclusive: output offset of lane's token - op
+    const bool viol = inb && (op + ex + olen > maxout || (!lit && op + ex < dist) || ex + olen > WMAX);
+    const uint64_t vm = __ballot(viol);
+    if (vm) {
+      st = __builtin_ctzll(vm);
+      batch &= (1ull << st) - 1;
+    }
+    int32_t nip, nop;
+    if (st < 64) {
+      nip = ip + st;
+      nop = op + __builtin_amdgcn_readlane(ex, st);
+    } else {
+      nip = ip + s;
+      nop = op + __builtin_amdgcn_readlane(ex + v, 63);
+    }
+    if (batch) {
+      if (nop - F > R) F = flush_to<RLOG>(ring, out, nop, F);
+      // ---- 4a. literal bytes: byte lane x belongs to the last batch token at or before it ----
+      const int32_t owner = wave_scan_max(inb ? lane : -1);
+      const uint32_t opk = (uint32_t)(ex << 6) | (uint32_t)(lit ? olen : 0);   // ex < 2^13, run <= 32
+      const uint32_t ow_pk = (uint32_t)__shfl((int)opk, owner & 63);
+      const int32_t orun = (int32_t)(ow_pk & 63u), oex = (int32_t)(ow_pk >> 6);
+      if (owner >= 0 && lane > owner && lane <= owner + orun)
+        ring[(op + oex + (lane - owner - 1)) & RM] = (uint8_t)ctrl;   // ctrl = the byte at ip + lane
+      const int32_t last = 63 - __builtin_clzll(batch);
+      const uint32_t last_pk = (uint32_t)__builtin_amdgcn_readlane((int)opk, last);
+      const int32_t lrun = (int32_t)(last_pk & 63u);
+      if (last + lrun >= 64) {   // the last literal run spills past the 64 parsed bytes
+        const int32_t x = 64 + lane;
+        const uint32_t byte = win_dword(W, k + x) & 0xffu;
+        if (x <= last + lrun) ring[(op + (int32_t)(last_pk >> 6) + (x - last - 1)) & RM] = (uint8_t)byte;
+      }
+      // ---- 4b. matches in order ----
+      uint64_t mm = batch & ~__ballot(lit);
+      while (mm) {
+        const int j = __builtin_ctzll(mm);
+        mm &= mm - 1;
+        const int32_t oj = op + __builtin_amdgcn_readlane(ex, j);
+        const int32_t lj = __builtin_amdgcn_readlane(olen, j);
+        const int32_t dj = __builtin_amdgcn_readlane(dist, j);
+        const int32_t src = oj - dj;
+        if (lj <= 64 && src >= F) {
+          const int32_t yl = dj < lj ? lane % dj : lane;
+          if (lane < lj) ring[(oj + lane) & RM] = ring[(src + yl) & RM];
+        } else {
+          F = copy_general<RLOG>(ring, out, oj, src, lj, dj, F);
+        }
+      }
+      ip = nip;
+      op = nop;
+    }
+    if (st >= 64) continue;
+    // ---- one token the serial way (ip is its ctrl byte) ----
+    {
+      const int32_t k2 = inwin_seek(W, in, length, ip);
+      const uint32_t t = inwin_peek4(W, k2);
+      const uint32_t c = t & 0xffu;
+      int32_t p = ip + 1;
+      if (c >= 32) {
+        int32_t len = (int32_t)(c >> 5) + 2;
+        const int32_t of = (int32_t)(c & 31u) << 8;
+        int32_t dd;
+        bool bad = false;
+        if (len == 9) {
+          uint32_t cd;
+          len = 6;
+          do {
+            if (p + 1 >= length) { bad = true; break; }
+            cd = inwin_byte(W, in, length, p++);
+            len += (int32_t)cd;
+          } while (cd == 255);
+          if (bad) { result = 0; break; }
+          cd = inwin_byte(W, in, length, p++);
+          len += 3;
+          dd = of + (int32_t)cd + 1;
+          if (cd == 255 && of == (31 << 8)) {
+            if (p + 1 >= length) { result = 0; break; }
+            const uint32_t hi = inwin_byte(W, in, length, p), lo = inwin_byte(W, in, length, p + 1);
+            dd = (int32_t)((hi << 8) | lo) + (int32_t)kLzNear + 1;
+            p += 2;
+          }
+        } else {
+          if (p + 1 >= length) { result = 0; break; }
+          const uint32_t cd = (t >> 8) & 0xffu;
+          p += 1;
+          dd = of + (int32_t)cd + 1;
+          if (cd == 255 && of == (31 << 8)) {
+            if (p + 1 >= length) { result = 0; break; }
+            dd = (int32_t)((((t >> 16) & 0xffu) << 8) | (t >> 24)) + (int32_t)kLzNear + 1;
+            p += 2;
+          }
+        }
+        if (op + len > maxout || op - dd < 0) { result = 0; break; }
+        if (p >= length) break;   // a trailing match is dropped (blosc/blosclz.c:742)
+        const int32_t src = op - dd;
+        if (len <= 64 && src >= F && op + len - F <= R) {
+          const int32_t yl = dd < len ? lane % dd : lane;
+          if (lane < len) ring[(op + lane) & RM] = ring[(src + yl) & RM];
+        } else {
+          F = copy_general<RLOG>(ring, out, op, src, len, dd, F);
+        }
+        op += len;
+      } else {
+        const int32_t run = (int32_t)c + 1;
+        if (op + run > maxout || p + run > length) { result = 0; break; }
+        if (op + run - F > R) F = flush_to<RLOG>(ring, out, op + run, F);
+        const int32_t k3 = inwin_seek(W, in, length, p);
+        const uint32_t byte = win_dword(W, k3 + lane) & 0xffu;
+        if (lane < run) ring[(op + lane) & RM] = (uint8_t)byte;
+        op += run;
+        p += run;
+        if (p >= length) break;
+      }
+      ip = p;
     }
   }
+  if (result == 0) return 0;
+  ring_flush<RLOG>(ring, out, F, op);
   return op;
 }
 

@@ -256,3 +256,50 @@ def test_c2_shuffle_256mib_roundtrip(B):
     L.b2h_shuffle(4, n, C.c_void_p(o.data_ptr()), C.c_void_p(back.data_ptr()), 1, None)
     torch.cuda.synchronize()
     assert torch.equal(back, d)
+
+
+def _far_match_data(n, seed):
+    """Streams whose matches reach further back than the decoder's LDS ring (32 KiB): a 20 KB
+    random segment repeated every 36 KB (zeros and a short period in between)."""
+    rng = np.random.default_rng(seed)
+    a = rng.integers(0, 256, 20_000, dtype=np.uint8)
+    parts = []
+    while sum(p.nbytes for p in parts) < n:
+        parts += [a, np.zeros(14_000, np.uint8), np.tile(rng.integers(0, 256, 5, dtype=np.uint8), 400)]
+    return np.concatenate(parts)[:n]
+
+
+@pytest.mark.parametrize("bs", [65536, 262144])
+@pytest.mark.parametrize("clevel", [1, 5, 9])
+def test_far_matches_long_streams(B, bs, clevel):
+    """Single-stream blocks (typesize 1) of 64 / 256 KiB: LZ distances up to the far limit, match
+    sources older than the decoder's LDS ring; compress == oracle, decompress round-trips."""
+    src = _far_match_data(3 * bs + 1000, clevel * 31 + bs)
+    kw = dict(clevel=clevel, typesize=1, filters=(0, 0, 0, 0, 0, 0), blocksize=bs)
+    want = oracle_compress(src, **kw)
+    got = B.compress(src, **kw)
+    assert isinstance(got, np.ndarray) and np.array_equal(got, want)
+    assert want.nbytes < 0.8 * src.nbytes        # the far matches were actually taken
+    dec = B.decompress(got, src.nbytes)
+    assert isinstance(dec, np.ndarray) and np.array_equal(dec, src)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_corrupted_streams_match_oracle(B, seed):
+    """Damaged LZ payloads: the device decoder accepts / rejects exactly like the oracle
+    (blosclz_decompress bound checks, blosc_d's size check), and agrees on the bytes it accepts."""
+    rng = np.random.default_rng(seed)
+    src = gen_f32(seed << 20, 1 << 16)
+    good = oracle_compress(src, clevel=5, typesize=4)
+    hdr = 32 + 4 * ((src.nbytes + 262143) // 262144)
+    for _ in range(25):
+        bad = good.copy()
+        k = int(rng.integers(1, 4))
+        for pos in rng.integers(hdr + 4, bad.nbytes, k):
+            bad[pos] ^= np.uint8(1 << int(rng.integers(0, 8)))
+        o = oracle_decompress(bad, src.nbytes)
+        g = B.decompress(bad, src.nbytes)
+        if isinstance(o, np.ndarray):
+            assert isinstance(g, np.ndarray) and np.array_equal(g, o)
+        else:
+            assert not isinstance(g, np.ndarray) and g < 0
