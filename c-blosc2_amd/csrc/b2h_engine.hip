@@ -215,6 +215,7 @@ __global__ __launch_bounds__(64) void k_encode(CGeom g, const uint8_t* __restric
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
   volatile B2H_LDS POS* htab = (volatile B2H_LDS POS*)(smem);
   volatile B2H_LDS uint32_t* tagm = (volatile B2H_LDS uint32_t*)(smem + (sizeof(POS) << hashlog));
+  B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + (sizeof(POS) << hashlog) + 4 * kTagBuckets);
   for (;;) {
     // branch-free grab: every lane takes part (lane 0 adds 1, the others 0), so no divergent
     // region sits between the atomic and the broadcast -- with a lane-0 branch the structurizer
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(64) void k_encode(CGeom g, const uint8_t* __restric
     gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide time base
-    StreamResult r = encode_stream<POS>(in, len, g.clevel, out, htab, tagm, g.overhead == kHdrExt);
+    StreamResult r = encode_stream<POS>(in, len, g.clevel, out, htab, tagm, oring, g.overhead == kHdrExt);
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
     if (lane_id() == 0) res[s] = r;
@@ -589,7 +590,7 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
   {
     const void* fn = small ? reinterpret_cast<const void*>(&k_encode<uint16_t>)
                            : reinterpret_cast<const void*>(&k_encode<uint32_t>);
-    const size_t lds = ((small ? sizeof(uint16_t) : sizeof(uint32_t)) << hashlog) + 4 * kTagBuckets;
+    const size_t lds = enc_lds_bytes(small ? sizeof(uint16_t) : sizeof(uint32_t), hashlog);
     static bool attr_set = false;
     if (!attr_set) {   // > 64 KiB of dynamic LDS per workgroup: opt in once
       HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_encode<uint32_t>),

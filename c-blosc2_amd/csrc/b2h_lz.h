@@ -33,7 +33,14 @@
 
 namespace b2h {
 
-constexpr int kTagBuckets = 2048;   // window bucket-repeat detector (u32 per bucket, LDS)
+constexpr int kTagBuckets = 1536;   // window bucket-repeat detector (u32 per bucket, LDS)
+constexpr int kOutRing = 2048;      // encoder output staging ring (LDS), flushed in 512 B pieces
+// LDS per encoder wave: hash table + tags + output ring = 40 KiB for 64 KiB streams (4 per CU)
+__host__ __device__ constexpr size_t enc_lds_bytes(size_t pos_bytes, int hashlog) {
+  return (pos_bytes << hashlog) + 4 * kTagBuckets + kOutRing;
+}
+// tag bucket of a hash: any fixed map works (a shared bucket only ends a window early)
+__device__ __forceinline__ uint32_t tag_bucket(uint32_t h, int hashlog) { return (h * 3u) >> (hashlog - 9); }
 
 // Explicit address spaces: generic (flat) pointers would turn every access into a flat_* op,
 // which couples vmcnt and lgkmcnt waits and serialises LDS behind global traffic.
@@ -79,6 +86,17 @@ __device__ __forceinline__ void ld16(gin_t p, uint32_t (&w)[4]) {
   w[3] = funnel(d, e, sh);
 }
 
+// 28 unaligned bytes as seven words (8 dword loads).
+__device__ __forceinline__ void ld28(gin_t p, uint32_t (&w)[7]) {
+  const B2H_GLB uint32_t* q = align4(p);
+  const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+  uint32_t d[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) d[i] = q[i];
+#pragma unroll
+  for (int i = 0; i < 7; i++) w[i] = funnel(d[i], d[i + 1], sh);
+}
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 __device__ __forceinline__ int32_t rdlane(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -122,13 +140,39 @@ struct LzPassOut {
   int32_t windows;
 };
 
+#ifdef B2H_ENC_PROF   // diagnostics build only (tools/enc_micro.hip): per-phase s_memtime sums
+__device__ uint64_t g_enc_prof[16];
+#define EPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define EPROF_USE(x) asm volatile("" :: "v"(x))
+#define EPROF_DECL uint64_t eprof[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define EPROF_ADD(i, a, b) eprof[i] += (b) - (a)
+#define EPROF_FLUSH                                                                            \
+  if (lane == 0)                                                                               \
+    for (int i_ = 0; i_ < 8; i_++) atomicAdd((unsigned long long*)&g_enc_prof[(PROBE ? 8 : 0) + i_], eprof[i_])
+#else
+#define EPROF_T(v)
+#define EPROF_USE(x)
+#define EPROF_DECL
+#define EPROF_ADD(i, a, b)
+#define EPROF_FLUSH
+#endif
+
 // One greedy parse.  PROBE: get_cratio (counts only, limit = min(length, 2^hashlog), no far
 // short-match rule, no clevel-9 double rehash, no tail).  !PROBE: the emitting main loop + tail.
 template <bool PROBE, typename POS>
 __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashlog, int clevel, gout_t out,
                                              int32_t maxout, volatile B2H_LDS POS* htab,
-                                             volatile B2H_LDS uint32_t* tagm) {
+                                             volatile B2H_LDS uint32_t* tagm, B2H_LDS uint8_t* oring) {
   const int lane = lane_id();
+  // Output bytes are staged in an LDS ring and leave for `out` in 512-byte pieces once they are
+  // final: global stores share vmcnt with loads on CDNA, so a byte store per token would make
+  // every following input load wait for the store round trip.
+  constexpr int32_t ORM = kOutRing - 1;
+  int32_t F = 0;   // output [0, F) already in `out`
+  auto flush = [&](int32_t to) {
+    for (int32_t y = F + lane; y < to; y += 64) out[y] = oring[y & ORM];
+    F = to;
+  };
   int32_t limit = length;
   if (PROBE) {
     const int32_t hl = 1 << hashlog;
@@ -154,22 +198,27 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
     pos = 0;
   } else {
     pos = 4;
-    if (lane < 5) out[lane] = lane == 0 ? (uint8_t)(kLzMaxCopy - 1) : in[lane - 1];
+    if (lane < 5) oring[lane] = lane == 0 ? (uint8_t)(kLzMaxCopy - 1) : in[lane - 1];
   }
   int32_t peak = 0;
   bool fail = false;
+  EPROF_DECL;
 
   while (pos < loop_end) {
     windows++;
+    if (!PROBE && o - F >= 1024) flush(F + 512);   // a window emits < 512 bytes
+    EPROF_T(t0);
     const int32_t P = pos;
     const int32_t p = P + lane;
     const bool valid = p < loop_end;
-    uint32_t v = 0, a1 = 0, a2 = 0;
-    if (valid) ld12(in + p, v, a1, a2);
+    uint32_t a[7] = {0, 0, 0, 0, 0, 0, 0};   // in[p .. p+27]
+    if (valid) ld28(in + p, a);
+    const uint32_t v = a[0];
+    EPROF_T(t1);
     const uint32_t h = lz_hash(v, hashlog);
     const uint32_t c0 = valid ? (uint32_t)htab[h] : 0u;
     // W: first lane whose bucket already occurs at an earlier lane of the window
-    const uint32_t b = h & (kTagBuckets - 1);
+    const uint32_t b = tag_bucket(h, hashlog);
     if (valid) __hip_atomic_fetch_min((B2H_LDS uint32_t*)&tagm[b], (uint32_t)lane, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_WORKGROUP);
     const uint32_t minl = valid ? tagm[b] : (uint32_t)lane;
@@ -183,23 +232,31 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
     int32_t W = dup ? __builtin_ctzll(dup) : 64;
     W = min(W, min(64, loop_end - P));
 
+    EPROF_T(t2);
     // candidate test (lanes < W): literal or match, exactly as the serial loop decides
     const uint32_t cand = same1 ? (uint32_t)(p - 1) : c0;
     const uint32_t dist = (uint32_t)(p - (int32_t)cand);
+    // 28 bytes are compared up front; only longer matches need the cooperative extension
     bool accept = false;
-    int32_t m12 = 0, len = 0;
+    int32_t lenx = 0;   // match length, or -1: the first 28 bytes all match (extend later)
     if (lane < W && dist != 0 && dist < kLzFar) {
-      uint32_t r0, r1, r2;
-      ld12(in + cand, r0, r1, r2);
-      if (r0 == v) {
-        const uint32_t x1 = a1 ^ r1, x2 = a2 ^ r2;
-        m12 = x1 ? 4 + (__builtin_ctz(x1) >> 3) : (x2 ? 8 + (__builtin_ctz(x2) >> 3) : 12);
-        const int32_t e = min(m12 < 12 ? p + m12 + 1 : 0x7fffffff, bound);
-        len = e - 4 - p;
+      uint32_t r[7];
+      ld28(in + cand, r);
+      if (r[0] == v) {
+        int32_t mm = 28;   // index of the first mismatching byte
+#pragma unroll
+        for (int i = 6; i >= 1; i--) {
+          const uint32_t x = a[i] ^ r[i];
+          if (x) mm = 4 * i + (__builtin_ctz(x) >> 3);
+        }
+        const int32_t e = min(mm < 28 ? p + mm + 1 : 0x7fffffff, bound);
+        const int32_t len = e - 4 - p;
         accept = len >= 4 && (PROBE || !(len <= 5 && (dist - 1) >= kLzNear));
+        lenx = mm < 28 ? len : -1;
       }
     }
     const uint64_t am = __ballot(accept);
+    EPROF_T(t3);
 
     // scalar walk of the window
     int32_t cur = 0;
@@ -211,6 +268,7 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
     for (;;) {
       const uint64_t rem = cur < 64 ? (am & (~0ull << cur)) : 0ull;
       const int32_t m = rem ? __builtin_ctzll(rem) : W;
+      EPROF_T(tl0);
       if (m > cur) {   // literals [cur, m)
         const int32_t cnt = m - cur;
         if (!PROBE) {
@@ -220,62 +278,82 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
           if (lane >= cur && lane < m) {
             const int32_t k = lane - cur;
             const int32_t off = o + k + (lit + k) / 32;
-            out[off] = (uint8_t)(v & 0xffu);
-            if (((lit + k + 1) & 31) == 0) out[off + 1] = (uint8_t)(kLzMaxCopy - 1);
+            oring[off & ORM] = (uint8_t)(v & 0xffu);
+            if (((lit + k + 1) & 31) == 0) oring[(off + 1) & ORM] = (uint8_t)(kLzMaxCopy - 1);
           }
         }
         o += cnt + (lit + cnt) / 32;
         lit = (lit + cnt) & 31;
         visit |= (m >= 64 ? ~0ull : ((1ull << m) - 1)) & (~0ull << cur);
       }
+      EPROF_T(tl1);
+      EPROF_ADD(7, tl0, tl1);
       if (!rem) { next_pos = P + W; break; }
       // ---- the match of lane m ----
       visit |= 1ull << m;
       const int32_t pm = P + m;
-      const uint32_t dm = (uint32_t)pm - (uint32_t)rdlane((int32_t)cand, m);
-      int32_t lm = rdlane(len, m);
-      if (rdlane(m12, m) == 12) lm = wave_match_end(in, pm + 12, dm, bound) - 4 - pm;
+      const uint32_t dm = (uint32_t)rdlane((int32_t)dist, m);
+      int32_t lm = rdlane(lenx, m);
+      if (lm < 0) {
+        EPROF_T(te0);
+        lm = wave_match_end(in, pm + 28, dm, bound) - 4 - pm;
+        EPROF_T(te1);
+        EPROF_ADD(5, te0, te1);
+      }
       const uint32_t bd = dm - 1;   // biased distance
-      if (lit) {   // close the open literal run
-        if (!PROBE) {
-          const int32_t at = o - lit - 1;
-          if (lane == 0) out[at] = (uint8_t)(lit - 1);
-          if (at == 0) byte0 = (uint32_t)(lit - 1);
-        }
+      const uint32_t ulen = (uint32_t)lm;
+      const bool near = bd < kLzNear;
+      int32_t at = -1;   // header of the literal run this match closes (patched below)
+      const uint32_t hdr = (uint32_t)(lit - 1);
+      if (lit) {
+        at = o - lit - 1;
+        if (!PROBE && at == 0) byte0 = hdr;
       } else {
         o--;
       }
       lit = 0;
-      const uint32_t ulen = (uint32_t)lm;
-      if (PROBE) {
-        if (ulen >= 7) o += (int32_t)((ulen - 7) / 255) + 1;
-        o += bd < kLzNear ? 2 : 4;
-      } else {
-        const bool near = bd < kLzNear;
+      const int32_t ext = ulen >= 7 ? (int32_t)((ulen - 7) / 255) : 0;   // 255 bytes
+      const int32_t tok = ulen < 7 ? (near ? 2 : 4) : 1 + ext + (near ? 2 : 4);
+      if (!PROBE) {
+        // every bound check of the token and of the literal marker after it is <= o + tok + 1
+        peak = max(peak, o + tok + 1);
+        if (o + tok + 1 > maxout) { fail = true; break; }
         const uint32_t fd = bd - kLzNear;
-        const int32_t ext = ulen >= 7 ? (int32_t)((ulen - 7) / 255) : 0;   // 255 bytes
-        const int32_t tok = ulen < 7 ? (near ? 2 : 4) : 1 + ext + (near ? 2 : 4);
-        // every bound check of a token is <= the offset after the token: one check suffices
-        peak = max(peak, o + tok);
-        if (o + tok > maxout) { fail = true; break; }
-        if (ulen < 7) {
-          if (lane == 0) {
-            if (near) { out[o] = (uint8_t)((ulen << 5) + (bd >> 8)); out[o + 1] = (uint8_t)(bd & 255); }
-            else { out[o] = (uint8_t)((ulen << 5) + 31); out[o + 1] = 255; out[o + 2] = (uint8_t)(fd >> 8); out[o + 3] = (uint8_t)(fd & 255); }
+        if (ext == 0) {
+          // token bytes + the marker that opens the next literal run, little-endian in a u64:
+          // one LDS write instruction (lanes 0..nb-1), the run header from lane 63
+          uint64_t tb;
+          int32_t nb;
+          if (ulen < 7) {
+            if (near) { tb = (uint64_t)((ulen << 5) + (bd >> 8)) | ((uint64_t)(bd & 255) << 8) | (31ull << 16); nb = 3; }
+            else { tb = (uint64_t)((ulen << 5) + 31) | (255ull << 8) | ((uint64_t)(fd >> 8) << 16) | ((uint64_t)(fd & 255) << 24) | (31ull << 32); nb = 5; }
+          } else {
+            const uint64_t rl = ulen - 7;
+            if (near) { tb = (uint64_t)((7u << 5) + (bd >> 8)) | (rl << 8) | ((uint64_t)(bd & 255) << 16) | (31ull << 24); nb = 4; }
+            else { tb = (uint64_t)((7u << 5) + 31) | (rl << 8) | (255ull << 16) | ((uint64_t)(fd >> 8) << 24) | ((uint64_t)(fd & 255) << 32) | (31ull << 40); nb = 6; }
           }
+          if (lane < nb) oring[(o + lane) & ORM] = (uint8_t)(tb >> (8 * lane));
+          else if (lane == 63 && at >= 0) oring[at & ORM] = (uint8_t)hdr;
         } else {
+          if (lane == 0 && at >= 0) oring[at & ORM] = (uint8_t)hdr;
           const uint32_t remlen = (ulen - 7) - 255u * (uint32_t)ext;
-          if (lane == 0) out[o] = (uint8_t)((7u << 5) + (near ? (bd >> 8) : 31u));
-          for (int32_t i = lane; i < ext; i += 64) out[o + 1 + i] = 255;
+          if (lane == 0) oring[o & ORM] = (uint8_t)((7u << 5) + (near ? (bd >> 8) : 31u));
+          // a match of n bytes carries (n - 7) / 255 extension bytes (~2 KiB for a 512 KiB stream):
+          // stream them through the ring in 512-byte slices
+          for (int32_t i0 = 0; i0 < ext; i0 += 512) {
+            if (o + 1 + i0 + 512 - F > kOutRing) flush(o + 1 + i0);
+            for (int32_t i = i0 + lane; i < min(ext, i0 + 512); i += 64) oring[(o + 1 + i) & ORM] = 255;
+          }
+          if (o + 1 + ext + 5 - F > kOutRing) flush(o + 1 + ext);
           if (lane == 0) {
             const int32_t qq = o + 1 + ext;
-            out[qq] = (uint8_t)remlen;
-            if (near) { out[qq + 1] = (uint8_t)(bd & 255); }
-            else { out[qq + 1] = 255; out[qq + 2] = (uint8_t)(fd >> 8); out[qq + 3] = (uint8_t)(fd & 255); }
+            oring[qq & ORM] = (uint8_t)remlen;
+            if (near) { oring[(qq + 1) & ORM] = (uint8_t)(bd & 255); oring[(qq + 2) & ORM] = (uint8_t)(kLzMaxCopy - 1); }
+            else { oring[(qq + 1) & ORM] = 255; oring[(qq + 2) & ORM] = (uint8_t)(fd >> 8); oring[(qq + 3) & ORM] = (uint8_t)(fd & 255); oring[(qq + 4) & ORM] = (uint8_t)(kLzMaxCopy - 1); }
           }
         }
-        o += tok;
       }
+      o += tok + 1;   // token + the literal marker after it
       // rehash at the match boundary q (and q+1 at clevel 9)
       const int32_t q = pm + lm;
       const int32_t ql = q - P;
@@ -284,40 +362,47 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
       } else {
         rehash_out = true;
         rq = q;
-        rseq = ldu32(in + q);
+        EPROF_T(tr0);
+        // the four bytes at q: from the lane that loaded them, else from memory
+        rseq = (ql < 64 && q < loop_end) ? (uint32_t)rdlane((int32_t)v, ql) : ldu32(in + q);
+        EPROF_USE(rseq);
+        EPROF_T(tr1);
+        EPROF_ADD(6, tr0, tr1);
       }
-      if (!PROBE) {
-        peak = max(peak, o + 1);
-        if (o + 1 > maxout) { fail = true; break; }
-        if (lane == 0) out[o] = (uint8_t)(kLzMaxCopy - 1);
-      }
-      o++;
       cur = q + 2 - P;
       next_pos = q + 2;
       // the lane after a match continues the window unless its neighbour-candidate (q + 1)
       // was skipped by the match
       if (!multi || rehash_out || cur >= W || ((s1mask >> cur) & 1ull)) break;
     }
+    EPROF_T(t4);
     if (fail) break;
     if ((visit >> lane) & 1ull) htab[h] = (POS)p;   // buckets are distinct below W
     if (rehash_out && lane == 0) {
       htab[lz_hash(rseq, hashlog)] = (POS)rq;
       if (!PROBE && clevel == 9) htab[lz_hash(rseq >> 8, hashlog)] = (POS)(rq + 1);
     }
+    EPROF_T(t5);
+    EPROF_ADD(0, t0, t1);
+    EPROF_ADD(1, t1, t2);
+    EPROF_ADD(2, t2, t3);
+    EPROF_ADD(3, t3, t4);
+    EPROF_ADD(4, t4, t5);
     pos = next_pos;
   }
 
   if (!PROBE && !fail) {
     // tail literals [pos, bound]
     while (pos <= bound) {
+      if (o - F >= 1024) flush(F + 512);
       const int32_t cnt = min(64, bound - pos + 1);
       const int32_t last = o + (cnt - 1) + (lit + cnt - 1) / 32;
       peak = max(peak, last + 2);
       if (last + 2 > maxout) { fail = true; break; }
       if (lane < cnt) {
         const int32_t off = o + lane + (lit + lane) / 32;
-        out[off] = in[pos + lane];
-        if (((lit + lane + 1) & 31) == 0) out[off + 1] = (uint8_t)(kLzMaxCopy - 1);
+        oring[off & ORM] = in[pos + lane];
+        if (((lit + lane + 1) & 31) == 0) oring[(off + 1) & ORM] = (uint8_t)(kLzMaxCopy - 1);
       }
       o += cnt + (lit + cnt) / 32;
       lit = (lit + cnt) & 31;
@@ -326,14 +411,22 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
     if (!fail) {
       if (lit) {
         const int32_t at = o - lit - 1;
-        if (lane == 0) out[at] = (uint8_t)(lit - 1);
+        if (lane == 0) oring[at & ORM] = (uint8_t)(lit - 1);
         if (at == 0) byte0 = (uint32_t)(lit - 1);
       } else {
         o--;
       }
-      if (lane == 0) out[0] = (uint8_t)(byte0 | 0x20u);
+      if (F == 0) {
+        if (lane == 0) oring[0] = (uint8_t)(byte0 | 0x20u);
+        flush(o);
+      } else {
+        flush(o);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the flushed byte 0 first
+        if (lane == 0) out[0] = (uint8_t)(byte0 | 0x20u);
+      }
     }
   }
+  EPROF_FLUSH;
   r.o = o;
   r.pos = pos;
   r.peak = peak;
@@ -369,7 +462,7 @@ __device__ __forceinline__ bool wave_is_run(gin_t s, int32_t n) {
 template <typename POS>
 __device__ __forceinline__ StreamResult encode_stream(gin_t in, int32_t n, int clevel, gout_t out,
                                                       volatile B2H_LDS POS* htab, volatile B2H_LDS uint32_t* tagm,
-                                                      bool allow_runs) {
+                                                      B2H_LDS uint8_t* oring, bool allow_runs) {
   StreamResult res;
   res.windows = 0;
   res.cycles = 0;
@@ -386,13 +479,13 @@ __device__ __forceinline__ StreamResult encode_stream(gin_t in, int32_t n, int c
   if (clevel < 2) maxlen /= 8;
   else if (clevel < 4) maxlen /= 4;
   else if (clevel < 7) maxlen /= 2;
-  const LzPassOut pr = lz_pass<true, POS>(in + (n - maxlen), maxlen, hashlog, clevel, out, 0, htab, tagm);
+  const LzPassOut pr = lz_pass<true, POS>(in + (n - maxlen), maxlen, hashlog, clevel, out, 0, htab, tagm, oring);
   res.windows = pr.windows;
   const double ratio = (double)pr.pos / (double)pr.o;
   // cratio_ thresholds of blosc/blosclz.c:465 (compared in double, as the reference does)
   const double thr = clevel == 1 ? 2.0 : clevel == 2 ? 1.5 : clevel <= 6 ? 1.2 : clevel == 7 ? 1.15 : clevel == 8 ? 1.1 : 1.0;
   if (ratio < thr || n < 16 || n < 66) return res;
-  const LzPassOut em = lz_pass<false, POS>(in, n, hashlog, clevel, out, n, htab, tagm);
+  const LzPassOut em = lz_pass<false, POS>(in, n, hashlog, clevel, out, n, htab, tagm, oring);
   res.windows += em.windows;
   if (em.fail) return res;
   res.kind = kStreamLz;
@@ -708,6 +801,15 @@ __device__ __forceinline__ uint32_t win_dword(const InWin& W, int32_t q) {
 //   4. all literal bytes of the batch are written at once (each byte lane finds its token with a
 //      max-scan), then the matches are copied in order (sources always precede the token, so
 //      literals-first is safe).
+#ifdef B2H_DEC_PROF   // diagnostics build only (tools/dec_micro.hip): per-phase s_memtime sums
+__device__ uint64_t g_dec_prof[8];
+#define DPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define DPROF_ADD(i, a, b) if (lane == 0) atomicAdd((unsigned long long*)&g_dec_prof[i], (unsigned long long)((b) - (a)))
+#else
+#define DPROF_T(v)
+#define DPROF_ADD(i, a, b)
+#endif
+
 template <int RLOG>
 __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, gout_t out, int32_t maxout,
                                                       B2H_LDS uint8_t* ring) {
@@ -721,6 +823,7 @@ __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, 
   if (lane == 0) W.w0 &= ~(0xe0u << (8 * (-W.wpos)));   // first ctrl is byte0 & 31
   asm volatile("" : "+s"(ip), "+s"(W.wpos));
   for (;;) {
+    DPROF_T(t0);
     const int32_t k = inwin_seek(W, in, length, ip);
     // ---- 1. parse every candidate start ----
     const int32_t P = ip + lane;
@@ -740,12 +843,14 @@ __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, 
     const bool special = (ext && b1 == 255) || (P + 8 > length) || (P + size >= length);
     // ---- 2. chain walk ----
     const int32_t step = special ? 128 : size;
+    DPROF_T(t1);
     uint64_t chain = 0;
     int32_t s = 0;
     do {
       chain |= 1ull << s;
       s += __builtin_amdgcn_readlane(step, s);
     } while (s < 64);
+    DPROF_T(t2);
     const uint64_t spec = chain & __ballot(special);
     int32_t st = spec ? __builtin_ctzll(spec) : 64;   // first token for the serial path
     uint64_t batch = chain & (st < 64 ? (1ull << st) - 1 : ~0ull);
@@ -767,6 +872,7 @@ __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, 
       nip = ip + s;
       nop = op + __builtin_amdgcn_readlane(ex + v, 63);
     }
+    DPROF_T(t3);
     if (batch) {
       if (nop - F > R) F = flush_to<RLOG>(ring, out, nop, F);
       // ---- 4a. literal bytes: byte lane x belongs to the last batch token at or before it ----
@@ -784,6 +890,7 @@ __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, 
         const uint32_t byte = win_dword(W, k + x) & 0xffu;
         if (x <= last + lrun) ring[(op + (int32_t)(last_pk >> 6) + (x - last - 1)) & RM] = (uint8_t)byte;
       }
+      DPROF_T(t4);
       // ---- 4b. matches in order ----
       uint64_t mm = batch & ~__ballot(lit);
       while (mm) {
@@ -800,10 +907,17 @@ __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, 
           F = copy_general<RLOG>(ring, out, oj, src, lj, dj, F);
         }
       }
+      DPROF_T(t5);
+      DPROF_ADD(3, t3, t4);
+      DPROF_ADD(4, t4, t5);
       ip = nip;
       op = nop;
     }
+    DPROF_ADD(0, t0, t1);
+    DPROF_ADD(1, t1, t2);
+    DPROF_ADD(2, t2, t3);
     if (st >= 64) continue;
+    DPROF_T(t6);
     // ---- one token the serial way (ip is its ctrl byte) ----
     {
       const int32_t k2 = inwin_seek(W, in, length, ip);
@@ -867,6 +981,8 @@ __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, 
       }
       ip = p;
     }
+    DPROF_T(t7);
+    DPROF_ADD(5, t6, t7);
   }
   if (result == 0) return 0;
   ring_flush<RLOG>(ring, out, F, op);

@@ -7,6 +7,7 @@
 #include <stdlib.h>
 #include <vector>
 
+#define B2H_DEC_PROF 1
 #include "b2h_lz.h"
 using namespace b2h;
 
@@ -116,6 +117,14 @@ static void run(const uint8_t* din, int32_t len, uint8_t* dout, int32_t nb, int 
   }
   printf("mode %d blocks %5d: %.3f ms, cycles/stream mean %.0f (got %d%s)\n", MODE, nblk, ms, mean, g[0],
          (MODE == 0 || MODE == 3) ? (ok ? ", output OK" : ", OUTPUT MISMATCH") : "");
+  if (MODE == 3) {
+    uint64_t pr[8];
+    hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_dec_prof), sizeof pr);
+    const char* nm[6] = {"parse", "walk", "scan+checks", "literals", "matches", "serial"};
+    for (int i = 0; i < 6; i++) printf("   %-12s %10.0f cycles/stream\n", nm[i], pr[i] / (2.0 * nblk));
+    uint64_t z[8] = {0};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_dec_prof), z, sizeof z);
+  }
   hipFree(dc); hipFree(dg);
 }
 

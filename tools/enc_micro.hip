@@ -1,0 +1,82 @@
+// Encoder micro-benchmark (diagnostics only): encode one stream per wave with the product
+// encode_stream, many waves, and report s_memtime cycles per stream plus per-phase sums.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../c-blosc2_amd/csrc enc_micro.hip -o enc_micro
+//   ./enc_micro plane.bin expected_stream.bin [clevel]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+
+#define B2H_ENC_PROF 1
+#include "b2h_lz.h"
+using namespace b2h;
+
+__global__ __launch_bounds__(64) void k_enc(const uint8_t* in, int32_t n, int clevel, uint8_t* out, int64_t* cycles,
+                                            StreamResult* res) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int hashlog = clevel == 1 ? 12 : (clevel == 2 ? 13 : 14);
+  volatile B2H_LDS uint16_t* htab = (volatile B2H_LDS uint16_t*)smem;
+  volatile B2H_LDS uint32_t* tagm = (volatile B2H_LDS uint32_t*)(smem + (2 << hashlog));
+  B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + (2 << hashlog) + 4 * kTagBuckets);
+  for (int i = threadIdx.x; i < kTagBuckets; i += 64) tagm[i] = 64u;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  StreamResult r = encode_stream<uint16_t>((gin_t)in, n, clevel, (gout_t)(out + (size_t)blockIdx.x * (n + 64)),
+                                           htab, tagm, oring, true);
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) { cycles[blockIdx.x] = (int64_t)(t1 - t0); res[blockIdx.x] = r; }
+}
+
+static std::vector<uint8_t> slurp(const char* f) {
+  FILE* fp = fopen(f, "rb");
+  if (!fp) { perror(f); exit(1); }
+  std::vector<uint8_t> v;
+  uint8_t buf[65536];
+  size_t k;
+  while ((k = fread(buf, 1, sizeof buf, fp)) > 0) v.insert(v.end(), buf, buf + k);
+  fclose(fp);
+  return v;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 3) { fprintf(stderr, "usage: %s plane.bin expected.bin [clevel]\n", argv[0]); return 2; }
+  auto in = slurp(argv[1]);
+  auto want = slurp(argv[2]);
+  const int clevel = argc > 3 ? atoi(argv[3]) : 5;
+  const int32_t n = (int32_t)in.size();
+  uint8_t *din, *dout;
+  hipMalloc(&din, n + 64);
+  hipMemset(din, 0, n + 64);
+  hipMemcpy(din, in.data(), n, hipMemcpyHostToDevice);
+  const int maxblk = 1024;
+  hipMalloc(&dout, (size_t)maxblk * (n + 64));
+  int64_t* dc; StreamResult* dr;
+  hipMalloc(&dc, maxblk * 8); hipMalloc(&dr, maxblk * sizeof(StreamResult));
+  const size_t lds = enc_lds_bytes(2, 14);
+  for (int nblk : {1, 256, 1024}) {
+    uint64_t z[16] = {0};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_enc_prof), z, sizeof z);
+    hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
+    hipEventRecord(a);
+    k_enc<<<nblk, 64, lds>>>(din, n, clevel, dout, dc, dr);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms = 0; hipEventElapsedTime(&ms, a, b);
+    std::vector<int64_t> c(nblk);
+    std::vector<StreamResult> r(nblk);
+    hipMemcpy(c.data(), dc, nblk * 8, hipMemcpyDeviceToHost);
+    hipMemcpy(r.data(), dr, nblk * sizeof(StreamResult), hipMemcpyDeviceToHost);
+    std::vector<uint8_t> o(r[0].size > 0 ? r[0].size : 1);
+    hipMemcpy(o.data(), dout, o.size(), hipMemcpyDeviceToHost);
+    const bool ok = r[0].kind == kStreamLz && o.size() == want.size() && o == want;
+    double mean = 0; for (auto x : c) mean += x; mean /= nblk;
+    printf("blocks %5d: %.3f ms, cycles/stream %.0f, kind %d size %d windows %d %s\n", nblk, ms, mean, r[0].kind,
+           r[0].size, r[0].windows, ok ? "output OK" : "OUTPUT MISMATCH");
+    uint64_t pr[16];
+    hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_enc_prof), sizeof pr);
+    const char* nm[8] = {"load", "hash+tags", "cand test", "walk", "htab upd", "(match ext)", "(rehash ld)", "(literals)"};
+    for (int pass = 1; pass >= 0; pass--)
+      for (int i = 0; i < 8; i++)
+        printf("   %s %-12s %10.0f cycles/stream\n", pass ? "probe" : "main ", nm[i], pr[8 * pass + i] / (double)nblk);
+  }
+  return 0;
+}
