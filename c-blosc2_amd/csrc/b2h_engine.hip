@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "b2h_engine.h"
@@ -69,7 +70,7 @@ struct Scratch {
 };
 
 struct Workspace {
-  Scratch t1, t2, work, sbuf, res, place, mode, qctr;          // compress
+  Scratch t1, t2, work, sbuf, res, place, mode, qctr, gtab;    // compress
   Scratch dchunks, dstreams, dblocks, dtotals, stage, stage2, ptrs, dqctr, ddbg;  // decompress
   std::mutex mu;
 };
@@ -206,16 +207,31 @@ __global__ __launch_bounds__(kBlockThreads) void k_ffilter(CGeom g, int pass, ui
 // varies ~100x (a float32 mantissa plane vs an all-zero exponent plane) and the hardware deals
 // workgroups to XCDs / shader engines by index, so one-workgroup-per-stream left most slots
 // waiting behind the expensive planes; pulling keeps every resident wave busy.  Every wave exits
-// once the counter passes `nstreams_total`.  Dynamic LDS: hash table (POS << hashlog) + tags.
-template <typename POS>
+// once the counter passes `nstreams_total`.  Dynamic LDS: hash table + bucket bitset + output ring.
+// GTAB: the hash table lives in global memory (`gtab`, one table per workgroup slot) and LDS holds
+// only the bucket bitset and the output ring, so occupancy is set by registers, not LDS (see
+// GlbTab in b2h_lz.h).
+template <typename POS, bool GTAB>
 __global__ __launch_bounds__(64) void k_encode(CGeom g, const uint8_t* __restrict__ filt,
                                                uint8_t* __restrict__ sbuf, StreamResult* __restrict__ res,
-                                               int32_t nstreams_total, int32_t* __restrict__ next) {
+                                               int32_t nstreams_total, int32_t* __restrict__ next,
+                                               POS* __restrict__ gtab) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
-  volatile B2H_LDS POS* htab = (volatile B2H_LDS POS*)(smem);
-  volatile B2H_LDS uint32_t* tagm = (volatile B2H_LDS uint32_t*)(smem + (sizeof(POS) << hashlog));
-  B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + (sizeof(POS) << hashlog) + 4 * kTagBuckets);
+  typedef typename std::conditional<GTAB, GlbTab<POS>, LdsTab<POS>>::type Tab;
+  Tab htab;
+  size_t bits_off, ring_off;
+  if constexpr (GTAB) {
+    htab.t = (B2H_GLB POS*)(gtab + ((size_t)blockIdx.x << hashlog));
+    bits_off = 0;
+    ring_off = (size_t(1) << hashlog) >> 3;
+  } else {
+    htab.t = (volatile B2H_LDS POS*)(smem);
+    bits_off = enc_bits_offset(sizeof(POS), hashlog);
+    ring_off = enc_ring_offset(sizeof(POS), hashlog);
+  }
+  B2H_LDS uint32_t* dbits = (B2H_LDS uint32_t*)(smem + bits_off);
+  B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + ring_off);
   for (;;) {
     // branch-free grab: every lane takes part (lane 0 adds 1, the others 0), so no divergent
     // region sits between the atomic and the broadcast -- with a lane-0 branch the structurizer
@@ -225,12 +241,11 @@ __global__ __launch_bounds__(64) void k_encode(CGeom g, const uint8_t* __restric
     const int32_t c = s / g.nsc, l = s - c * g.nsc;
     int32_t off, len, blk;
     stream_locate(g, l, &off, &len, &blk);
-    for (int i = lane_id(); i < kTagBuckets; i += 64) tagm[i] = 64u;
     gin_t in = (gin_t)(filt + (int64_t)c * g.wstride + off);
     gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide time base
-    StreamResult r = encode_stream<POS>(in, len, g.clevel, out, htab, tagm, oring, g.overhead == kHdrExt);
+    StreamResult r = encode_stream<Tab>(in, len, g.clevel, out, htab, dbits, oring, g.overhead == kHdrExt);
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
     if (lane_id() == 0) res[s] = r;
@@ -588,20 +603,33 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
   int32_t* next = ws->qctr.as<int32_t>();
   HIPCHK(hipMemsetAsync(next, 0, sizeof(int32_t), st));
   {
-    const void* fn = small ? reinterpret_cast<const void*>(&k_encode<uint16_t>)
-                           : reinterpret_cast<const void*>(&k_encode<uint32_t>);
-    const size_t lds = enc_lds_bytes(small ? sizeof(uint16_t) : sizeof(uint32_t), hashlog);
+    static const bool gtab = getenv("B2H_ENC_GTAB") != nullptr && atoi(getenv("B2H_ENC_GTAB")) != 0;
+    const size_t pos_bytes = small ? sizeof(uint16_t) : sizeof(uint32_t);
+    const void* fn = small ? (gtab ? reinterpret_cast<const void*>(&k_encode<uint16_t, true>)
+                                   : reinterpret_cast<const void*>(&k_encode<uint16_t, false>))
+                           : (gtab ? reinterpret_cast<const void*>(&k_encode<uint32_t, true>)
+                                   : reinterpret_cast<const void*>(&k_encode<uint32_t, false>));
+    const size_t lds = gtab ? (((size_t(1) << hashlog) >> 3) + kOutRing) : enc_lds_bytes(pos_bytes, hashlog);
     static bool attr_set = false;
     if (!attr_set) {   // > 64 KiB of dynamic LDS per workgroup: opt in once
-      HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_encode<uint32_t>),
+      HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_encode<uint32_t, false>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
       attr_set = true;
     }
     const uint32_t grid = (uint32_t)std::min<int64_t>(ntot, resident_slots(fn, lds));
-    if (small)
-      k_encode<uint16_t><<<grid, 64, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next);
-    else
-      k_encode<uint32_t><<<grid, 64, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next);
+    void* gt = nullptr;
+    if (gtab) {
+      if (ws->gtab.ensure(((size_t)grid << hashlog) * pos_bytes)) return E_MEMORY;
+      gt = ws->gtab.p;
+    }
+    uint8_t* sb = ws->sbuf.as<uint8_t>();
+    if (small) {
+      if (gtab) k_encode<uint16_t, true><<<grid, 64, lds, st>>>(g, filt, sb, res, (int32_t)ntot, next, (uint16_t*)gt);
+      else k_encode<uint16_t, false><<<grid, 64, lds, st>>>(g, filt, sb, res, (int32_t)ntot, next, nullptr);
+    } else {
+      if (gtab) k_encode<uint32_t, true><<<grid, 64, lds, st>>>(g, filt, sb, res, (int32_t)ntot, next, (uint32_t*)gt);
+      else k_encode<uint32_t, false><<<grid, 64, lds, st>>>(g, filt, sb, res, (int32_t)ntot, next, nullptr);
+    }
   }
   ev_encode.stop(st);
   HIPCHK(hipGetLastError());

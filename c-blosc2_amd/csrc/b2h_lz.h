@@ -5,15 +5,19 @@
 // inherently serial, so the wave advances through the stream in WINDOWS of up to 64 positions:
 //   * every lane hashes its own position and reads the hash table (LDS).  The value is the serial
 //     loop's candidate for every lane below W, the first lane whose hash bucket already occurs at
-//     an earlier lane of the window (found with one LDS atomic-min per lane).
-//   * every lane tests its candidate (one 12-byte compare) and decides literal / match exactly as
+//     an earlier lane of the window (found exactly with one LDS atomic-or per lane on a
+//     one-bit-per-bucket table).
+//   * every lane tests its candidate (a 28-byte compare) and decides literal / match exactly as
 //     the serial loop would; `__ballot` yields the accepted-match mask.
-//   * a scalar scan then walks the window: literal runs are emitted in parallel (closed-form
-//     offsets incl. the 32-literal run markers), each accepted match is emitted, and the scan
-//     continues after the match while it stays below W -- the lanes after a match still hold
-//     their exact candidates because every position inserted inside the window (literals,
-//     anchors, in-window rehash points) owns a distinct bucket.  Long matches are extended
-//     cooperatively, 1 KiB per step (64 lanes x 16 bytes).
+//   * a short scalar chain walk picks the matches the serial loop takes (first accepted lane,
+//     then the first accepted lane at or after that match's end + 2, ...) while they stay below
+//     W -- the lanes after a match still hold their exact candidates because every position
+//     inserted inside the window (literals, anchors, in-window rehash points) owns a distinct
+//     bucket.  Matches longer than the up-front compare are extended cooperatively, 1 KiB per
+//     step (64 lanes x 16 bytes).
+//   * all tokens of the window are then emitted at once: per-lane output sizes (literal bytes,
+//     32-literal run markers, match tokens) go through one DPP prefix sum, every lane writes its
+//     bytes to an LDS output ring, and run headers are patched in a second write.
 //   * the window's hash inserts are one LDS store per visited lane, then the out-of-window
 //     rehash (if any) exactly in the serial order.
 //
@@ -33,14 +37,16 @@
 
 namespace b2h {
 
-constexpr int kTagBuckets = 1536;   // window bucket-repeat detector (u32 per bucket, LDS)
 constexpr int kOutRing = 2048;      // encoder output staging ring (LDS), flushed in 512 B pieces
-// LDS per encoder wave: hash table + tags + output ring = 40 KiB for 64 KiB streams (4 per CU)
-__host__ __device__ constexpr size_t enc_lds_bytes(size_t pos_bytes, int hashlog) {
-  return (pos_bytes << hashlog) + 4 * kTagBuckets + kOutRing;
+// LDS per encoder wave: hash table + bucket bitset + output ring = 36 KiB for 64 KiB streams
+// (4 waves per CU).  Layout: [htab: POS << hashlog][bits: 2^hashlog / 8][ring: kOutRing].
+__host__ __device__ constexpr size_t enc_bits_offset(size_t pos_bytes, int hashlog) { return pos_bytes << hashlog; }
+__host__ __device__ constexpr size_t enc_ring_offset(size_t pos_bytes, int hashlog) {
+  return (pos_bytes << hashlog) + ((size_t(1) << hashlog) >> 3);
 }
-// tag bucket of a hash: any fixed map works (a shared bucket only ends a window early)
-__device__ __forceinline__ uint32_t tag_bucket(uint32_t h, int hashlog) { return (h * 3u) >> (hashlog - 9); }
+__host__ __device__ constexpr size_t enc_lds_bytes(size_t pos_bytes, int hashlog) {
+  return enc_ring_offset(pos_bytes, hashlog) + kOutRing;
+}
 
 // Explicit address spaces: generic (flat) pointers would turn every access into a flat_* op,
 // which couples vmcnt and lgkmcnt waits and serialises LDS behind global traffic.
@@ -101,6 +107,68 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 __device__ __forceinline__ int32_t rdlane(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
+// Wave64 inclusive scans with DPP (row shifts inside 16-lane rows, then row broadcasts 15/31).
+// Lanes whose DPP source is masked or out of row read the identity of the operation.
+__device__ __forceinline__ int32_t wave_scan_add(int32_t v) {
+  int32_t r = v;
+  r += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+  r += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+  r += __builtin_amdgcn_update_dpp(0, v, 0x113, 0xf, 0xf, false);   // row_shr:3
+  r += __builtin_amdgcn_update_dpp(0, r, 0x114, 0xf, 0xe, false);   // row_shr:4, banks 1-3
+  r += __builtin_amdgcn_update_dpp(0, r, 0x118, 0xf, 0xc, false);   // row_shr:8, banks 2-3
+  r += __builtin_amdgcn_update_dpp(0, r, 0x142, 0xa, 0xf, false);   // row_bcast:15, rows 1,3
+  r += __builtin_amdgcn_update_dpp(0, r, 0x143, 0xc, 0xf, false);   // row_bcast:31, rows 2,3
+  return r;
+}
+__device__ __forceinline__ int32_t wave_scan_max(int32_t v) {   // values >= -1
+  int32_t r = v;
+  r = max(r, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));
+  r = max(r, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));
+  r = max(r, __builtin_amdgcn_update_dpp(-1, v, 0x113, 0xf, 0xf, false));
+  r = max(r, __builtin_amdgcn_update_dpp(-1, r, 0x114, 0xf, 0xe, false));
+  r = max(r, __builtin_amdgcn_update_dpp(-1, r, 0x118, 0xf, 0xc, false));
+  r = max(r, __builtin_amdgcn_update_dpp(-1, r, 0x142, 0xa, 0xf, false));
+  r = max(r, __builtin_amdgcn_update_dpp(-1, r, 0x143, 0xc, 0xf, false));
+  return r;
+}
+
+// The encoder's hash table (one per wave): in LDS, or in global memory.  LDS holds a 64 KiB
+// stream's table (32 KiB) for only 4 waves per CU, one per SIMD, and a lone wave leaves its SIMD
+// idle while it waits on memory; with the table in global memory a wave needs 4 KiB of LDS (bucket
+// bitset + output ring) and 4 waves share each SIMD.  Global tables are accessed at workgroup
+// scope: the table is private to the wave, and at agent scope the accesses bypass the XCD's L2
+// (a lane then need not see what another lane stored in the previous window).
+template <typename POS>
+struct LdsTab {
+  typedef POS pos_t;
+  volatile B2H_LDS POS* t;
+  __device__ __forceinline__ uint32_t get(uint32_t h) const { return t[h]; }
+  __device__ __forceinline__ void put(uint32_t h, uint32_t v) const { t[h] = (POS)v; }
+  __device__ __forceinline__ void clear(int hashlog) const {   // 8-byte LDS stores
+    B2H_LDS uint64_t* h8 = (B2H_LDS uint64_t*)(t);
+    const int32_t n8 = (int32_t)((sizeof(POS) << hashlog) / 8);
+    for (int32_t i = lane_id(); i < n8; i += 64) h8[i] = 0;
+  }
+};
+template <typename POS>
+struct GlbTab {
+  typedef POS pos_t;
+  B2H_GLB POS* t;
+  __device__ __forceinline__ uint32_t get(uint32_t h) const {
+    return __hip_atomic_load(t + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  __device__ __forceinline__ void put(uint32_t h, uint32_t v) const {
+    __hip_atomic_store(t + h, (POS)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  __device__ __forceinline__ void clear(int hashlog) const {   // 16-byte stores; they complete
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // before the first window's loads
+    B2H_GLB u32x4* t16 = (B2H_GLB u32x4*)(t);
+    const int32_t n16 = (int32_t)((sizeof(POS) << hashlog) / 16);
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    for (int32_t i = lane_id(); i < n16; i += 64) t16[i] = z;
+  }
+};
+
 // End of the common prefix of in[x..] and in[x-d..], one past the first mismatch, capped at
 // `bound` (get_match / get_run semantics, blosc/blosclz.c:119-165).  64 lanes x 16 bytes per step.
 __device__ __forceinline__ int32_t wave_match_end(gin_t in, int32_t x, uint32_t d, int32_t bound) {
@@ -159,10 +227,10 @@ __device__ uint64_t g_enc_prof[16];
 
 // One greedy parse.  PROBE: get_cratio (counts only, limit = min(length, 2^hashlog), no far
 // short-match rule, no clevel-9 double rehash, no tail).  !PROBE: the emitting main loop + tail.
-template <bool PROBE, typename POS>
+template <bool PROBE, typename TAB>
 __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashlog, int clevel, gout_t out,
-                                             int32_t maxout, volatile B2H_LDS POS* htab,
-                                             volatile B2H_LDS uint32_t* tagm, B2H_LDS uint8_t* oring) {
+                                             int32_t maxout, TAB htab, B2H_LDS uint32_t* dbits,
+                                             B2H_LDS uint8_t* oring) {
   const int lane = lane_id();
   // Output bytes are staged in an LDS ring and leave for `out` in 512-byte pieces once they are
   // final: global stores share vmcnt with loads on CDNA, so a byte store per token would make
@@ -179,11 +247,10 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
     limit = length > hl ? hl : length;
   }
   const int32_t bound = limit - 1, loop_end = limit - 12;
-  {  // clear the hash table with 8-byte LDS stores
-    B2H_LDS uint64_t* h8 = (B2H_LDS uint64_t*)(htab);
-    const int32_t n8 = (int32_t)((sizeof(POS) << hashlog) / 8);
-    for (int32_t i = lane; i < n8; i += 64) h8[i] = 0;
-    // the clear goes through a u64 view: keep the compiler from sinking it below the
+  {  // clear the hash table and the bucket bitset
+    htab.clear(hashlog);
+    for (int32_t i = lane; i < (1 << hashlog) / 32; i += 64) dbits[i] = 0u;
+    // the clear goes through a wider view: keep the compiler from sinking it below the
     // (differently typed) table reads that follow
     asm volatile("" ::: "memory");
   }
@@ -216,23 +283,28 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
     const uint32_t v = a[0];
     EPROF_T(t1);
     const uint32_t h = lz_hash(v, hashlog);
-    const uint32_t c0 = valid ? (uint32_t)htab[h] : 0u;
-    // W: first lane whose bucket already occurs at an earlier lane of the window
-    const uint32_t b = tag_bucket(h, hashlog);
-    if (valid) __hip_atomic_fetch_min((B2H_LDS uint32_t*)&tagm[b], (uint32_t)lane, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-    const uint32_t minl = valid ? tagm[b] : (uint32_t)lane;
-    if (valid) tagm[b] = 64u;
+    const uint32_t c0 = valid ? htab.get(h) : 0u;
+    // W: first lane whose bucket already occurs at an earlier lane of the window.  One atomic-or
+    // per lane on a bit-per-bucket table: the lanes that find their bit set are the repeats (LDS
+    // applies the lanes of one instruction in lane order; any other order would only flag an
+    // earlier lane of a repeated bucket -- a shorter window, still exact below W).  The words are
+    // cleared right after: every bit set in them belongs to this window.
+    uint32_t old = 0;
+    if (valid) {
+      old = __hip_atomic_fetch_or(&dbits[h >> 5], 1u << (h & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      dbits[h >> 5] = 0u;
+    }
+    const bool rep = valid && ((old >> (h & 31)) & 1u);
     // A lane whose left neighbour has the same hash (runs, short periods) knows its serial
     // candidate exactly: the neighbour, inserted just before it.  Other repeats end the window.
     const uint32_t hprev = (uint32_t)__shfl_up((int)h, 1);
     const bool same1 = valid && lane > 0 && hprev == h;
     const uint64_t s1mask = __ballot(same1);
-    const uint64_t dup = __ballot(minl < (uint32_t)lane && !same1);
+    const uint64_t dup = __ballot(rep && !same1);
     int32_t W = dup ? __builtin_ctzll(dup) : 64;
-    W = min(W, min(64, loop_end - P));
-
+    W = max(1, min(W, loop_end - P));   // lane 0's candidate is always exact
     EPROF_T(t2);
+
     // candidate test (lanes < W): literal or match, exactly as the serial loop decides
     const uint32_t cand = same1 ? (uint32_t)(p - 1) : c0;
     const uint32_t dist = (uint32_t)(p - (int32_t)cand);
@@ -240,88 +312,98 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
     bool accept = false;
     int32_t lenx = 0;   // match length, or -1: the first 28 bytes all match (extend later)
     if (lane < W && dist != 0 && dist < kLzFar) {
-      uint32_t r[7];
-      ld28(in + cand, r);
-      if (r[0] == v) {
+      uint32_t rr[7];
+      ld28(in + cand, rr);
+      if (rr[0] == v) {
         int32_t mm = 28;   // index of the first mismatching byte
 #pragma unroll
         for (int i = 6; i >= 1; i--) {
-          const uint32_t x = a[i] ^ r[i];
+          const uint32_t x = a[i] ^ rr[i];
           if (x) mm = 4 * i + (__builtin_ctz(x) >> 3);
         }
         const int32_t e = min(mm < 28 ? p + mm + 1 : 0x7fffffff, bound);
         const int32_t len = e - 4 - p;
         accept = len >= 4 && (PROBE || !(len <= 5 && (dist - 1) >= kLzNear));
-        lenx = mm < 28 ? len : -1;
+        lenx = (mm < 28 || p + 29 >= bound) ? len : -1;
       }
     }
     const uint64_t am = __ballot(accept);
     EPROF_T(t3);
 
-    // scalar walk of the window
-    int32_t cur = 0;
-    uint64_t visit = 0;
-    int32_t next_pos = P + W;
-    bool rehash_out = false;
-    int32_t rq = 0;
-    uint32_t rseq = 0;
-    for (;;) {
-      const uint64_t rem = cur < 64 ? (am & (~0ull << cur)) : 0ull;
-      const int32_t m = rem ? __builtin_ctzll(rem) : W;
-      EPROF_T(tl0);
-      if (m > cur) {   // literals [cur, m)
-        const int32_t cnt = m - cur;
-        if (!PROBE) {
-          const int32_t last = o + (cnt - 1) + (lit + cnt - 1) / 32;
-          peak = max(peak, last + 2);
-          if (last + 2 > maxout) { fail = true; break; }
-          if (lane >= cur && lane < m) {
-            const int32_t k = lane - cur;
-            const int32_t off = o + k + (lit + k) / 32;
-            oring[off & ORM] = (uint8_t)(v & 0xffu);
-            if (((lit + k + 1) & 31) == 0) oring[(off + 1) & ORM] = (uint8_t)(kLzMaxCopy - 1);
-          }
+    // ---- chain walk: the matches the serial loop takes in this window ----
+    uint64_t chain = 0;
+    int32_t E = W;        // the window consumes positions P .. P+E-1 (E > 64 after a long match)
+    int32_t ser = -1;     // a match with length-extension bytes, emitted by the scalar path below
+    int32_t lastc2 = -1;  // end + 2 of the chain match that closes the window
+    {
+      uint64_t rem = am;
+      while (rem) {
+        const int32_t m = __builtin_ctzll(rem);
+        int32_t lm = rdlane(lenx, m);
+        if (lm < 0) {
+          EPROF_T(te0);
+          lm = wave_match_end(in, P + m + 28, (uint32_t)rdlane((int32_t)dist, m), bound) - 4 - (P + m);
+          lenx = lane == m ? lm : lenx;
+          EPROF_T(te1);
+          EPROF_ADD(5, te0, te1);
         }
-        o += cnt + (lit + cnt) / 32;
-        lit = (lit + cnt) & 31;
-        visit |= (m >= 64 ? ~0ull : ((1ull << m) - 1)) & (~0ull << cur);
+        if (lm >= 262) { ser = m; E = m; break; }   // (len - 7) / 255 extension bytes
+        chain |= 1ull << m;
+        const int32_t c2 = m + lm + 2;   // the serial loop resumes at the match end + 2
+        // it stays in this window while the lane there holds an exact candidate: below W, and
+        // not a left-neighbour candidate whose neighbour (end + 1) the match skipped
+        if (!multi || c2 >= W || ((s1mask >> c2) & 1ull)) { E = c2; lastc2 = c2; break; }
+        rem = am & (~0ull << c2);
       }
-      EPROF_T(tl1);
-      EPROF_ADD(7, tl0, tl1);
-      if (!rem) { next_pos = P + W; break; }
-      // ---- the match of lane m ----
-      visit |= 1ull << m;
-      const int32_t pm = P + m;
-      const uint32_t dm = (uint32_t)rdlane((int32_t)dist, m);
-      int32_t lm = rdlane(lenx, m);
-      if (lm < 0) {
-        EPROF_T(te0);
-        lm = wave_match_end(in, pm + 28, dm, bound) - 4 - pm;
-        EPROF_T(te1);
-        EPROF_ADD(5, te0, te1);
-      }
-      const uint32_t bd = dm - 1;   // biased distance
-      const uint32_t ulen = (uint32_t)lm;
-      const bool near = bd < kLzNear;
-      int32_t at = -1;   // header of the literal run this match closes (patched below)
-      const uint32_t hdr = (uint32_t)(lit - 1);
-      if (lit) {
-        at = o - lit - 1;
-        if (!PROBE && at == 0) byte0 = hdr;
-      } else {
-        o--;
-      }
-      lit = 0;
-      const int32_t ext = ulen >= 7 ? (int32_t)((ulen - 7) / 255) : 0;   // 255 bytes
-      const int32_t tok = ulen < 7 ? (near ? 2 : 4) : 1 + ext + (near ? 2 : 4);
+    }
+    EPROF_T(t4);
+
+    // ---- all tokens of the window at once ----
+    // owner: the last chain match at or before the lane; prev: the last one strictly before
+    const bool ischain = (chain >> lane) & 1ull;
+    const int32_t own = wave_scan_max(ischain ? lane : -1);
+    int32_t prev = __shfl_up(own, 1);
+    if (lane == 0) prev = -1;
+    const int32_t c2v = lane + lenx + 2;                        // chain lanes: where the walk resumes
+    const int32_t pc2 = __shfl(c2v, prev < 0 ? 0 : prev);
+    const int32_t segstart = prev >= 0 ? pc2 : 0;               // first lane after prev's match
+    const int32_t lpos = (prev >= 0 ? 0 : lit) + lane - segstart;   // literals of the run before the lane
+    const bool islit = !ischain && lane >= segstart && lane < min(E, W);
+    const int32_t rr5 = lpos & 31;   // 32-literal runs: the run restarts after every marker
+    const uint32_t bd = dist - 1;    // biased distance
+    const bool near = bd < kLzNear;
+    const uint32_t ulen = (uint32_t)lenx;
+    const int32_t tok = ulen < 7 ? (near ? 2 : 4) : (near ? 3 : 5);   // no extension bytes here
+    // output bytes per lane: a literal (+ the marker opening the next run after its 32nd), or a
+    // match token + the marker opening the next run (- the pending marker it overwrites when no
+    // literal precedes it)
+    int32_t contrib = 0;
+    if (islit) contrib = 1 + (rr5 == 31 ? 1 : 0);
+    if (ischain) contrib = tok + 1 - (rr5 == 0 ? 1 : 0);
+    const int32_t incl = wave_scan_add(contrib);
+    const int32_t excl = incl - contrib;
+    const uint64_t litm = __ballot(islit);
+    const uint64_t elems = litm | chain;
+    if (elems) {
+      const int32_t le = 63 - __builtin_clzll(elems);
+      const bool lelit = (litm >> le) & 1ull;
       if (!PROBE) {
-        // every bound check of the token and of the literal marker after it is <= o + tok + 1
-        peak = max(peak, o + tok + 1);
-        if (o + tok + 1 > maxout) { fail = true; break; }
-        const uint32_t fd = bd - kLzNear;
-        if (ext == 0) {
-          // token bytes + the marker that opens the next literal run, little-endian in a u64:
-          // one LDS write instruction (lanes 0..nb-1), the run header from lane 63
+        const int32_t base = o + excl;
+        const int32_t ts = base - (rr5 == 0 ? 1 : 0);   // chain lanes: first token byte
+        // every bound check grows with the output position: the window's last element makes
+        // the largest (a literal checks op + 2, a match op + token + 1)
+        const int32_t req = lelit ? rdlane(base, le) + 2 : rdlane(ts + tok + 1, le);
+        peak = max(peak, req);
+        if (req > maxout) { fail = true; break; }
+        const bool nextchain = lane < 63 && ((chain >> (lane + 1)) & 1ull);
+        if (islit) {
+          oring[base & ORM] = (uint8_t)(v & 0xffu);
+          // the marker after a 32nd literal is overwritten by a match right behind it
+          if (rr5 == 31 && !nextchain) oring[(base + 1) & ORM] = (uint8_t)(kLzMaxCopy - 1);
+        }
+        if (ischain) {
+          // token bytes + the marker that opens the next literal run, little-endian in a u64
+          const uint32_t fd = bd - kLzNear;
           uint64_t tb;
           int32_t nb;
           if (ulen < 7) {
@@ -332,14 +414,59 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
             if (near) { tb = (uint64_t)((7u << 5) + (bd >> 8)) | (rl << 8) | ((uint64_t)(bd & 255) << 16) | (31ull << 24); nb = 4; }
             else { tb = (uint64_t)((7u << 5) + 31) | (rl << 8) | (255ull << 16) | ((uint64_t)(fd >> 8) << 24) | ((uint64_t)(fd & 255) << 32) | (31ull << 40); nb = 6; }
           }
-          if (lane < nb) oring[(o + lane) & ORM] = (uint8_t)(tb >> (8 * lane));
-          else if (lane == 63 && at >= 0) oring[at & ORM] = (uint8_t)hdr;
+          if (c2v < 64 && ((chain >> c2v) & 1ull)) nb--;   // the next match overwrites the marker
+#pragma unroll
+          for (int i = 0; i < 6; i++)
+            if (i < nb) oring[(ts + i) & ORM] = (uint8_t)(tb >> (8 * i));
+        }
+        // run headers closed by a match, after every byte of the window is in place
+        if (ischain && rr5 > 0) oring[(ts - rr5 - 1) & ORM] = (uint8_t)(rr5 - 1);
+        const uint64_t z = __ballot(ischain && rr5 > 0 && ts - rr5 - 1 == 0);
+        if (z) byte0 = (uint32_t)(rdlane(rr5, __builtin_ctzll(z)) - 1);
+      }
+      lit = lelit ? ((rdlane(lpos, le) + 1) & 31) : 0;
+    }
+    o += rdlane(incl, 63);
+
+    // visited positions: literals, match anchors, in-window rehash points (match end)
+    uint64_t visit = elems | __ballot(!ischain && prev >= 0 && lane == pc2 - 2 && lane < W && multi);
+    bool rehash_out = false;
+    int32_t rq = 0;
+    if (lastc2 >= 0 && (lastc2 - 2 >= W || !multi)) {
+      rehash_out = true;
+      rq = P + lastc2 - 2;
+    }
+
+    // ---- a match with extension bytes: the scalar token path ----
+    if (ser >= 0) {
+      visit |= 1ull << ser;
+      const uint32_t dm = (uint32_t)rdlane((int32_t)dist, ser);
+      const int32_t lm = rdlane(lenx, ser);
+      const uint32_t sbd = dm - 1;
+      const uint32_t sulen = (uint32_t)lm;
+      const bool snear = sbd < kLzNear;
+      int32_t at = -1;   // header of the literal run this match closes
+      const uint32_t hdr = (uint32_t)(lit - 1);
+      if (lit) {
+        at = o - lit - 1;
+        if (!PROBE && at == 0) byte0 = hdr;
+      } else {
+        o--;
+      }
+      lit = 0;
+      const int32_t ext = (int32_t)((sulen - 7) / 255);
+      const int32_t stok = 1 + ext + (snear ? 2 : 4);
+      if (!PROBE) {
+        peak = max(peak, o + stok + 1);
+        if (o + stok + 1 > maxout) {
+          fail = true;
         } else {
           if (lane == 0 && at >= 0) oring[at & ORM] = (uint8_t)hdr;
-          const uint32_t remlen = (ulen - 7) - 255u * (uint32_t)ext;
-          if (lane == 0) oring[o & ORM] = (uint8_t)((7u << 5) + (near ? (bd >> 8) : 31u));
-          // a match of n bytes carries (n - 7) / 255 extension bytes (~2 KiB for a 512 KiB stream):
-          // stream them through the ring in 512-byte slices
+          const uint32_t remlen = (sulen - 7) - 255u * (uint32_t)ext;
+          const uint32_t fd = sbd - kLzNear;
+          if (lane == 0) oring[o & ORM] = (uint8_t)((7u << 5) + (snear ? (sbd >> 8) : 31u));
+          // a match of n bytes carries (n - 7) / 255 extension bytes (~2 KiB for a 512 KiB
+          // stream): stream them through the ring in 512-byte slices
           for (int32_t i0 = 0; i0 < ext; i0 += 512) {
             if (o + 1 + i0 + 512 - F > kOutRing) flush(o + 1 + i0);
             for (int32_t i = i0 + lane; i < min(ext, i0 + 512); i += 64) oring[(o + 1 + i) & ORM] = 255;
@@ -348,47 +475,42 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
           if (lane == 0) {
             const int32_t qq = o + 1 + ext;
             oring[qq & ORM] = (uint8_t)remlen;
-            if (near) { oring[(qq + 1) & ORM] = (uint8_t)(bd & 255); oring[(qq + 2) & ORM] = (uint8_t)(kLzMaxCopy - 1); }
+            if (snear) { oring[(qq + 1) & ORM] = (uint8_t)(sbd & 255); oring[(qq + 2) & ORM] = (uint8_t)(kLzMaxCopy - 1); }
             else { oring[(qq + 1) & ORM] = 255; oring[(qq + 2) & ORM] = (uint8_t)(fd >> 8); oring[(qq + 3) & ORM] = (uint8_t)(fd & 255); oring[(qq + 4) & ORM] = (uint8_t)(kLzMaxCopy - 1); }
           }
         }
       }
-      o += tok + 1;   // token + the literal marker after it
-      // rehash at the match boundary q (and q+1 at clevel 9)
-      const int32_t q = pm + lm;
-      const int32_t ql = q - P;
-      if (ql < W && !(!PROBE && clevel == 9)) {
-        visit |= 1ull << ql;           // lane ql holds hash(ld32(in + q)) already
+      o += stok + 1;   // token + the literal marker after it
+      const int32_t ql = ser + lm;   // the match end, relative to P
+      if (ql < W && multi) {
+        visit |= 1ull << ql;         // lane ql holds hash(ld32(in + q)) already
       } else {
         rehash_out = true;
-        rq = q;
-        EPROF_T(tr0);
-        // the four bytes at q: from the lane that loaded them, else from memory
-        rseq = (ql < 64 && q < loop_end) ? (uint32_t)rdlane((int32_t)v, ql) : ldu32(in + q);
-        EPROF_USE(rseq);
-        EPROF_T(tr1);
-        EPROF_ADD(6, tr0, tr1);
+        rq = P + ql;
       }
-      cur = q + 2 - P;
-      next_pos = q + 2;
-      // the lane after a match continues the window unless its neighbour-candidate (q + 1)
-      // was skipped by the match
-      if (!multi || rehash_out || cur >= W || ((s1mask >> cur) & 1ull)) break;
+      E = ql + 2;
     }
-    EPROF_T(t4);
     if (fail) break;
-    if ((visit >> lane) & 1ull) htab[h] = (POS)p;   // buckets are distinct below W
-    if (rehash_out && lane == 0) {
-      htab[lz_hash(rseq, hashlog)] = (POS)rq;
-      if (!PROBE && clevel == 9) htab[lz_hash(rseq >> 8, hashlog)] = (POS)(rq + 1);
-    }
     EPROF_T(t5);
+    uint32_t rseq = 0;
+    if (rehash_out) {
+      // the four bytes at the match end: from the lane that loaded them, else from memory
+      const int32_t ql = rq - P;
+      rseq = (ql < 64 && rq < loop_end) ? (uint32_t)rdlane((int32_t)v, ql) : ldu32(in + rq);
+    }
+    if ((visit >> lane) & 1ull) htab.put(h, (uint32_t)p);   // buckets are distinct below W
+    if (rehash_out && lane == 0) {
+      htab.put(lz_hash(rseq, hashlog), (uint32_t)rq);
+      if (!PROBE && clevel == 9) htab.put(lz_hash(rseq >> 8, hashlog), (uint32_t)(rq + 1));
+    }
+    EPROF_T(t6);
     EPROF_ADD(0, t0, t1);
     EPROF_ADD(1, t1, t2);
     EPROF_ADD(2, t2, t3);
     EPROF_ADD(3, t3, t4);
     EPROF_ADD(4, t4, t5);
-    pos = next_pos;
+    EPROF_ADD(6, t5, t6);
+    pos = P + E;
   }
 
   if (!PROBE && !fail) {
@@ -459,9 +581,9 @@ __device__ __forceinline__ bool wave_is_run(gin_t s, int32_t n) {
 }
 
 // Full per-stream encode with maxout = neblock: run test, entropy probe, main pass.
-template <typename POS>
+template <typename TAB>
 __device__ __forceinline__ StreamResult encode_stream(gin_t in, int32_t n, int clevel, gout_t out,
-                                                      volatile B2H_LDS POS* htab, volatile B2H_LDS uint32_t* tagm,
+                                                      TAB htab, B2H_LDS uint32_t* dbits,
                                                       B2H_LDS uint8_t* oring, bool allow_runs) {
   StreamResult res;
   res.windows = 0;
@@ -479,13 +601,13 @@ __device__ __forceinline__ StreamResult encode_stream(gin_t in, int32_t n, int c
   if (clevel < 2) maxlen /= 8;
   else if (clevel < 4) maxlen /= 4;
   else if (clevel < 7) maxlen /= 2;
-  const LzPassOut pr = lz_pass<true, POS>(in + (n - maxlen), maxlen, hashlog, clevel, out, 0, htab, tagm, oring);
+  const LzPassOut pr = lz_pass<true, TAB>(in + (n - maxlen), maxlen, hashlog, clevel, out, 0, htab, dbits, oring);
   res.windows = pr.windows;
   const double ratio = (double)pr.pos / (double)pr.o;
   // cratio_ thresholds of blosc/blosclz.c:465 (compared in double, as the reference does)
   const double thr = clevel == 1 ? 2.0 : clevel == 2 ? 1.5 : clevel <= 6 ? 1.2 : clevel == 7 ? 1.15 : clevel == 8 ? 1.1 : 1.0;
   if (ratio < thr || n < 16 || n < 66) return res;
-  const LzPassOut em = lz_pass<false, POS>(in, n, hashlog, clevel, out, n, htab, tagm, oring);
+  const LzPassOut em = lz_pass<false, TAB>(in, n, hashlog, clevel, out, n, htab, dbits, oring);
   res.windows += em.windows;
   if (em.fail) return res;
   res.kind = kStreamLz;
@@ -757,31 +879,6 @@ __device__ __forceinline__ int32_t wave_lz_decode_ring(gin_t in, int32_t length,
 }
 
 // ------------------------------------------------------------- window-parallel decoder ----
-// Wave64 inclusive scans with DPP (row shifts inside 16-lane rows, then row broadcasts 15/31).
-// `id` is the identity of the operation: lanes whose DPP source is masked or out of row read it.
-__device__ __forceinline__ int32_t wave_scan_add(int32_t v) {
-  int32_t r = v;
-  r += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
-  r += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
-  r += __builtin_amdgcn_update_dpp(0, v, 0x113, 0xf, 0xf, false);   // row_shr:3
-  r += __builtin_amdgcn_update_dpp(0, r, 0x114, 0xf, 0xe, false);   // row_shr:4, banks 1-3
-  r += __builtin_amdgcn_update_dpp(0, r, 0x118, 0xf, 0xc, false);   // row_shr:8, banks 2-3
-  r += __builtin_amdgcn_update_dpp(0, r, 0x142, 0xa, 0xf, false);   // row_bcast:15, rows 1,3
-  r += __builtin_amdgcn_update_dpp(0, r, 0x143, 0xc, 0xf, false);   // row_bcast:31, rows 2,3
-  return r;
-}
-__device__ __forceinline__ int32_t wave_scan_max(int32_t v) {   // values >= -1
-  int32_t r = v;
-  r = max(r, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));
-  r = max(r, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));
-  r = max(r, __builtin_amdgcn_update_dpp(-1, v, 0x113, 0xf, 0xf, false));
-  r = max(r, __builtin_amdgcn_update_dpp(-1, r, 0x114, 0xf, 0xe, false));
-  r = max(r, __builtin_amdgcn_update_dpp(-1, r, 0x118, 0xf, 0xc, false));
-  r = max(r, __builtin_amdgcn_update_dpp(-1, r, 0x142, 0xa, 0xf, false));
-  r = max(r, __builtin_amdgcn_update_dpp(-1, r, 0x143, 0xc, 0xf, false));
-  return r;
-}
-
 // Four bytes at (lane-varying) offset q of the 512-byte register window w0|w1 (q <= 504).
 __device__ __forceinline__ uint32_t win_dword(const InWin& W, int32_t q) {
   const int32_t d = q >> 2;
