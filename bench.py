@@ -128,6 +128,25 @@ def cpu_baseline(nchunks_sample, chunk_nbytes, threads, reps=5):
                       f"host CPU: {cpu}"}
 
 
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary of this workload
+    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from the FETCH_SIZE/WRITE_SIZE
+    rocprofv3 passes over this same bench command); (None, None) when there is none."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), key=os.path.getmtime):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") != workload:
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if k.split("<")[0].endswith(kernel) and "hbm_bytes_per_launch" in v:
+                best = (v["hbm_bytes_per_launch"], os.path.basename(f))
+    return best if best else (None, None)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -223,20 +242,24 @@ def main():
         # dominant kernel: k_encode; algorithmic bytes per launch = N (read) + C (written)
         alg = shard + total_c
         achieved = alg / (enc * 1e-3) / 1e9
+        workload = ("T: float32 ts=4 SHUFFLE+BloscLZ clevel 5, 256 KiB blocks, "
+                    f"{args.chunk_mib} MiB chunks x {nch} per GPU")
+        traffic, traffic_src = pmc_traffic("k_encode", workload)
         res = {
             "metric": "device-resident GiB/s compress+decompress, f32 shuffle+blosclz, 1/2/4/8 GPU",
             "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic gen_f32 (SURVEY §8d), generated on device",
-            "config": {"workload": "T: float32 ts=4 SHUFFLE+BloscLZ clevel 5, 256 KiB blocks, "
-                                   f"{args.chunk_mib} MiB chunks x {nch} per GPU",
+            "config": {"workload": workload,
                        "chunks_per_gpu": nch, "chunk_bytes": chunk, "clevel": args.clevel,
                        "parallelism": f"chunk-sharded x{world}",
                        "cratio": round(shard / total_c, 4)},
             "roofline": {"bound": "hbm", "kernel": "k_encode", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": None,
+                         "traffic": round(traffic) if traffic else None,
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes": alg,
                          "encode_ms": round(enc, 3), "decode_ms": round(float(np.mean(dec_ms)), 3)},
         }
         if scatter_s is not None:

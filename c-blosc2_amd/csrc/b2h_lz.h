@@ -498,7 +498,15 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
       const int32_t ql = rq - P;
       rseq = (ql < 64 && rq < loop_end) ? (uint32_t)rdlane((int32_t)v, ql) : ldu32(in + rq);
     }
-    if ((visit >> lane) & 1ull) htab.put(h, (uint32_t)p);   // buckets are distinct below W
+    // Below W a bucket repeats only inside a run of equal hashes (left-neighbour lanes); the
+    // serial loop leaves the run's last visited position in it, so only that lane stores (in one
+    // store instruction the surviving lane of a shared address is not specified).
+    {
+      const uint64_t above = ~0ull << lane << 1;                       // lanes > lane
+      const uint64_t brk = ~s1mask & above;                            // lanes that start a new run
+      const uint64_t run = brk ? (above & ((1ull << __builtin_ctzll(brk)) - 1)) : above;
+      if (((visit >> lane) & 1ull) && !(visit & run)) htab.put(h, (uint32_t)p);
+    }
     if (rehash_out && lane == 0) {
       htab.put(lz_hash(rseq, hashlog), (uint32_t)rq);
       if (!PROBE && clevel == 9) htab.put(lz_hash(rseq >> 8, hashlog), (uint32_t)(rq + 1));

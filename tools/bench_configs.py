@@ -1,0 +1,193 @@
+"""The other BASELINE.json configurations on one MI355X (bench.py measures the headline one, T).
+Each prints one JSON line; every run checks its own results.
+
+  C2  shuffle filter only, ts=4, 256 MiB gen_f32: one blosc2_shuffle over the whole buffer and the
+      unshuffle back, bit-exact against the oracle restatement (blosc/shuffle-generic.c).
+  C3  bitshuffle + BloscLZ clevel 5, ts=4, 256 KiB blocks x 4096 chunks (1 GiB gen_f32, continuing
+      global index): exact round trip; the first chunks byte-identical to the oracle.
+  C4  schunk of 10 000 x 1 MiB chunks, DELTA + SHUFFLE + BloscLZ clevel 5, int64 ramp (ts=8, auto
+      512 KiB blocks): exact round trip, sample chunks byte-identical to the oracle.
+  E2E the T workload from and back to pinned host memory: H2D + compress + D2H of the compressed
+      bytes, and H2D of the compressed bytes + decompress + D2H (PCIe-inclusive; never `value`).
+
+    python tools/bench_configs.py [--only C2,C3,C4,E2E] [--steps K]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(REPO, "c-blosc2_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+sys.path.insert(0, REPO)
+import blosc2_amd as B  # noqa: E402
+from bench import gen_f32_device  # noqa: E402
+
+GiB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0
+
+
+def _timed(fn, steps, stream):
+    """Average ms of `fn` over `steps` runs after one warmup, HIP events on `stream`."""
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s = torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()
+    a.record(s)
+    for _ in range(steps):
+        fn()
+    b.record(s)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / steps
+
+
+def c2(steps):
+    from oracle_lib import oracle, p
+    n = 256 << 20
+    src = gen_f32_device(0, n // 4, torch.device("cuda")).view(torch.uint8)
+    dst = torch.empty_like(src)
+    back = torch.empty_like(src)
+    L = B.lib()
+    st = torch.cuda.current_stream().cuda_stream
+    t_s = _timed(lambda: L.b2h_shuffle(4, n, src.data_ptr(), dst.data_ptr(), 0, st), steps, st)
+    t_u = _timed(lambda: L.b2h_shuffle(4, n, dst.data_ptr(), back.data_ptr(), 1, st), steps, st)
+    host = src.cpu().numpy()
+    want = np.empty_like(host)
+    oracle().or_shuffle(4, n, p(host), p(want))
+    exact = bool(np.array_equal(dst.cpu().numpy(), want)) and bool(torch.equal(back, src))
+    return {"config": "C2: shuffle only ts=4, 256 MiB gen_f32, one blosc2_shuffle call", "bit_exact_vs_oracle": exact,
+            "shuffle_ms": round(t_s, 4), "unshuffle_ms": round(t_u, 4),
+            "shuffle_GiBps": round(n / GiB / (t_s * 1e-3), 2), "unshuffle_GiBps": round(n / GiB / (t_u * 1e-3), 2),
+            "roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                         "achieved_shuffle": round(2 * n / (t_s * 1e-3) / 1e9, 1),
+                         "frac_shuffle": round(2 * n / (t_s * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "achieved_unshuffle": round(2 * n / (t_u * 1e-3) / 1e9, 1),
+                         "frac_unshuffle": round(2 * n / (t_u * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+
+
+def _batch_roundtrip(name, src_u8, chunk, nch, cp, steps, check):
+    cap = chunk + 32
+    stride = (cap + 255) // 256 * 256
+    comp = torch.empty(nch * stride, dtype=torch.uint8, device="cuda")
+    cb = torch.zeros(nch, dtype=torch.int32, device="cuda")
+    out = torch.empty(nch * chunk, dtype=torch.uint8, device="cuda")
+    status = torch.zeros(nch, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    enc = lambda: B.compress_batch(cp, src_u8.data_ptr(), chunk, nch, chunk, comp.data_ptr(), stride, cap,  # noqa: E731
+                                   cb.data_ptr(), st)
+    dec = lambda: B.decompress_batch(comp.data_ptr(), stride, cb.data_ptr(), nch, out.data_ptr(), chunk,  # noqa: E731
+                                     chunk, status.data_ptr(), st)
+    t_c = _timed(enc, steps, st)
+    t_d = _timed(dec, steps, st)
+    exact = bool(torch.equal(out, src_u8[:nch * chunk])) and bool((status == chunk).all())
+    C = int(cb.sum().item())
+    N = nch * chunk
+    sample_ok = check(comp, cb, stride)
+    return {"config": name, "round_trip_exact": exact, "sample_chunks_match_oracle": sample_ok,
+            "cratio": round(N / C, 4), "compress_ms": round(t_c, 3), "decompress_ms": round(t_d, 3),
+            "GiBps_c_plus_d": round(N / GiB / ((t_c + t_d) * 1e-3), 3),
+            "roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                         "achieved": round(2 * (N + C) / ((t_c + t_d) * 1e-3) / 1e9, 1),
+                         "frac": round(2 * (N + C) / ((t_c + t_d) * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}}
+
+
+def _oracle_check(src_u8, chunk, idxs, kw):
+    from oracle_lib import oracle_compress
+
+    def check(comp, cb, stride):
+        cbh = cb.cpu().numpy()
+        for i in idxs:
+            raw = src_u8[i * chunk:(i + 1) * chunk].cpu().numpy()
+            want = oracle_compress(raw, **kw)
+            got = comp[i * stride:i * stride + int(cbh[i])].cpu().numpy()
+            if not np.array_equal(got, want):
+                return False
+        return True
+    return check
+
+
+def c3(steps):
+    chunk, nch = 256 << 10, 4096
+    src = gen_f32_device(0, nch * chunk // 4, torch.device("cuda")).view(torch.uint8)
+    kw = dict(clevel=5, typesize=4, filters=(0, 0, 0, 0, 0, B.BITSHUFFLE), blocksize=262144)
+    cp = B.cparams(**kw)
+    return _batch_roundtrip("C3: BITSHUFFLE+BloscLZ clevel 5 ts=4, 256 KiB blocks x 4096 chunks (gen_f32)",
+                            src, chunk, nch, cp, steps, _oracle_check(src, chunk, (0, 1, 2047, 4095), kw))
+
+
+def c4(steps):
+    chunk, nch = 1 << 20, 10000
+    src = torch.arange(0, nch * chunk // 8, dtype=torch.int64, device="cuda").view(torch.uint8)
+    kw = dict(clevel=5, typesize=8, filters=(0, 0, 0, 0, B.DELTA, B.SHUFFLE))
+    cp = B.cparams(**kw)
+    return _batch_roundtrip("C4: schunk 10000 x 1 MiB, DELTA+SHUFFLE+BloscLZ clevel 5, int64 ramp",
+                            src, chunk, nch, cp, steps, _oracle_check(src, chunk, (0, 1, 5000, 9999), kw))
+
+
+def e2e(steps):
+    """T from pinned host memory and back (PCIe-inclusive wall clock, one direction at a time)."""
+    chunk, nch = 4 << 20, 1024
+    N = chunk * nch
+    dev = torch.device("cuda")
+    h_src = torch.empty(N, dtype=torch.uint8, pin_memory=True)
+    h_src.copy_(gen_f32_device(0, N // 4, dev).view(torch.uint8).cpu())
+    cap = chunk + 32
+    stride = (cap + 255) // 256 * 256
+    d_src = torch.empty(N, dtype=torch.uint8, device=dev)
+    comp = torch.empty(nch * stride, dtype=torch.uint8, device=dev)
+    cb = torch.zeros(nch, dtype=torch.int32, device=dev)
+    out = torch.empty(N, dtype=torch.uint8, device=dev)
+    status = torch.zeros(nch, dtype=torch.int32, device=dev)
+    h_comp = torch.empty(nch * stride, dtype=torch.uint8, pin_memory=True)
+    h_out = torch.empty(N, dtype=torch.uint8, pin_memory=True)
+    cp = B.cparams(clevel=5, typesize=4, filters=(0, 0, 0, 0, 0, B.SHUFFLE))
+    st = torch.cuda.current_stream().cuda_stream
+    d_src.copy_(h_src)
+    B.compress_batch(cp, d_src.data_ptr(), chunk, nch, chunk, comp.data_ptr(), stride, cap, cb.data_ptr(), st)
+    torch.cuda.synchronize()
+    C = int(cb.sum().item())
+    tc, td = [], []
+    for _ in range(steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        d_src.copy_(h_src, non_blocking=True)
+        B.compress_batch(cp, d_src.data_ptr(), chunk, nch, chunk, comp.data_ptr(), stride, cap, cb.data_ptr(), st)
+        h_comp[:C].copy_(comp[:C], non_blocking=True)   # the compressed bytes (chunk gather not timed apart)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        comp[:C].copy_(h_comp[:C], non_blocking=True)
+        B.decompress_batch(comp.data_ptr(), stride, cb.data_ptr(), nch, out.data_ptr(), chunk, chunk,
+                           status.data_ptr(), st)
+        h_out.copy_(out, non_blocking=True)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        tc.append(t1 - t0)
+        td.append(t2 - t1)
+    exact = bool(torch.equal(h_out, h_src))
+    tcm, tdm = float(np.median(tc)), float(np.median(td))
+    return {"config": "E2E: T from/to pinned host memory (H2D + compress + D2H of C bytes; H2D of C bytes + "
+                      "decompress + D2H)", "round_trip_exact": exact, "cratio": round(N / C, 4),
+            "compress_GiBps": round(N / GiB / tcm, 3), "decompress_GiBps": round(N / GiB / tdm, 3),
+            "GiBps_c_plus_d": round(N / GiB / (tcm + tdm), 3)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="C2,C3,C4,E2E")
+    ap.add_argument("--steps", type=int, default=3)
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    for name in args.only.split(","):
+        r = {"C2": c2, "C3": c3, "C4": c4, "E2E": e2e}[name](args.steps)
+        print(json.dumps(r), flush=True)
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -18,8 +18,11 @@ __global__ __launch_bounds__(64) void k_enc(const uint8_t* in, int32_t n, int cl
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int hashlog = clevel == 1 ? 12 : (clevel == 2 ? 13 : 14);
 #ifdef ENC_GTAB
-  GlbTab<uint16_t> htab;
-  htab.t = (B2H_GLB uint16_t*)(gtab + ((size_t)blockIdx.x << hashlog));
+#ifndef ENC_GPOS
+#define ENC_GPOS uint16_t
+#endif
+  GlbTab<ENC_GPOS> htab;
+  htab.t = (B2H_GLB ENC_GPOS*)((ENC_GPOS*)gtab + ((size_t)blockIdx.x << hashlog));
   B2H_LDS uint32_t* dbits = (B2H_LDS uint32_t*)smem;
   B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + ((1 << hashlog) >> 3));
 #else
@@ -66,7 +69,7 @@ int main(int argc, char** argv) {
   const size_t lds = enc_lds_bytes(2, 14);
 #endif
   uint16_t* gtab;
-  hipMalloc(&gtab, (size_t)maxblk * (2 << 14));
+  hipMalloc(&gtab, (size_t)maxblk * (4 << 14));
   std::vector<int> sizes = {1, 256, 1024};
   if (argc > 4) sizes = {atoi(argv[4])};
   for (int nblk : sizes) {

@@ -22,4 +22,5 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 200 rocprofv3 --pmc $ctr --kernel-include-regex "k_encode|k_decode|k_ffilter|k_dfilter|k_scatter" --output-format csv \
       -d $O/pmc_${TAG}_$ctr -o run -- python3 -u $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/pmc_${TAG}_$ctr.log 2>&1 || { echo "pmc $ctr failed"; tail -20 $O/pmc_${TAG}_$ctr.log; exit 1; }
 done
+python3 $R/tools/pmc_traffic.py $O $TAG $O/pmc_traffic_$TAG.json > /dev/null && echo "traffic summary: gpurun_out/pmc_traffic_$TAG.json"
 echo DONE
