@@ -202,36 +202,22 @@ __global__ __launch_bounds__(kBlockThreads) void k_ffilter(CGeom g, int pass, ui
   }
 }
 
-// Persistent encoder: one wave per workgroup, as many workgroups as fit on the chip (LDS-bound),
-// each pulling stream indices from a device counter until the batch is exhausted.  Stream cost
-// varies ~100x (a float32 mantissa plane vs an all-zero exponent plane) and the hardware deals
-// workgroups to XCDs / shader engines by index, so one-workgroup-per-stream left most slots
-// waiting behind the expensive planes; pulling keeps every resident wave busy.  Every wave exits
-// once the counter passes `nstreams_total`.  Dynamic LDS: hash table + bucket bitset + output ring.
-// GTAB: the hash table lives in global memory (`gtab`, one table per workgroup slot) and LDS holds
-// only the bucket bitset and the output ring, so occupancy is set by registers, not LDS (see
-// GlbTab in b2h_lz.h).
-template <typename POS, bool GTAB>
-__global__ __launch_bounds__(64) void k_encode(CGeom g, const uint8_t* __restrict__ filt,
-                                               uint8_t* __restrict__ sbuf, StreamResult* __restrict__ res,
-                                               int32_t nstreams_total, int32_t* __restrict__ next,
-                                               POS* __restrict__ gtab) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
-  typedef typename std::conditional<GTAB, GlbTab<POS>, LdsTab<POS>>::type Tab;
-  Tab htab;
-  size_t bits_off, ring_off;
-  if constexpr (GTAB) {
-    htab.t = (B2H_GLB POS*)(gtab + ((size_t)blockIdx.x << hashlog));
-    bits_off = 0;
-    ring_off = (size_t(1) << hashlog) >> 3;
-  } else {
-    htab.t = (volatile B2H_LDS POS*)(smem);
-    bits_off = enc_bits_offset(sizeof(POS), hashlog);
-    ring_off = enc_ring_offset(sizeof(POS), hashlog);
-  }
-  B2H_LDS uint32_t* dbits = (B2H_LDS uint32_t*)(smem + bits_off);
-  B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + ring_off);
+// Persistent encoder: as many workgroups as fit on the chip, every wave pulling stream indices
+// from a device counter until the batch is exhausted.  Stream cost varies ~100x (a float32
+// mantissa plane vs an all-zero exponent plane) and the hardware deals workgroups to XCDs / shader
+// engines by index, so one-workgroup-per-stream left most slots waiting behind the expensive
+// planes; pulling keeps every resident wave busy.  Every wave exits once the counter passes
+// `nstreams_total`.
+//
+// A workgroup holds NLDS waves whose hash table lives in LDS and NGLB waves whose table lives in
+// global memory (`gtab`, one per wave slot, see GlbTab in b2h_lz.h).  LDS tables cost 32 KiB per
+// wave (4 waves per CU); global tables cost L2/MALL traffic instead.  Dynamic LDS layout:
+// [NLDS tables][per wave: bucket bitset + output ring].
+template <typename TAB>
+__device__ __forceinline__ void encode_loop(const CGeom& g, TAB htab, B2H_LDS uint32_t* dbits, B2H_LDS uint8_t* oring,
+                                            const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
+                                            StreamResult* __restrict__ res, int32_t nstreams_total,
+                                            int32_t* __restrict__ next) {
   for (;;) {
     // branch-free grab: every lane takes part (lane 0 adds 1, the others 0), so no divergent
     // region sits between the atomic and the broadcast -- with a lane-0 branch the structurizer
@@ -245,10 +231,39 @@ __global__ __launch_bounds__(64) void k_encode(CGeom g, const uint8_t* __restric
     gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide time base
-    StreamResult r = encode_stream<Tab>(in, len, g.clevel, out, htab, dbits, oring, g.overhead == kHdrExt);
+    StreamResult r = encode_stream<TAB>(in, len, g.clevel, out, htab, dbits, oring, g.overhead == kHdrExt);
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
     if (lane_id() == 0) res[s] = r;
+  }
+}
+
+__host__ __device__ constexpr size_t enc_wave_lds(int hashlog) { return ((size_t(1) << hashlog) >> 3) + kOutRing; }
+template <typename POS>
+__host__ __device__ constexpr size_t enc_wg_lds(int hashlog, int nlds, int nglb) {
+  return (size_t)nlds * (sizeof(POS) << hashlog) + (size_t)(nlds + nglb) * enc_wave_lds(hashlog);
+}
+
+template <typename POS, int NLDS, int NGLB>
+__global__ __launch_bounds__(64 * (NLDS + NGLB)) void k_encode(CGeom g, const uint8_t* __restrict__ filt,
+                                                               uint8_t* __restrict__ sbuf, StreamResult* __restrict__ res,
+                                                               int32_t nstreams_total, int32_t* __restrict__ next,
+                                                               POS* __restrict__ gtab) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const size_t tabsz = sizeof(POS) << hashlog;
+  B2H_LDS uint8_t* mine = (B2H_LDS uint8_t*)(smem + NLDS * tabsz + w * enc_wave_lds(hashlog));
+  B2H_LDS uint32_t* dbits = (B2H_LDS uint32_t*)mine;
+  B2H_LDS uint8_t* oring = mine + ((size_t(1) << hashlog) >> 3);
+  if (NLDS > 0 && w < NLDS) {
+    LdsTab<POS> t;
+    t.t = (volatile B2H_LDS POS*)(smem + w * tabsz);
+    encode_loop(g, t, dbits, oring, filt, sbuf, res, nstreams_total, next);
+  } else if (NGLB > 0) {
+    GlbTab<POS> t;
+    t.t = (B2H_GLB POS*)(gtab + (((size_t)blockIdx.x * NGLB + (w - NLDS)) << hashlog));
+    encode_loop(g, t, dbits, oring, filt, sbuf, res, nstreams_total, next);
   }
 }
 
@@ -490,6 +505,62 @@ static bool hostside_trunc_ok(int8_t prec, int32_t ts, int* zeroed) {
   return *zeroed < mant;
 }
 
+// Encoder workgroup shape: B2H_ENC_MODE = "lds" (one LDS-table wave per workgroup), "glb" (one
+// global-table wave), or "hybN" (one LDS-table wave + N global-table waves).  Default: hyb3, i.e.
+// 3 LDS-table + 9 global-table waves per CU (T bench: lds 54.2 ms, glb 30.3, hyb1 34.4, hyb2 33.1,
+// hyb3 28.7, hyb4 32.3 ms per 4 GiB encode -- more global tables than that overflow L2 into MALL).
+static void enc_mode(int* nlds, int* nglb) {
+  static int ml = -1, mg = -1;
+  if (ml < 0) {
+    const char* e = getenv("B2H_ENC_MODE");
+    ml = 1; mg = 3;
+    if (e && !strcmp(e, "lds")) { ml = 1; mg = 0; }
+    else if (e && !strcmp(e, "glb")) { ml = 0; mg = 1; }
+    else if (e && !strncmp(e, "hyb", 3)) { ml = 1; mg = std::max(1, std::min(4, atoi(e + 3))); }
+  }
+  *nlds = ml;
+  *nglb = mg;
+}
+
+template <typename POS, int NL, int NG>
+static int launch_encode_shape(Workspace* ws, const CGeom& g, int hashlog, const uint8_t* filt, StreamResult* res,
+                               int64_t ntot, int32_t* next, hipStream_t st) {
+  const void* fn = reinterpret_cast<const void*>(&k_encode<POS, NL, NG>);
+  const size_t lds = enc_wg_lds<POS>(hashlog, NL, NG);
+  static bool attr_set = false;
+  if (!attr_set) {   // > 64 KiB of dynamic LDS per workgroup: opt in once
+    HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  int dev = 0, per_cu = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * (NL + NG), lds) != hipSuccess) per_cu = 1;
+  const int64_t slots = (int64_t)std::max(1, per_cu) * std::max(1, ncu);
+  const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>((ntot + NL + NG - 1) / (NL + NG), slots));
+  POS* gt = nullptr;
+  if (NG > 0) {
+    if (ws->gtab.ensure(((size_t)grid * NG << hashlog) * sizeof(POS))) return E_MEMORY;
+    gt = ws->gtab.as<POS>();
+  }
+  k_encode<POS, NL, NG><<<grid, 64 * (NL + NG), lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, gt);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+template <typename POS>
+static int launch_encode(Workspace* ws, const CGeom& g, int hashlog, const uint8_t* filt, StreamResult* res,
+                         int64_t ntot, int32_t* next, hipStream_t st) {
+  int nl, ng;
+  enc_mode(&nl, &ng);
+  if (nl == 1 && ng == 0) return launch_encode_shape<POS, 1, 0>(ws, g, hashlog, filt, res, ntot, next, st);
+  if (nl == 0) return launch_encode_shape<POS, 0, 1>(ws, g, hashlog, filt, res, ntot, next, st);
+  if (ng == 1) return launch_encode_shape<POS, 1, 1>(ws, g, hashlog, filt, res, ntot, next, st);
+  if (ng == 2) return launch_encode_shape<POS, 1, 2>(ws, g, hashlog, filt, res, ntot, next, st);
+  if (ng == 3) return launch_encode_shape<POS, 1, 3>(ws, g, hashlog, filt, res, ntot, next, st);
+  return launch_encode_shape<POS, 1, 4>(ws, g, hashlog, filt, res, ntot, next, st);
+}
+
 int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stride, int32_t nchunks, uint8_t* d_dst,
                    int64_t dst_stride, int32_t* d_cbytes, hipStream_t st) {
   if (nchunks <= 0) return 0;
@@ -603,33 +674,9 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
   int32_t* next = ws->qctr.as<int32_t>();
   HIPCHK(hipMemsetAsync(next, 0, sizeof(int32_t), st));
   {
-    static const bool gtab = getenv("B2H_ENC_GTAB") != nullptr && atoi(getenv("B2H_ENC_GTAB")) != 0;
-    const size_t pos_bytes = small ? sizeof(uint16_t) : sizeof(uint32_t);
-    const void* fn = small ? (gtab ? reinterpret_cast<const void*>(&k_encode<uint16_t, true>)
-                                   : reinterpret_cast<const void*>(&k_encode<uint16_t, false>))
-                           : (gtab ? reinterpret_cast<const void*>(&k_encode<uint32_t, true>)
-                                   : reinterpret_cast<const void*>(&k_encode<uint32_t, false>));
-    const size_t lds = gtab ? (((size_t(1) << hashlog) >> 3) + kOutRing) : enc_lds_bytes(pos_bytes, hashlog);
-    static bool attr_set = false;
-    if (!attr_set) {   // > 64 KiB of dynamic LDS per workgroup: opt in once
-      HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_encode<uint32_t, false>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      attr_set = true;
-    }
-    const uint32_t grid = (uint32_t)std::min<int64_t>(ntot, resident_slots(fn, lds));
-    void* gt = nullptr;
-    if (gtab) {
-      if (ws->gtab.ensure(((size_t)grid << hashlog) * pos_bytes)) return E_MEMORY;
-      gt = ws->gtab.p;
-    }
-    uint8_t* sb = ws->sbuf.as<uint8_t>();
-    if (small) {
-      if (gtab) k_encode<uint16_t, true><<<grid, 64, lds, st>>>(g, filt, sb, res, (int32_t)ntot, next, (uint16_t*)gt);
-      else k_encode<uint16_t, false><<<grid, 64, lds, st>>>(g, filt, sb, res, (int32_t)ntot, next, nullptr);
-    } else {
-      if (gtab) k_encode<uint32_t, true><<<grid, 64, lds, st>>>(g, filt, sb, res, (int32_t)ntot, next, (uint32_t*)gt);
-      else k_encode<uint32_t, false><<<grid, 64, lds, st>>>(g, filt, sb, res, (int32_t)ntot, next, nullptr);
-    }
+    rc = small ? launch_encode<uint16_t>(ws, g, hashlog, filt, res, ntot, next, st)
+               : launch_encode<uint32_t>(ws, g, hashlog, filt, res, ntot, next, st);
+    if (rc) return rc;
   }
   ev_encode.stop(st);
   HIPCHK(hipGetLastError());

@@ -13,7 +13,12 @@
 #include "b2h_lz.h"
 using namespace b2h;
 
-__global__ __launch_bounds__(64) void k_enc(const uint8_t* in, int32_t n, int clevel, uint8_t* out, int64_t* cycles,
+#ifdef ENC_WPE
+#define ENC_ATTR __attribute__((amdgpu_waves_per_eu(ENC_WPE, ENC_WPE)))
+#else
+#define ENC_ATTR
+#endif
+__global__ __launch_bounds__(64) ENC_ATTR void k_enc(const uint8_t* in, int32_t n, int clevel, uint8_t* out, int64_t* cycles,
                                             StreamResult* res, uint16_t* gtab) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int hashlog = clevel == 1 ? 12 : (clevel == 2 ? 13 : 14);
