@@ -974,10 +974,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_dfilter(DChunk* __restrict__ 
     case kShuffle: block_unshuffle(s, o, bsize, meta ? meta : d.typesize); break;
     case kBitshuffle: block_bitunshuffle(s, o, bsize, d.typesize, d.version); break;
     case kDelta:
-      for (int32_t i = threadIdx.x; i < bsize; i += blockDim.x) o[i] = s[i];
-      __syncthreads();
-      if (bk.block == 0) block_delta_decode_first(o, bsize, d.typesize);
-      else block_delta_decode_rest(dsts[bk.chunk], o, bsize, d.typesize);
+      if (bk.block == 0) block_delta_decode_first(s, o, bsize, d.typesize);
+      else block_delta_decode_rest(s, dsts[bk.chunk], o, bsize, d.typesize);
       break;
     default: break;
   }
@@ -1114,30 +1112,30 @@ int decompress_batch_strided(const uint8_t* d_src, int64_t src_stride, const int
 // ============================================================================ raw filters ====
 __global__ __launch_bounds__(kBlockThreads) void k_raw_shuffle(const uint8_t* __restrict__ s, uint8_t* __restrict__ d,
                                                                int32_t nbytes, int32_t ts, int inverse) {
-  // one workgroup over the whole buffer is far too slow for 256 MiB; split into planes-major
-  // tiles: every workgroup owns elements [e0, e1) of all planes.
+  // blosc2_shuffle over a whole buffer (blosc/shuffle.c:416-449): every workgroup owns elements
+  // [e0, e1) of all planes (plane stride n), 16-byte element-side loads / u32 plane-side stores
   const int32_t n = nbytes / ts;
   const int32_t per = ((n + gridDim.x - 1) / gridDim.x + 3) & ~3;
   const int32_t e0 = min(n, (int32_t)blockIdx.x * per), e1 = min(n, e0 + per);
   if (e0 < e1) {
     const int32_t cnt = e1 - e0;
-    const bool fast = (cnt % 4 == 0) && (n % 4 == 0) && (e0 % 4 == 0) &&
-                      aligned16(s) && aligned16(d) && (ts == 2 || ts == 4 || ts == 8 || ts == 16);
+    const bool fast = (cnt % 4 == 0) && (n % 4 == 0) && aligned16(s) && aligned16(d) &&
+                      (ts == 2 || ts == 4 || ts == 8 || ts == 16);
     if (fast) {
-      for (int32_t q = threadIdx.x; q < cnt / 4; q += blockDim.x) {
-        const int32_t e = e0 + 4 * q;
-        if (!inverse) {
-          for (int plane = 0; plane < ts; plane++) {
-            uint32_t o = 0;
-            for (int k = 0; k < 4; k++) o |= (uint32_t)s[(int64_t)(e + k) * ts + plane] << (8 * k);
-            *reinterpret_cast<uint32_t*>(d + (int64_t)plane * n + e) = o;
-          }
-        } else {
-          for (int plane = 0; plane < ts; plane++) {
-            const uint32_t w = *reinterpret_cast<const uint32_t*>(s + (int64_t)plane * n + e);
-            for (int k = 0; k < 4; k++) d[(int64_t)(e + k) * ts + plane] = (uint8_t)(w >> (8 * k));
-          }
-        }
+      const uint8_t* es = (inverse ? d : s) + (int64_t)e0 * ts;   // element side
+      const uint8_t* ps = (inverse ? s : d) + e0;                  // plane side
+      if (!inverse) {
+        uint8_t* pd = d + e0;
+        if (ts == 4) shuffle_fast<4>(es, pd, cnt, n);
+        else if (ts == 8) shuffle_fast<8>(es, pd, cnt, n);
+        else if (ts == 2) shuffle_fast<2>(es, pd, cnt, n);
+        else shuffle_fast<16>(es, pd, cnt, n);
+      } else {
+        uint8_t* ed = d + (int64_t)e0 * ts;
+        if (ts == 4) unshuffle_fast<4>(ps, ed, cnt, n);
+        else if (ts == 8) unshuffle_fast<8>(ps, ed, cnt, n);
+        else if (ts == 2) unshuffle_fast<2>(ps, ed, cnt, n);
+        else unshuffle_fast<16>(ps, ed, cnt, n);
       }
     } else {
       for (int64_t i = threadIdx.x; i < (int64_t)cnt * ts; i += blockDim.x) {

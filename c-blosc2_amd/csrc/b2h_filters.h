@@ -20,8 +20,9 @@ __device__ __forceinline__ uint32_t byte_of(uint32_t w, int k) { return (w >> (8
 // ------------------------------------------------------------------------------- shuffle ----
 // Fast path: TS in {2,4,8,16}, n % 4 == 0, 16-byte aligned src/dst.  Thread t owns elements
 // [4t, 4t+4): it reads 4*TS contiguous bytes and writes one u32 into each of the TS planes.
+// `n` elements from `src`; plane p of `dst` starts at dst + p * pstride (pstride = n for a block).
 template <int TS>
-__device__ void shuffle_fast(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t n) {
+__device__ void shuffle_fast(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t n, int64_t pstride) {
   const int32_t quads = n / 4;
   for (int32_t q = threadIdx.x; q < quads; q += blockDim.x) {
     uint32_t w[TS];   // 4*TS bytes = elements 4q..4q+3
@@ -44,18 +45,18 @@ __device__ void shuffle_fast(const uint8_t* __restrict__ src, uint8_t* __restric
         const int byte = e * TS + plane;     // byte index inside the 4*TS bytes
         o |= byte_of(w[byte / 4], byte % 4) << (8 * e);
       }
-      reinterpret_cast<uint32_t*>(dst + (int64_t)plane * n)[q] = o;
+      reinterpret_cast<uint32_t*>(dst + (int64_t)plane * pstride)[q] = o;
     }
   }
 }
 
 template <int TS>
-__device__ void unshuffle_fast(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t n) {
+__device__ void unshuffle_fast(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t n, int64_t pstride) {
   const int32_t quads = n / 4;
   for (int32_t q = threadIdx.x; q < quads; q += blockDim.x) {
     uint32_t p[TS];
 #pragma unroll
-    for (int plane = 0; plane < TS; plane++) p[plane] = reinterpret_cast<const uint32_t*>(src + (int64_t)plane * n)[q];
+    for (int plane = 0; plane < TS; plane++) p[plane] = reinterpret_cast<const uint32_t*>(src + (int64_t)plane * pstride)[q];
     uint32_t w[TS];
 #pragma unroll
     for (int k = 0; k < TS; k++) {
@@ -83,10 +84,10 @@ __device__ __forceinline__ bool aligned16(const void* p) { return (reinterpret_c
 __device__ void block_shuffle(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t bsize, int32_t ts) {
   const int32_t n = bsize / ts;
   const bool fast = (n % 4 == 0) && aligned16(src) && aligned16(dst);
-  if (fast && ts == 4) shuffle_fast<4>(src, dst, n);
-  else if (fast && ts == 8) shuffle_fast<8>(src, dst, n);
-  else if (fast && ts == 2) shuffle_fast<2>(src, dst, n);
-  else if (fast && ts == 16) shuffle_fast<16>(src, dst, n);
+  if (fast && ts == 4) shuffle_fast<4>(src, dst, n, n);
+  else if (fast && ts == 8) shuffle_fast<8>(src, dst, n, n);
+  else if (fast && ts == 2) shuffle_fast<2>(src, dst, n, n);
+  else if (fast && ts == 16) shuffle_fast<16>(src, dst, n, n);
   else if (ts == 1) {
     for (int32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
   } else {
@@ -101,10 +102,10 @@ __device__ void block_shuffle(const uint8_t* __restrict__ src, uint8_t* __restri
 __device__ void block_unshuffle(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t bsize, int32_t ts) {
   const int32_t n = bsize / ts;
   const bool fast = (n % 4 == 0) && aligned16(src) && aligned16(dst);
-  if (fast && ts == 4) unshuffle_fast<4>(src, dst, n);
-  else if (fast && ts == 8) unshuffle_fast<8>(src, dst, n);
-  else if (fast && ts == 2) unshuffle_fast<2>(src, dst, n);
-  else if (fast && ts == 16) unshuffle_fast<16>(src, dst, n);
+  if (fast && ts == 4) unshuffle_fast<4>(src, dst, n, n);
+  else if (fast && ts == 8) unshuffle_fast<8>(src, dst, n, n);
+  else if (fast && ts == 2) unshuffle_fast<2>(src, dst, n, n);
+  else if (fast && ts == 16) unshuffle_fast<16>(src, dst, n, n);
   else if (ts == 1) {
     for (int32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
   } else {
@@ -128,11 +129,86 @@ __device__ __forceinline__ uint64_t bit_transpose8(uint64_t x) {
   return x;
 }
 
+// Fast bitshuffle, TS in {1,2,4,8}, m % 32 == 0, 16-byte aligned: a thread owns 32 consecutive
+// elements (4 groups of 8), reads them with 16-byte loads and writes one u32 (4 group bytes) per
+// bit row, so both sides are coalesced.
+template <int TS>
+__device__ void bitshuffle_fast(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t m) {
+  const int32_t rowlen = m / 8;
+  for (int32_t t = threadIdx.x; t < m / 32; t += blockDim.x) {
+    uint32_t w[8 * TS];   // 32 * TS bytes
+    const uint4* s16 = reinterpret_cast<const uint4*>(src + (int64_t)t * 32 * TS);
+#pragma unroll
+    for (int k = 0; k < 2 * TS; k++) {
+      const uint4 v = s16[k];
+      w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+    }
+#pragma unroll
+    for (int b = 0; b < TS; b++) {
+      uint32_t o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        uint64_t x = 0;
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+          const int byte = (8 * j + r) * TS + b;
+          x |= (uint64_t)byte_of(w[byte / 4], byte % 4) << (8 * r);
+        }
+        x = bit_transpose8(x);
+#pragma unroll
+        for (int k = 0; k < 8; k++) o[k] |= (uint32_t)((x >> (8 * k)) & 0xff) << (8 * j);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) reinterpret_cast<uint32_t*>(dst + (int64_t)(8 * b + k) * rowlen)[t] = o[k];
+    }
+  }
+}
+
+template <int TS>
+__device__ void bitunshuffle_fast(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t m) {
+  const int32_t rowlen = m / 8;
+  for (int32_t t = threadIdx.x; t < m / 32; t += blockDim.x) {
+    uint32_t w[8 * TS];
+#pragma unroll
+    for (int i = 0; i < 8 * TS; i++) w[i] = 0;
+#pragma unroll
+    for (int b = 0; b < TS; b++) {
+      uint32_t rows[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) rows[k] = reinterpret_cast<const uint32_t*>(src + (int64_t)(8 * b + k) * rowlen)[t];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        uint64_t y = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) y |= (uint64_t)byte_of(rows[k], j) << (8 * k);
+        y = bit_transpose8(y);
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+          const int byte = (8 * j + r) * TS + b;
+          w[byte / 4] |= (uint32_t)((y >> (8 * r)) & 0xff) << (8 * (byte % 4));
+        }
+      }
+    }
+    uint4* d16 = reinterpret_cast<uint4*>(dst + (int64_t)t * 32 * TS);
+#pragma unroll
+    for (int k = 0; k < 2 * TS; k++) d16[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+  }
+}
+
 // Output row r = 8*b + k (b: byte of the element, k: bit) has m/8 bytes; byte g of row r packs
 // bit k of byte b of elements 8g..8g+7 (element 8g+i in bit i).  Thread g owns one 8-element group.
 __device__ void block_bitshuffle(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t bsize, int32_t ts) {
   const int32_t m = (bsize / ts) & ~7;
   const int32_t rowlen = m / 8;
+  const bool fast = (m % 32) == 0 && aligned16(src) && aligned16(dst);
+  if (fast && (ts == 1 || ts == 2 || ts == 4 || ts == 8)) {
+    if (ts == 4) bitshuffle_fast<4>(src, dst, m);
+    else if (ts == 8) bitshuffle_fast<8>(src, dst, m);
+    else if (ts == 2) bitshuffle_fast<2>(src, dst, m);
+    else bitshuffle_fast<1>(src, dst, m);
+    for (int32_t i = m * ts + threadIdx.x; i < bsize; i += blockDim.x) dst[i] = src[i];
+    return;
+  }
   for (int32_t g = threadIdx.x; g < rowlen; g += blockDim.x) {
     const uint8_t* e8 = src + (int64_t)g * 8 * ts;   // 8 consecutive elements
     for (int32_t b = 0; b < ts; b++) {
@@ -158,6 +234,14 @@ __device__ void block_bitunshuffle(const uint8_t* __restrict__ src, uint8_t* __r
   }
   const int32_t m = n & ~7;
   const int32_t rowlen = m / 8;
+  if ((m % 32) == 0 && aligned16(src) && aligned16(dst) && (ts == 1 || ts == 2 || ts == 4 || ts == 8)) {
+    if (ts == 4) bitunshuffle_fast<4>(src, dst, m);
+    else if (ts == 8) bitunshuffle_fast<8>(src, dst, m);
+    else if (ts == 2) bitunshuffle_fast<2>(src, dst, m);
+    else bitunshuffle_fast<1>(src, dst, m);
+    for (int32_t i = m * ts + threadIdx.x; i < bsize; i += blockDim.x) dst[i] = src[i];
+    return;
+  }
   for (int32_t g = threadIdx.x; g < rowlen; g += blockDim.x) {
     uint8_t* e8 = dst + (int64_t)g * 8 * ts;
     for (int32_t b = 0; b < ts; b++) {
@@ -178,63 +262,131 @@ __device__ __forceinline__ int delta_width(int32_t ts) {
   return (ts % 8 == 0) ? 8 : 1;
 }
 
+// XOR delta works on w-byte words, byte lanes independent: it is processed in 8-byte chunks
+// (little-endian), every chunk holding 8 / w words.
+// Prefix XOR of the words inside one chunk.
+__device__ __forceinline__ uint64_t xor_prefix64(uint64_t x, int w) {
+  if (w == 1) x ^= x << 8;
+  if (w <= 2) x ^= x << 16;
+  if (w <= 4) x ^= x << 32;
+  return x;
+}
+// The chunk's last word, replicated over the 8 bytes (the carry into the next chunk).
+__device__ __forceinline__ uint64_t xor_last_word64(uint64_t x, int w) {
+  uint64_t t = w == 8 ? x : x >> (64 - 8 * w);
+  if (w == 1) t |= t << 8;
+  if (w <= 2) t |= t << 16;
+  if (w <= 4) t |= t << 32;
+  return t;
+}
+// The chunk shifted up by one word, the previous chunk's last word entering at the bottom.
+__device__ __forceinline__ uint64_t shift_in_word64(uint64_t x, uint64_t prev, int w) {
+  return w == 8 ? prev : (x << (8 * w)) | (prev >> (64 - 8 * w));
+}
+
 // Encoder.  Block 0: d[i] = s[i] ^ s[i-1] over w-byte words (d[0] = s[0]); `cur` is the stage
 // input (the reference passes _src as dref for block 0).  Other blocks: d = s ^ dref where dref is
 // the chunk's block-0 region of the pipeline input (blosc/blosc2.c:1126-1128).  Only
-// (bsize / w) * w bytes are written, as in the reference.
+// (bsize / w) * w bytes are written, as in the reference.  16 B per lane when aligned.
 __device__ void block_delta_encode(const uint8_t* __restrict__ cur, const uint8_t* __restrict__ dref,
                                    uint8_t* __restrict__ dst, int32_t bsize, int32_t ts, bool first_block) {
   const int w = delta_width(ts);
   const int32_t nb = bsize / w * w;
-  if (first_block) {
-    for (int32_t i = threadIdx.x; i < nb; i += blockDim.x) dst[i] = i < w ? cur[i] : (uint8_t)(cur[i] ^ cur[i - w]);
-  } else if ((nb % 16) == 0 && aligned16(cur) && aligned16(dref) && aligned16(dst)) {
+  const bool vec = (nb % 16) == 0 && aligned16(cur) && aligned16(dst) && (first_block || aligned16(dref));
+  if (vec && first_block) {
+    const ulonglong2* c16 = reinterpret_cast<const ulonglong2*>(cur);
+    for (int32_t i = threadIdx.x; i < nb / 16; i += blockDim.x) {
+      const ulonglong2 v = c16[i];
+      const uint64_t prev = i ? reinterpret_cast<const uint64_t*>(cur)[2 * i - 1] : 0ull;
+      ulonglong2 o;
+      o.x = v.x ^ shift_in_word64(v.x, prev, w);
+      o.y = v.y ^ shift_in_word64(v.y, v.x, w);
+      reinterpret_cast<ulonglong2*>(dst)[i] = o;
+    }
+  } else if (vec) {
     for (int32_t i = threadIdx.x; i < nb / 16; i += blockDim.x) {
       uint4 a = reinterpret_cast<const uint4*>(cur)[i], b = reinterpret_cast<const uint4*>(dref)[i];
       reinterpret_cast<uint4*>(dst)[i] = make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
     }
+  } else if (first_block) {
+    for (int32_t i = threadIdx.x; i < nb; i += blockDim.x) dst[i] = i < w ? cur[i] : (uint8_t)(cur[i] ^ cur[i - w]);
   } else {
     for (int32_t i = threadIdx.x; i < nb; i += blockDim.x) dst[i] = cur[i] ^ dref[i];
   }
 }
 
-// Decoder for blocks >= 1 (in place): d ^= decoded block 0.
-__device__ void block_delta_decode_rest(const uint8_t* __restrict__ dref, uint8_t* __restrict__ d, int32_t bsize, int32_t ts) {
+// Decoder for blocks >= 1: d = s ^ decoded block 0 (bytes past (bsize / w) * w are copied).
+__device__ void block_delta_decode_rest(const uint8_t* __restrict__ s, const uint8_t* __restrict__ dref,
+                                        uint8_t* __restrict__ d, int32_t bsize, int32_t ts) {
   const int w = delta_width(ts);
   const int32_t nb = bsize / w * w;
-  if ((nb % 16) == 0 && aligned16(dref) && aligned16(d)) {
+  int32_t done = 0;
+  if (aligned16(s) && aligned16(dref) && aligned16(d)) {
+    done = nb / 16 * 16;
     for (int32_t i = threadIdx.x; i < nb / 16; i += blockDim.x) {
-      uint4 a = reinterpret_cast<uint4*>(d)[i], b = reinterpret_cast<const uint4*>(dref)[i];
+      uint4 a = reinterpret_cast<const uint4*>(s)[i], b = reinterpret_cast<const uint4*>(dref)[i];
       reinterpret_cast<uint4*>(d)[i] = make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
     }
-  } else {
-    for (int32_t i = threadIdx.x; i < nb; i += blockDim.x) d[i] ^= dref[i];
   }
+  for (int32_t i = done + threadIdx.x; i < bsize; i += blockDim.x) d[i] = i < nb ? (uint8_t)(s[i] ^ dref[i]) : s[i];
 }
 
-// Decoder for block 0 (in place): running XOR over w-byte words = inclusive XOR-scan.  Each
-// thread scans a contiguous segment, the segment totals are XOR-scanned through LDS, then each
-// segment is re-walked with its carry.  Byte-wise: d[x] ^= d[x - w] serially == XOR of the bytes
-// x, x-w, x-2w, ... so the scan runs on w-byte words.
-__device__ void block_delta_decode_first(uint8_t* __restrict__ d, int32_t bsize, int32_t ts) {
+// Decoder for block 0: running XOR over w-byte words = inclusive XOR-scan (blosc/delta.c:96-161).
+// Each thread scans a contiguous run of 16-byte pieces, the run totals are XOR-scanned through
+// LDS, then each run is re-walked with its carry.  Scalar word path when unaligned.
+__device__ void block_delta_decode_first(const uint8_t* __restrict__ s, uint8_t* __restrict__ d, int32_t bsize,
+                                         int32_t ts) {
   __shared__ uint64_t carry[kBlockThreads];
   const int w = delta_width(ts);
+  const int32_t nb = bsize / w * w;
+  if ((nb % 16) == 0 && aligned16(s) && aligned16(d)) {
+    const int32_t n16 = nb / 16;
+    const int32_t per = (n16 + blockDim.x - 1) / blockDim.x;
+    const int32_t lo = min(n16, (int32_t)threadIdx.x * per), hi = min(n16, lo + per);
+    const ulonglong2* s16 = reinterpret_cast<const ulonglong2*>(s);
+    uint64_t run = 0;
+    for (int32_t i = lo; i < hi; i++) {
+      const ulonglong2 v = s16[i];
+      run = xor_last_word64(xor_prefix64(v.x, w) ^ run, w);
+      run = xor_last_word64(xor_prefix64(v.y, w) ^ run, w);
+    }
+    carry[threadIdx.x] = run;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint64_t acc = 0;
+      for (int t = 0; t < (int)blockDim.x; t++) { const uint64_t v = carry[t]; carry[t] = acc; acc ^= v; }
+    }
+    __syncthreads();
+    run = carry[threadIdx.x];
+    for (int32_t i = lo; i < hi; i++) {
+      const ulonglong2 v = s16[i];
+      ulonglong2 o;
+      o.x = xor_prefix64(v.x, w) ^ run;
+      run = xor_last_word64(o.x, w);
+      o.y = xor_prefix64(v.y, w) ^ run;
+      run = xor_last_word64(o.y, w);
+      reinterpret_cast<ulonglong2*>(d)[i] = o;
+    }
+    __syncthreads();
+    return;
+  }
   const int32_t nw = bsize / w;
   const int32_t per = (nw + blockDim.x - 1) / blockDim.x;
   const int32_t lo = min(nw, (int32_t)threadIdx.x * per), hi = min(nw, lo + per);
-  auto ldw = [&](int32_t i) { uint64_t v = 0; for (int k = 0; k < w; k++) v |= (uint64_t)d[(int64_t)i * w + k] << (8 * k); return v; };
+  auto ldw = [&](int32_t i) { uint64_t v = 0; for (int k = 0; k < w; k++) v |= (uint64_t)s[(int64_t)i * w + k] << (8 * k); return v; };
   auto stw = [&](int32_t i, uint64_t v) { for (int k = 0; k < w; k++) d[(int64_t)i * w + k] = (uint8_t)(v >> (8 * k)); };
   uint64_t acc = 0;
   for (int32_t i = lo; i < hi; i++) acc ^= ldw(i);
   carry[threadIdx.x] = acc;
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint64_t run = 0;
-    for (int t = 0; t < (int)blockDim.x; t++) { uint64_t v = carry[t]; carry[t] = run; run ^= v; }
+    uint64_t r = 0;
+    for (int t = 0; t < (int)blockDim.x; t++) { uint64_t v = carry[t]; carry[t] = r; r ^= v; }
   }
   __syncthreads();
-  uint64_t run = carry[threadIdx.x];
-  for (int32_t i = lo; i < hi; i++) { run ^= ldw(i); stw(i, run); }
+  uint64_t r = carry[threadIdx.x];
+  for (int32_t i = lo; i < hi; i++) { r ^= ldw(i); stw(i, r); }
+  for (int32_t i = nb + threadIdx.x; i < bsize; i += blockDim.x) d[i] = s[i];
   __syncthreads();
 }
 
