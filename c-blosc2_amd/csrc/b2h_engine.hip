@@ -782,6 +782,7 @@ struct DTotals {
   int64_t stage_bytes;
   int32_t nblocks, nstreams;
   int32_t any_delta, max_filters;
+  int32_t slot_mask;   // filter slots with a backward filter in any chunk (bit i = slot i)
 };
 
 // Single-workgroup exclusive scans (block_base, stream_base, stage_off) + totals.
@@ -797,7 +798,9 @@ __global__ __launch_bounds__(1024) void k_dscan(DChunk* __restrict__ ch, int32_t
     a += ch[i].nstreams ? ch[i].nbytes : 0;
     bk += ch[i].nblocks;
     st += ch[i].nstreams;
-    dl |= ch[i].has_delta;
+    dl |= ch[i].has_delta ? 0x100 : 0;
+    for (int f = 0; f < 6; f++)
+      if (ch[i].filters[f] != kNoFilter && ch[i].filters[f] != kTruncPrec) dl |= 1 << f;
     mf = max(mf, (int32_t)ch[i].nfilters_bwd);
   }
   sb[threadIdx.x] = a; sbk[threadIdx.x] = bk; sst[threadIdx.x] = st; sdl[threadIdx.x] = dl; smf[threadIdx.x] = mf;
@@ -810,7 +813,7 @@ __global__ __launch_bounds__(1024) void k_dscan(DChunk* __restrict__ ch, int32_t
       sb[t] = ra; sbk[t] = rb; sst[t] = rs;
       ra += va; rb += vb; rs += vs; rd |= sdl[t]; rm = max(rm, smf[t]);
     }
-    tot->stage_bytes = ra; tot->nblocks = rb; tot->nstreams = rs; tot->any_delta = rd; tot->max_filters = rm;
+    tot->stage_bytes = ra; tot->nblocks = rb; tot->nstreams = rs; tot->any_delta = (rd >> 8) & 1; tot->slot_mask = rd & 0x3f; tot->max_filters = rm;
   }
   __syncthreads();
   int64_t ra = sb[threadIdx.x];
@@ -891,8 +894,12 @@ __global__ void k_dplan_blocks(const uint8_t* const* __restrict__ srcs, const in
 // allows), streams pulled from a device counter -- stream cost ranges from a 64 KiB memset to
 // thousands of LZ tokens, and a blockIdx-based mapping parks the expensive byte planes on a
 // fraction of the chip (workgroups are dealt to XCDs / shader engines by index).
-constexpr int kRingLog = 15;   // 32 KiB LDS output ring per wave: 5 waves per CU
+// LDS output ring per wave: 2^RLOG bytes.  The ring is the decoder's only LDS, so it sets the
+// waves per CU (32 KiB: 5, 16 KiB: 10, 8 KiB: 20 = the 96-VGPR limit).  B2H_DEC_RING = 12..15
+// picks it; default 13 (T decode: 15 -> 10.2 ms, 14 -> 6.3 ms, 13 -> 5.6 ms: the token loop is
+// latency-bound, and more resident waves beat keeping older match sources in LDS).
 
+template <int RLOG>
 __device__ __forceinline__ void decode_stream(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
                                               DChunk* __restrict__ ch, const DStream& st, uint8_t* __restrict__ stage,
                                               const uint8_t* __restrict__ maskout, B2H_LDS uint8_t* ring,
@@ -921,13 +928,14 @@ __device__ __forceinline__ void decode_stream(const uint8_t* const* __restrict__
   } else if ((d.flags >> 5) != 0) {
     if (lane == 0) atomicMin(&ch[c].status, E_CODEC);
   } else {
-    const int32_t got = wave_lz_decode_par<kRingLog>(in, st.csize, out, nb, ring);
+    const int32_t got = wave_lz_decode_par<RLOG>(in, st.csize, out, nb, ring);
     if (got != nb && lane == 0) atomicMin(&ch[c].status, E_DATA);
     *kind_out = 3;
   }
 }
 
-__global__ __launch_bounds__(64) void k_decode(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
+template <int RLOG>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RLOG == 12 ? 8 : 1, 8))) void k_decode(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
                                                DChunk* __restrict__ ch, const DStream* __restrict__ streams,
                                                uint8_t* __restrict__ stage, int32_t nstreams_total,
                                                const uint8_t* __restrict__ maskout, int32_t* __restrict__ next,
@@ -940,7 +948,7 @@ __global__ __launch_bounds__(64) void k_decode(const uint8_t* const* __restrict_
     if (s >= nstreams_total) return;
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     int32_t kind = 0;
-    decode_stream(srcs, dsts, ch, streams[s], stage, maskout, ring, &kind);
+    decode_stream<RLOG>(srcs, dsts, ch, streams[s], stage, maskout, ring, &kind);
     if (dbg && lane_id() == 0) {
       dbg[2 * s] = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
       dbg[2 * s + 1] = kind;
@@ -1012,6 +1020,25 @@ __global__ void k_dstatus(const DChunk* __restrict__ ch, int32_t* __restrict__ s
   if (c < n) status[c] = ch[c].status;
 }
 
+static int dec_ring_log() {
+  static int v = 0;
+  if (!v) {
+    const char* e = getenv("B2H_DEC_RING");
+    v = e ? std::max(12, std::min(15, atoi(e))) : 13;
+  }
+  return v;
+}
+
+template <int RLOG>
+static void launch_decode(const uint8_t* const* d_src, uint8_t* const* d_dst, DChunk* ch, const DStream* streams,
+                          uint8_t* stage, int32_t nstreams, const uint8_t* d_maskout, int32_t* next, int64_t* dbg,
+                          hipStream_t st) {
+  const size_t lds = size_t(1) << RLOG;
+  const int slots = resident_slots(reinterpret_cast<const void*>(&k_decode<RLOG>), lds);
+  const uint32_t grid = (uint32_t)std::min<int64_t>(nstreams, slots);
+  k_decode<RLOG><<<grid, 64, lds, st>>>(d_src, d_dst, ch, streams, stage, nstreams, d_maskout, next, dbg);
+}
+
 int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint8_t* const* d_dst,
                      const int32_t* d_dstsize, int32_t n, int64_t dst_bound, int32_t* d_status,
                      const uint8_t* d_maskout, hipStream_t st) {
@@ -1043,16 +1070,16 @@ int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint
     ev_decode.start(st);
     HIPCHK(hipMemsetAsync(next, 0, sizeof(int32_t), st));
     {
-      const size_t lds = size_t(1) << kRingLog;
-      const int slots = resident_slots(reinterpret_cast<const void*>(&k_decode), lds);
-      const uint32_t grid = (uint32_t)std::min<int64_t>(h.nstreams, slots);
       int64_t* dbg = nullptr;
       if (g_ddebug) {
         if (ws->ddbg.ensure(sizeof(int64_t) * 2 * (size_t)h.nstreams)) return E_MEMORY;
         dbg = ws->ddbg.as<int64_t>();
       }
-      k_decode<<<grid, 64, lds, st>>>(d_src, d_dst, ch, streams, ws->stage.as<uint8_t>(), h.nstreams, d_maskout,
-                                      next, dbg);
+      const int rlog = dec_ring_log();
+      if (rlog == 12) launch_decode<12>(d_src, d_dst, ch, streams, ws->stage.as<uint8_t>(), h.nstreams, d_maskout, next, dbg, st);
+      else if (rlog == 13) launch_decode<13>(d_src, d_dst, ch, streams, ws->stage.as<uint8_t>(), h.nstreams, d_maskout, next, dbg, st);
+      else if (rlog == 14) launch_decode<14>(d_src, d_dst, ch, streams, ws->stage.as<uint8_t>(), h.nstreams, d_maskout, next, dbg, st);
+      else launch_decode<15>(d_src, d_dst, ch, streams, ws->stage.as<uint8_t>(), h.nstreams, d_maskout, next, dbg, st);
     }
     ev_decode.stop(st);
     ev_unfilter.start(st);
@@ -1061,7 +1088,8 @@ int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint
       for (int ps = 0; ps < passes; ps++) {
         const int pass = h.any_delta ? ps + 1 : 0;
         for (int slot = 5; slot >= 0; slot--)
-          k_dfilter<<<h.nblocks, kBlockThreads, 0, st>>>(ch, blocks, d_dst, ws->stage.as<uint8_t>(),
+          if ((h.slot_mask >> slot) & 1)
+            k_dfilter<<<h.nblocks, kBlockThreads, 0, st>>>(ch, blocks, d_dst, ws->stage.as<uint8_t>(),
                                                          ws->stage2.as<uint8_t>(), slot, pass, h.nblocks, d_maskout);
       }
     }

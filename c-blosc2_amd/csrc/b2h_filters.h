@@ -18,63 +18,104 @@ constexpr int kBlockThreads = 256;
 __device__ __forceinline__ uint32_t byte_of(uint32_t w, int k) { return (w >> (8 * k)) & 0xffu; }
 
 // ------------------------------------------------------------------------------- shuffle ----
-// Fast path: TS in {2,4,8,16}, n % 4 == 0, 16-byte aligned src/dst.  Thread t owns elements
-// [4t, 4t+4): it reads 4*TS contiguous bytes and writes one u32 into each of the TS planes.
+// Fast path: TS in {2,4,8,16}, n % 4 == 0, 16-byte aligned src/dst.  A thread owns quads
+// (4 elements = 4*TS contiguous bytes) q, q + T, q + 2T, q + 3T (T = threads): every load and
+// store instruction stays coalesced across the wave, and the four quads' loads are issued before
+// the first store, so 4x the bytes are in flight per lane (HBM latency x bandwidth wants
+// ~64 KiB in flight per CU).  Quad q writes one u32 into each of the TS planes.
 // `n` elements from `src`; plane p of `dst` starts at dst + p * pstride (pstride = n for a block).
+constexpr int kQuadUnroll = 4;
+
+template <int TS>
+__device__ __forceinline__ void load_quad(const uint8_t* __restrict__ src, int32_t q, uint32_t (&w)[TS]) {
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + (int64_t)q * 4 * TS);
+  if constexpr (TS % 4 == 0) {
+#pragma unroll
+    for (int k = 0; k < TS / 4; k++) {
+      uint4 v = reinterpret_cast<const uint4*>(s32)[k];
+      w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+    }
+  } else {  // TS == 2
+    uint2 v = *reinterpret_cast<const uint2*>(s32);
+    w[0] = v.x; w[1] = v.y;
+  }
+}
+
+template <int TS>
+__device__ __forceinline__ void store_planes(uint8_t* __restrict__ dst, int32_t q, int64_t pstride, const uint32_t (&w)[TS]) {
+#pragma unroll
+  for (int plane = 0; plane < TS; plane++) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int byte = e * TS + plane;     // byte index inside the 4*TS bytes
+      o |= byte_of(w[byte / 4], byte % 4) << (8 * e);
+    }
+    reinterpret_cast<uint32_t*>(dst + (int64_t)plane * pstride)[q] = o;
+  }
+}
+
 template <int TS>
 __device__ void shuffle_fast(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t n, int64_t pstride) {
-  const int32_t quads = n / 4;
-  for (int32_t q = threadIdx.x; q < quads; q += blockDim.x) {
-    uint32_t w[TS];   // 4*TS bytes = elements 4q..4q+3
-    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + (int64_t)q * 4 * TS);
-    if constexpr (TS % 4 == 0) {
+  const int32_t quads = n / 4, T = blockDim.x;
+  int32_t q = threadIdx.x;
+  for (; q + (kQuadUnroll - 1) * T < quads; q += kQuadUnroll * T) {
+    uint32_t w[kQuadUnroll][TS];
 #pragma unroll
-      for (int k = 0; k < TS / 4; k++) {
-        uint4 v = reinterpret_cast<const uint4*>(s32)[k];
-        w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
-      }
-    } else {  // TS == 2
-      uint2 v = *reinterpret_cast<const uint2*>(s32);
-      w[0] = v.x; w[1] = v.y;
+    for (int u = 0; u < kQuadUnroll; u++) load_quad<TS>(src, q + u * T, w[u]);
+#pragma unroll
+    for (int u = 0; u < kQuadUnroll; u++) store_planes<TS>(dst, q + u * T, pstride, w[u]);
+  }
+  for (; q < quads; q += T) {
+    uint32_t w[TS];
+    load_quad<TS>(src, q, w);
+    store_planes<TS>(dst, q, pstride, w);
+  }
+}
+
+template <int TS>
+__device__ __forceinline__ void load_planes(const uint8_t* __restrict__ src, int32_t q, int64_t pstride, uint32_t (&p)[TS]) {
+#pragma unroll
+  for (int plane = 0; plane < TS; plane++) p[plane] = reinterpret_cast<const uint32_t*>(src + (int64_t)plane * pstride)[q];
+}
+
+template <int TS>
+__device__ __forceinline__ void store_quad(uint8_t* __restrict__ dst, int32_t q, const uint32_t (&p)[TS]) {
+  uint32_t w[TS];
+#pragma unroll
+  for (int k = 0; k < TS; k++) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const int byte = 4 * k + b;           // output byte inside the 4*TS bytes
+      o |= byte_of(p[byte % TS], byte / TS) << (8 * b);
     }
+    w[k] = o;
+  }
+  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + (int64_t)q * 4 * TS);
+  if constexpr (TS % 4 == 0) {
 #pragma unroll
-    for (int plane = 0; plane < TS; plane++) {
-      uint32_t o = 0;
-#pragma unroll
-      for (int e = 0; e < 4; e++) {
-        const int byte = e * TS + plane;     // byte index inside the 4*TS bytes
-        o |= byte_of(w[byte / 4], byte % 4) << (8 * e);
-      }
-      reinterpret_cast<uint32_t*>(dst + (int64_t)plane * pstride)[q] = o;
-    }
+    for (int k = 0; k < TS / 4; k++) reinterpret_cast<uint4*>(d32)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+  } else {
+    *reinterpret_cast<uint2*>(d32) = make_uint2(w[0], w[1]);
   }
 }
 
 template <int TS>
 __device__ void unshuffle_fast(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t n, int64_t pstride) {
-  const int32_t quads = n / 4;
-  for (int32_t q = threadIdx.x; q < quads; q += blockDim.x) {
+  const int32_t quads = n / 4, T = blockDim.x;
+  int32_t q = threadIdx.x;
+  for (; q + (kQuadUnroll - 1) * T < quads; q += kQuadUnroll * T) {
+    uint32_t p[kQuadUnroll][TS];
+#pragma unroll
+    for (int u = 0; u < kQuadUnroll; u++) load_planes<TS>(src, q + u * T, pstride, p[u]);
+#pragma unroll
+    for (int u = 0; u < kQuadUnroll; u++) store_quad<TS>(dst, q + u * T, p[u]);
+  }
+  for (; q < quads; q += T) {
     uint32_t p[TS];
-#pragma unroll
-    for (int plane = 0; plane < TS; plane++) p[plane] = reinterpret_cast<const uint32_t*>(src + (int64_t)plane * pstride)[q];
-    uint32_t w[TS];
-#pragma unroll
-    for (int k = 0; k < TS; k++) {
-      uint32_t o = 0;
-#pragma unroll
-      for (int b = 0; b < 4; b++) {
-        const int byte = 4 * k + b;           // output byte inside the 4*TS bytes
-        o |= byte_of(p[byte % TS], byte / TS) << (8 * b);
-      }
-      w[k] = o;
-    }
-    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + (int64_t)q * 4 * TS);
-    if constexpr (TS % 4 == 0) {
-#pragma unroll
-      for (int k = 0; k < TS / 4; k++) reinterpret_cast<uint4*>(d32)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
-    } else {
-      *reinterpret_cast<uint2*>(d32) = make_uint2(w[0], w[1]);
-    }
+    load_planes<TS>(src, q, pstride, p);
+    store_quad<TS>(dst, q, p);
   }
 }
 

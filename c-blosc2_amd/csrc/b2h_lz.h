@@ -330,6 +330,35 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
     const uint64_t am = __ballot(accept);
     EPROF_T(t3);
 
+    if (PROBE && am == 0) {
+      // ---- all-literal probe window (no match below W): the counting below in closed form ----
+      // literal k of the window lands at o + k + (lit + k) / 32 (a run marker after every 32nd)
+      if (!PROBE) {
+        const int32_t last = o + (W - 1) + (lit + W - 1) / 32;
+        peak = max(peak, last + 2);
+        if (last + 2 > maxout) { fail = true; break; }
+        if (lane < W) {
+          const int32_t off = o + lane + (lit + lane) / 32;
+          oring[off & ORM] = (uint8_t)(v & 0xffu);
+          if (((lit + lane + 1) & 31) == 0) oring[(off + 1) & ORM] = (uint8_t)(kLzMaxCopy - 1);
+        }
+      }
+      o += W + (lit + W) / 32;
+      lit = (lit + W) & 31;
+      {  // every lane below W is a visited literal (same run rule as the general insert below)
+        const uint64_t visit = W >= 64 ? ~0ull : ((1ull << W) - 1ull);
+        const uint64_t above = ~0ull << lane << 1;
+        const uint64_t brk = ~s1mask & above;
+        const uint64_t run = brk ? (above & ((1ull << __builtin_ctzll(brk)) - 1)) : above;
+        if (((visit >> lane) & 1ull) && !(visit & run)) htab.put(h, (uint32_t)p);
+      }
+      EPROF_ADD(0, t0, t1);
+      EPROF_ADD(1, t1, t2);
+      EPROF_ADD(2, t2, t3);
+      pos = P + W;
+      continue;
+    }
+
     // ---- chain walk: the matches the serial loop takes in this window ----
     uint64_t chain = 0;
     int32_t E = W;        // the window consumes positions P .. P+E-1 (E > 64 after a long match)
@@ -760,13 +789,19 @@ __device__ __forceinline__ void ring_flush(const B2H_LDS uint8_t* ring, gout_t o
 }
 
 
+// The decoder's LDS ring leaves for global memory in pieces of ring_piece bytes, from the flush
+// frontier F (a multiple of the piece) up to at most the current output position: a copy of n
+// bytes at op may flush only while op + n - F > R, so R >= n + piece keeps every flushed byte final
+// (copies go in steps of <= 1024, literal runs are <= 32).
+__host__ __device__ constexpr int32_t ring_piece(int rlog) { return (1 << rlog) / 4 < 4096 ? (1 << rlog) / 4 : 4096; }
+
 // Slow paths of the decoder, kept out of line on purpose: inlined, their loops and the flushes
 // made the token loop irreducible (the backend then wraps every token in a guard-variable
 // state machine, ~4x the instructions).  Called for copies longer than 64 bytes, sources older
 // than the ring, and ring flushes.  Returns the new flush frontier F.
 template <int RLOG>
 __device__ __noinline__ int32_t copy_general(B2H_LDS uint8_t* ring, gout_t out, int32_t op, int32_t src, int32_t len, int32_t dist, int32_t F) {
-  constexpr int32_t R = 1 << RLOG, RM = R - 1, PIECE = 4096, STEP = 1024;
+  constexpr int32_t R = 1 << RLOG, RM = R - 1, PIECE = ring_piece(RLOG), STEP = 1024;
   const int lane = lane_id();
   const bool overlap = dist < len;
   const int32_t step = overlap ? 64 % dist : 0;
@@ -784,10 +819,25 @@ __device__ __noinline__ int32_t copy_general(B2H_LDS uint8_t* ring, gout_t out, 
   }
   return F;
 }
+// Ring-resident match of up to 256 bytes whose source ends before it starts (dist >= len):
+// every source byte is final, so the four 64-byte slices' LDS reads are all issued before the
+// first write.  Matches over 64 bytes are ~8 % of a float32 mantissa plane's tokens; through
+// copy_general each cost a call and a dependent read->write per slice.
+template <int RLOG>
+__device__ __forceinline__ void ring_copy256(B2H_LDS uint8_t* ring, int32_t op, int32_t src, int32_t len) {
+  constexpr int32_t RM = (1 << RLOG) - 1;
+  const int lane = lane_id();
+  uint8_t b[4];
+#pragma unroll
+  for (int u = 0; u < 4; u++) b[u] = lane + 64 * u < len ? ring[(src + lane + 64 * u) & RM] : (uint8_t)0;
+#pragma unroll
+  for (int u = 0; u < 4; u++)
+    if (lane + 64 * u < len) ring[(op + lane + 64 * u) & RM] = b[u];
+}
 // Flush 4 KiB pieces until end - F <= ring size.
 template <int RLOG>
 __device__ __noinline__ int32_t flush_to(B2H_LDS uint8_t* ring, gout_t out, int32_t end, int32_t F) {
-  constexpr int32_t R = 1 << RLOG, PIECE = 4096;
+  constexpr int32_t R = 1 << RLOG, PIECE = ring_piece(RLOG);
   while (end - F > R) { ring_flush<RLOG>(ring, out, F, F + PIECE); F += PIECE; }
   return F;
 }
@@ -918,7 +968,9 @@ __device__ uint64_t g_dec_prof[8];
 template <int RLOG>
 __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, gout_t out, int32_t maxout,
                                                       B2H_LDS uint8_t* ring) {
-  constexpr int32_t R = 1 << RLOG, RM = R - 1, WMAX = 8192;
+  // a batch's output must fit the ring next to the unflushed tail (F moves in whole pieces and
+  // never past op): WMAX + PIECE <= R
+  constexpr int32_t R = 1 << RLOG, RM = R - 1, WMAX = R - ring_piece(RLOG) < 8192 ? R - ring_piece(RLOG) : 8192;
   const int lane = lane_id();
   if (length == 0) return 0;
   InWin W;
@@ -1008,6 +1060,8 @@ __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, 
         if (lj <= 64 && src >= F) {
           const int32_t yl = dj < lj ? lane % dj : lane;
           if (lane < lj) ring[(oj + lane) & RM] = ring[(src + yl) & RM];
+        } else if (lj <= 256 && dj >= lj && src >= F) {
+          ring_copy256<RLOG>(ring, oj, src, lj);
         } else {
           F = copy_general<RLOG>(ring, out, oj, src, lj, dj, F);
         }
@@ -1069,6 +1123,8 @@ __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, 
         if (len <= 64 && src >= F && op + len - F <= R) {
           const int32_t yl = dd < len ? lane % dd : lane;
           if (lane < len) ring[(op + lane) & RM] = ring[(src + yl) & RM];
+        } else if (len <= 256 && dd >= len && src >= F && op + len - F <= R) {
+          ring_copy256<RLOG>(ring, op, src, len);
         } else {
           F = copy_general<RLOG>(ring, out, op, src, len, dd, F);
         }

@@ -303,3 +303,32 @@ def test_corrupted_streams_match_oracle(B, seed):
             assert isinstance(g, np.ndarray) and np.array_equal(g, o)
         else:
             assert not isinstance(g, np.ndarray) and g < 0
+
+
+def _long_match_data(n, seed):
+    """A random 4 KiB segment repeated with one byte changed every ~190 bytes: streams of
+    (literal, ~190-byte match) token pairs, so one 64-token decode batch outputs several KiB --
+    more than half of the decoder's 8 KiB LDS ring."""
+    rng = np.random.default_rng(seed)
+    base = rng.integers(0, 256, 4096, dtype=np.uint8)
+    parts = [base]
+    while sum(p.nbytes for p in parts) < n:
+        seg = base.copy()
+        for pos in range(int(rng.integers(0, 60)), seg.nbytes, 190):
+            seg[pos] ^= np.uint8(1 + int(rng.integers(0, 255)))
+        parts.append(seg)
+    return np.concatenate(parts)[:n]
+
+
+@pytest.mark.parametrize("bs", [65536, 262144])
+def test_long_match_batches(B, bs):
+    """Decode batches whose output approaches the ring capacity (flush frontier bookkeeping):
+    compress == oracle, decompress round-trips and equals the oracle's decode."""
+    src = _long_match_data(2 * bs + 777, bs)
+    kw = dict(clevel=5, typesize=1, filters=(0, 0, 0, 0, 0, 0), blocksize=bs)
+    want = oracle_compress(src, **kw)
+    got = B.compress(src, **kw)
+    assert isinstance(got, np.ndarray) and np.array_equal(got, want)
+    assert want.nbytes < 0.2 * src.nbytes        # long matches were taken
+    dec = B.decompress(got, src.nbytes)
+    assert isinstance(dec, np.ndarray) and np.array_equal(dec, src)
