@@ -233,6 +233,7 @@ __device__ __forceinline__ void encode_loop(const CGeom& g, TAB htab, B2H_LDS ui
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide time base
     StreamResult r = encode_stream<TAB>(in, len, g.clevel, out, htab, dbits, oring, g.overhead == kHdrExt);
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
+    if (TAB::kGlobal) r.windows |= 1 << 30;   // diagnostics: the stream ran on a global-table wave
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
     if (lane_id() == 0) res[s] = r;
   }

@@ -141,6 +141,7 @@ __device__ __forceinline__ int32_t wave_scan_max(int32_t v) {   // values >= -1
 template <typename POS>
 struct LdsTab {
   typedef POS pos_t;
+  static constexpr bool kGlobal = false;
   volatile B2H_LDS POS* t;
   __device__ __forceinline__ uint32_t get(uint32_t h) const { return t[h]; }
   __device__ __forceinline__ void put(uint32_t h, uint32_t v) const { t[h] = (POS)v; }
@@ -153,6 +154,7 @@ struct LdsTab {
 template <typename POS>
 struct GlbTab {
   typedef POS pos_t;
+  static constexpr bool kGlobal = true;
   B2H_GLB POS* t;
   __device__ __forceinline__ uint32_t get(uint32_t h) const {
     return __hip_atomic_load(t + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

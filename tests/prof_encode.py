@@ -26,6 +26,14 @@ rec = np.zeros(ns, dtype=[("kind", "i4"), ("size", "i4"), ("peak", "i4"), ("wind
 L.b2h_debug_stream_results.argtypes = [C.c_void_p, C.c_int32]
 assert L.b2h_debug_stream_results(rec.ctypes.data, ns) == ns
 plane = np.arange(ns) % 4
+glb = (rec["windows"] >> 30) & 1
+rec["windows"] &= (1 << 30) - 1
+for p in range(4):
+    for t, name in ((0, "lds"), (1, "glb")):
+        r = rec[(plane == p) & (glb == t)]
+        if r.size:
+            print(f"  plane {p} {name}: streams {r.size} cycles mean {r['cycles'].mean():.0f} "
+                  f"cyc/window {r['cycles'].sum() / max(1, r['windows'].sum()):.0f}")
 for p in range(4):
     r = rec[plane == p]
     print(f"plane {p}: kinds {np.bincount(r['kind'], minlength=4).tolist()} size mean {r['size'].mean():.0f} "
