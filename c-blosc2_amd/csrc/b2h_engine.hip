@@ -198,6 +198,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_ffilter(CGeom g, int pass, ui
     case kBitshuffle: block_bitshuffle(s, d, bsize, g.ts); break;
     case kDelta: block_delta_encode(s, dref + (int64_t)c * dref_stride, d, bsize, g.ts, b == 0); break;
     case kTruncPrec: block_trunc(s, d, bsize, g.ts, zeroed); break;
+    case kBytedelta: block_bytedelta_encode(s, d, bsize, meta); break;   // meta: channels (host-resolved)
+    case kIntTrunc: block_int_trunc(s, d, bsize, g.ts, zeroed); break;
     default: break;
   }
 }
@@ -497,6 +499,17 @@ int make_compress_plan(CompressPlan* p, int32_t nbytes, int32_t destsize, int cl
   return 0;
 }
 
+// int_trunc's precision check (plugins/filters/int_trunc/int_trunc.c:18-83): uint8 arithmetic on
+// the zeroed bit count, element sizes 1/2/4/8 only.
+static bool hostside_int_trunc_ok(int8_t prec, int32_t ts, int* zeroed) {
+  if (ts != 1 && ts != 2 && ts != 4 && ts != 8) return false;
+  const uint8_t bits = (uint8_t)(8 * ts);
+  const uint8_t z = prec >= 0 ? (uint8_t)(bits - prec) : (uint8_t)(-prec);
+  if (z >= bits) return false;
+  *zeroed = z;
+  return true;
+}
+
 static bool hostside_trunc_ok(int8_t prec, int32_t ts, int* zeroed) {
   const int mant = ts == 4 ? 23 : (ts == 8 ? 52 : -1);
   if (mant < 0) return false;
@@ -603,7 +616,10 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
   for (int i = 0; i < 6; i++) if (P.filters[i] != kNoFilter) act[nact++] = i;
   for (int k = 0; k < nact; k++) {
     const uint8_t f = P.filters[act[k]];
-    if (f > kTruncPrec) { snprintf(g_err, sizeof g_err, "filter %d is not a built-in filter", f); return E_FILTER; }
+    if (f > kTruncPrec && f != kBytedelta && f != kIntTrunc) {
+      snprintf(g_err, sizeof g_err, "filter %d is neither built in nor a device plugin filter", f);
+      return E_FILTER;
+    }
   }
   const size_t wbytes = (size_t)g.wstride * nchunks;
   int rc = 0;
@@ -643,10 +659,14 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
       const uint8_t f = P.filters[act[k]], meta = P.filters_meta[act[k]];
       int zeroed = 0;
       if (f == kTruncPrec && !hostside_trunc_ok((int8_t)meta, g.ts, &zeroed)) return E_FILTER;
+      if (f == kIntTrunc && !hostside_int_trunc_ok((int8_t)meta, P.typesize, &zeroed)) return E_FILTER;
+      // bytedelta's channel count is its meta; 0 means the super-chunk's typesize (bytedelta.c:90-98),
+      // which a caller without a super-chunk resolves before this point -- the chunk's own here
+      const uint8_t kmeta = (f == kBytedelta && meta == 0) ? (uint8_t)g.ts : meta;
       uint8_t* outb = ring[k % 3];
       const int64_t out_stride = (k % 3 == 2) ? g.wstride : g.wstride;
       dim3 grid(pass == 1 ? 1 : (pass == 2 ? g.nblocks - 1 : g.nblocks), nchunks);
-      k_ffilter<<<grid, kBlockThreads, 0, st>>>(g, pass, f, meta, cur, cur_stride, outb, out_stride, raw, raw_stride, zeroed);
+      k_ffilter<<<grid, kBlockThreads, 0, st>>>(g, pass, f, kmeta, cur, cur_stride, outb, out_stride, raw, raw_stride, zeroed);
       cur = outb;
       cur_stride = out_stride;
     }
@@ -707,6 +727,10 @@ __device__ __forceinline__ int32_t rd32(const uint8_t* p) {
   return (int32_t)((uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24));
 }
 
+// Filters with nothing to undo: TRUNC_PREC (blosc/blosc2.c:1531-1533) and int_trunc, whose
+// backward is a plain copy (plugins/filters/int_trunc/int_trunc.c:116-125).
+__host__ __device__ __forceinline__ bool bwd_noop(uint8_t f) { return f == kNoFilter || f == kTruncPrec || f == kIntTrunc; }
+
 // read_chunk_header + initialize_context_decompression (blosc/blosc2.c:738-852, 2688-2909)
 __global__ void k_dplan_chunks(const uint8_t* const* __restrict__ srcs, const int32_t* __restrict__ srcsize,
                                const int32_t* __restrict__ dstsize, DChunk* __restrict__ ch, int32_t n) {
@@ -765,11 +789,11 @@ __global__ void k_dplan_chunks(const uint8_t* const* __restrict__ srcs, const in
   d.nstreams = (d.nblocks - (d.leftover ? 1 : 0)) * spb + (d.leftover ? 1 : 0);
   // backward pipeline: active filters (not NOFILTER / TRUNC_PREC), applied high slot -> low
   int k = 0, K = 0;
-  for (int i = 5; i >= 0; i--) if (d.filters[i] != kNoFilter && d.filters[i] != kTruncPrec) K++;
+  for (int i = 5; i >= 0; i--) if (!bwd_noop(d.filters[i])) K++;
   for (int i = 5; i >= 0; i--) {
     const uint8_t f = d.filters[i];
-    if (f == kNoFilter || f == kTruncPrec) continue;
-    if (f > kTruncPrec) return fail(E_FILTER);   // user filters: host path only
+    if (bwd_noop(f)) continue;
+    if (f > kTruncPrec && f != kBytedelta) return fail(E_FILTER);   // other user filters: not on device
     d.has_delta |= f == kDelta;
     d.fsrc[i] = (k % 2 == 0) ? 0 : 1;
     d.fdst[i] = (k == K - 1) ? 2 : ((k % 2 == 0) ? 1 : 0);
@@ -801,7 +825,7 @@ __global__ __launch_bounds__(1024) void k_dscan(DChunk* __restrict__ ch, int32_t
     st += ch[i].nstreams;
     dl |= ch[i].has_delta ? 0x100 : 0;
     for (int f = 0; f < 6; f++)
-      if (ch[i].filters[f] != kNoFilter && ch[i].filters[f] != kTruncPrec) dl |= 1 << f;
+      if (!bwd_noop(ch[i].filters[f])) dl |= 1 << f;
     mf = max(mf, (int32_t)ch[i].nfilters_bwd);
   }
   sb[threadIdx.x] = a; sbk[threadIdx.x] = bk; sst[threadIdx.x] = st; sdl[threadIdx.x] = dl; smf[threadIdx.x] = mf;
@@ -970,7 +994,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_dfilter(DChunk* __restrict__ 
   const DChunk d = ch[bk.chunk];
   if (d.status < 0) return;
   const uint8_t f = d.filters[slot];
-  if (f == kNoFilter || f == kTruncPrec) return;
+  if (bwd_noop(f)) return;
   if (maskout && maskout[bk.block]) return;
   const bool lo = (bk.block == d.nblocks - 1) && d.leftover;
   const int32_t bsize = lo ? d.leftover : d.blocksize;
@@ -982,6 +1006,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_dfilter(DChunk* __restrict__ 
   switch (f) {
     case kShuffle: block_unshuffle(s, o, bsize, meta ? meta : d.typesize); break;
     case kBitshuffle: block_bitunshuffle(s, o, bsize, d.typesize, d.version); break;
+    case kBytedelta: block_bytedelta_decode(s, o, bsize, meta ? meta : d.typesize); break;
     case kDelta:
       if (bk.block == 0) block_delta_decode_first(s, o, bsize, d.typesize);
       else block_delta_decode_rest(s, dsts[bk.chunk], o, bsize, d.typesize);

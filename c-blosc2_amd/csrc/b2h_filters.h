@@ -457,4 +457,139 @@ __device__ void block_trunc(const uint8_t* __restrict__ src, uint8_t* __restrict
   }
 }
 
+// ---------------------------------------------------------------------- bytedelta (35) ----
+// plugins/filters/bytedelta/bytedelta.c:86-135 (forward) / 138-185 (backward).  The block is `ts`
+// channels of n = bsize / ts bytes (the planes a preceding SHUFFLE produced): forward stores every
+// byte minus its predecessor in the channel (the first minus 0), backward the running byte sum;
+// the trailing bsize % ts bytes pass through.  Bytes are handled four to a u32 with SWAR add/sub.
+__device__ __forceinline__ uint32_t swar_sub8(uint32_t a, uint32_t b) {
+  return ((a | 0x80808080u) - (b & 0x7f7f7f7fu)) ^ ((a ^ ~b) & 0x80808080u);
+}
+__device__ __forceinline__ uint32_t swar_add8(uint32_t a, uint32_t b) {
+  return ((a & 0x7f7f7f7fu) + (b & 0x7f7f7f7fu)) ^ ((a ^ b) & 0x80808080u);
+}
+// byte-wise inclusive prefix sum inside a u32 (little-endian byte order)
+__device__ __forceinline__ uint32_t swar_prefix8(uint32_t x) {
+  x = swar_add8(x, x << 8);
+  return swar_add8(x, x << 16);
+}
+
+// Exclusive workgroup scan of per-thread values (sums taken mod 2^32); *total = the sum of all.
+__device__ __forceinline__ uint32_t wg_excl_scan(uint32_t v, uint32_t* total) {
+  __shared__ uint32_t wsum[kBlockThreads / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+  for (int i = 0; i < nw; i++) {
+    const uint32_t t = wsum[i];
+    before += i < w ? t : 0u;
+    all += t;
+  }
+  __syncthreads();   // wsum is reused by the next call
+  *total = all;
+  return before + x - v;
+}
+
+__device__ void block_bytedelta_encode(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t bsize, int32_t ts) {
+  const int32_t n = bsize / ts;
+  const bool fast = (n % 16 == 0) && aligned16(src) && aligned16(dst);
+  for (int32_t ch = 0; ch < ts; ch++) {
+    const uint8_t* s = src + (int64_t)ch * n;
+    uint8_t* d = dst + (int64_t)ch * n;
+    if (fast) {
+      for (int32_t q = threadIdx.x; q < n / 16; q += blockDim.x) {
+        const uint4 v = reinterpret_cast<const uint4*>(s)[q];
+        const uint32_t prev = q ? (uint32_t)s[16 * (int64_t)q - 1] : 0u;
+        uint4 o;
+        o.x = swar_sub8(v.x, (v.x << 8) | prev);
+        o.y = swar_sub8(v.y, (v.y << 8) | (v.x >> 24));
+        o.z = swar_sub8(v.z, (v.z << 8) | (v.y >> 24));
+        o.w = swar_sub8(v.w, (v.w << 8) | (v.z >> 24));
+        reinterpret_cast<uint4*>(d)[q] = o;
+      }
+    } else {
+      for (int32_t i = threadIdx.x; i < n; i += blockDim.x) d[i] = (uint8_t)(s[i] - (i ? s[i - 1] : 0));
+    }
+  }
+  for (int32_t i = n * ts + threadIdx.x; i < bsize; i += blockDim.x) dst[i] = src[i];
+}
+
+__device__ void block_bytedelta_decode(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t bsize, int32_t ts) {
+  const int32_t n = bsize / ts;
+  const bool fast = (n % 16 == 0) && aligned16(src) && aligned16(dst);
+  const int32_t T = (int32_t)blockDim.x;
+  for (int32_t ch = 0; ch < ts; ch++) {
+    const uint8_t* s = src + (int64_t)ch * n;
+    uint8_t* d = dst + (int64_t)ch * n;
+    uint32_t carry = 0;   // channel sum of the bytes before this round
+    if (fast) {
+      // a round: thread t owns bytes [16 (base + t), +16)
+      for (int32_t base = 0; base < n / 16; base += T) {
+        const int32_t q = base + (int32_t)threadIdx.x;
+        uint4 v = q < n / 16 ? reinterpret_cast<const uint4*>(s)[q] : make_uint4(0u, 0u, 0u, 0u);
+        v.x = swar_prefix8(v.x);
+        v.y = swar_add8(swar_prefix8(v.y), (v.x >> 24) * 0x01010101u);
+        v.z = swar_add8(swar_prefix8(v.z), (v.y >> 24) * 0x01010101u);
+        v.w = swar_add8(swar_prefix8(v.w), (v.z >> 24) * 0x01010101u);
+        uint32_t all;
+        const uint32_t off = (carry + wg_excl_scan(v.w >> 24, &all)) & 0xffu;
+        const uint32_t ob = off * 0x01010101u;
+        v.x = swar_add8(v.x, ob); v.y = swar_add8(v.y, ob); v.z = swar_add8(v.z, ob); v.w = swar_add8(v.w, ob);
+        if (q < n / 16) reinterpret_cast<uint4*>(d)[q] = v;
+        carry = (carry + all) & 0xffu;
+      }
+    } else {
+      // contiguous segments per thread: local sums, one scan, then the running sums
+      const int32_t seg = (n + T - 1) / T;
+      const int32_t lo = min(n, (int32_t)threadIdx.x * seg), hi = min(n, lo + seg);
+      uint32_t local = 0;
+      for (int32_t i = lo; i < hi; i++) local += s[i];
+      uint32_t all;
+      uint32_t run = wg_excl_scan(local & 0xffu, &all);
+      for (int32_t i = lo; i < hi; i++) {
+        run += s[i];
+        d[i] = (uint8_t)run;
+      }
+    }
+  }
+  for (int32_t i = n * ts + threadIdx.x; i < bsize; i += blockDim.x) dst[i] = src[i];
+}
+
+// ---------------------------------------------------------------------- int_trunc (36) ----
+// plugins/filters/int_trunc/int_trunc.c:18-114: elements of ts in {1, 2, 4, 8} bytes keep their top
+// bits, x & ~((1 << zeroed) - 1).  The reference leaves the trailing bsize % ts bytes of its
+// scratch buffer unwritten; they are copied here.  Backward is the identity (a copy, 116-125).
+__device__ void block_int_trunc(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t bsize, int32_t ts, int zeroed) {
+  const uint64_t m64 = ~((1ull << zeroed) - 1ull);
+  // the element mask repeats every ts bytes: as u32 words it is m_lo (ts <= 4) or m_lo, m_hi (ts 8)
+  uint32_t mlo, mhi;
+  if (ts == 8) { mlo = (uint32_t)m64; mhi = (uint32_t)(m64 >> 32); }
+  else {
+    const uint32_t e = (uint32_t)m64 & (ts == 4 ? 0xffffffffu : ts == 2 ? 0xffffu : 0xffu);
+    mlo = ts == 4 ? e : ts == 2 ? (e | (e << 16)) : e * 0x01010101u;
+    mhi = mlo;
+  }
+  const int32_t body = bsize / ts * ts;
+  int32_t done = 0;
+  if (aligned16(src) && aligned16(dst)) {
+    const int32_t n16 = body / 16;
+    for (int32_t q = threadIdx.x; q < n16; q += blockDim.x) {
+      uint4 v = reinterpret_cast<const uint4*>(src)[q];
+      v.x &= mlo; v.y &= mhi; v.z &= mlo; v.w &= mhi;
+      reinterpret_cast<uint4*>(dst)[q] = v;
+    }
+    done = n16 * 16;
+  }
+  for (int32_t i = done + threadIdx.x; i < body; i += blockDim.x)
+    dst[i] = src[i] & (uint8_t)(m64 >> (8 * (i % ts)));
+  for (int32_t i = body + threadIdx.x; i < bsize; i += blockDim.x) dst[i] = src[i];
+}
+
 }  // namespace b2h

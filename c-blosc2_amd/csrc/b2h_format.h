@@ -17,6 +17,9 @@ constexpr uint8_t kFlagShuffle = 0x1, kFlagMemcpy = 0x2, kFlagBitshuffle = 0x4, 
                   kFlagDontSplit = 0x10;
 // filter ids (include/blosc2.h:248-259)
 constexpr uint8_t kNoFilter = 0, kShuffle = 1, kBitshuffle = 2, kDelta = 3, kTruncPrec = 4;
+// Registered plugin filters (include/blosc2/filters-registry.h:27-28, registered at blosc2_init by
+// plugins/filters/filters-registry.c:43-57) that the device pipeline also runs.
+constexpr uint8_t kBytedelta = 35, kIntTrunc = 36;
 constexpr uint8_t kSpecialZero = 1, kSpecialNan = 2, kSpecialValue = 3, kSpecialUninit = 4;
 
 // BloscLZ constants (blosc/blosclz.c:45-47, 442-465)

@@ -176,8 +176,15 @@ int check_supported(const blosc2_context* c) {
     return BLOSC2_ERROR_CODEC_PARAM;
   }
   for (int i = 0; i < 6; i++) {
-    if (c->filters[i] > BLOSC_TRUNC_PREC) {
-      TRACE_ERROR("filter %d runs on host callbacks; not part of the device pipeline", c->filters[i]);
+    const uint8_t f = c->filters[i];
+    if (f > BLOSC_TRUNC_PREC && f != b2h::kBytedelta && f != b2h::kIntTrunc) {
+      TRACE_ERROR("filter %d runs on host callbacks; not part of the device pipeline", f);
+      return BLOSC2_ERROR_FILTER_PIPELINE;
+    }
+    // bytedelta with meta 0 takes the super-chunk's typesize and fails without one
+    // (plugins/filters/bytedelta/bytedelta.c:90-98 -> pipeline_forward returns NULL)
+    if (f == b2h::kBytedelta && c->filters_meta[i] == 0 && c->schunk == nullptr) {
+      TRACE_ERROR("When meta is 0, you need to be on a schunk!");
       return BLOSC2_ERROR_FILTER_PIPELINE;
     }
   }

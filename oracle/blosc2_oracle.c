@@ -19,6 +19,7 @@ enum {
   MIN_BUF = 32,                               /* BLOSC_MIN_BUFFERSIZE, include/blosc2.h:193 */
   F_SHUF = 1, F_MEMCPY = 2, F_BITSHUF = 4, F_DELTA = 8, /* include/blosc2.h:273-277 */
   FLT_NONE = 0, FLT_SHUFFLE = 1, FLT_BITSHUFFLE = 2, FLT_DELTA = 3, FLT_TRUNC = 4,
+  FLT_BYTEDELTA = 35, FLT_INT_TRUNC = 36,     /* include/blosc2/filters-registry.h:27-28 */
   SPLIT_ALWAYS = 1, SPLIT_NEVER = 2, SPLIT_AUTO = 3, SPLIT_FWD = 4,
   SPECIAL_ZERO = 1, SPECIAL_NAN = 2, SPECIAL_VALUE = 3, SPECIAL_UNINIT = 4,
   ERR_DATA = -3, ERR_READ = -5, ERR_WRITE = -6, ERR_PARAM = -12, ERR_CODEC = -7,
@@ -169,6 +170,48 @@ int or_trunc_prec(int8_t prec_bits, int32_t ts, int32_t nbytes, const uint8_t *s
   uint64_t mask = ~((1ULL << zeroed) - 1ULL);
   int32_t n = nbytes / ts;
   for (int32_t i = 0; i < n; i++) stw(dst + (int64_t)i * ts, ldw(src + (int64_t)i * ts, ts) & mask, ts);
+  return 0;
+}
+
+/* ------------------------------------------------------------ registered plugin filters ---- */
+/* plugins/filters/bytedelta/bytedelta.c:86-135: `channels` planes of nbytes / channels bytes, each
+ * byte minus its predecessor in the plane (the first minus 0); the tail is copied. */
+void or_bytedelta_encode(int32_t channels, int32_t nbytes, const uint8_t *src, uint8_t *dst) {
+  int32_t n = nbytes / channels;
+  for (int32_t c = 0; c < channels; c++)
+    for (int32_t i = 0; i < n; i++) {
+      int64_t k = (int64_t)c * n + i;
+      dst[k] = (uint8_t)(src[k] - (i ? src[k - 1] : 0));
+    }
+  memcpy(dst + (int64_t)n * channels, src + (int64_t)n * channels, (size_t)(nbytes - n * channels));
+}
+
+/* bytedelta.c:138-185: the running byte sum of every plane */
+void or_bytedelta_decode(int32_t channels, int32_t nbytes, const uint8_t *src, uint8_t *dst) {
+  int32_t n = nbytes / channels;
+  for (int32_t c = 0; c < channels; c++) {
+    uint8_t acc = 0;
+    for (int32_t i = 0; i < n; i++) {
+      int64_t k = (int64_t)c * n + i;
+      acc = (uint8_t)(acc + src[k]);
+      dst[k] = acc;
+    }
+  }
+  memcpy(dst + (int64_t)n * channels, src + (int64_t)n * channels, (size_t)(nbytes - n * channels));
+}
+
+/* plugins/filters/int_trunc/int_trunc.c:18-114: elements of 1/2/4/8 bytes keep their top bits; the
+ * zeroed-bit count is computed in uint8 arithmetic.  The reference leaves the trailing
+ * nbytes % ts bytes of its scratch buffer unwritten; this restatement copies them. */
+int or_int_trunc(int8_t prec_bits, int32_t ts, int32_t nbytes, const uint8_t *src, uint8_t *dst) {
+  if (ts != 1 && ts != 2 && ts != 4 && ts != 8) return -1;
+  uint8_t bits = (uint8_t)(8 * ts);
+  uint8_t zeroed = prec_bits >= 0 ? (uint8_t)(bits - prec_bits) : (uint8_t)(-prec_bits);
+  if (zeroed >= bits) return -1;
+  uint64_t mask = ~((1ULL << zeroed) - 1ULL);
+  int32_t n = nbytes / ts;
+  for (int32_t i = 0; i < n; i++) stw(dst + (int64_t)i * ts, ldw(src + (int64_t)i * ts, ts) & mask, ts);
+  memcpy(dst + (int64_t)n * ts, src + (int64_t)n * ts, (size_t)(nbytes - n * ts));
   return 0;
 }
 
@@ -474,6 +517,10 @@ static const uint8_t *pipe_forward(const or_cparams *cp, int32_t ts, uint8_t *ch
       case FLT_TRUNC:
         if (or_trunc_prec((int8_t)meta, ts, bsize, cur, dst) < 0) return NULL;
         break;
+      case FLT_BYTEDELTA: or_bytedelta_encode(meta ? meta : ts, bsize, cur, dst); break;
+      case FLT_INT_TRUNC:
+        if (or_int_trunc((int8_t)meta, cp->typesize, bsize, cur, dst) < 0) return NULL;
+        break;
       default: return NULL;
     }
     cur = dst;
@@ -663,12 +710,13 @@ static int pipe_backward(const or_hdr *h, uint8_t *out, int32_t offset, int32_t 
   int nb = 0;
   for (int i = 5; i >= 0; i--) {
     uint8_t f = h->filters[i];
-    if (f == FLT_NONE || f == FLT_TRUNC) continue;
+    if (f == FLT_NONE || f == FLT_TRUNC || f == FLT_INT_TRUNC) continue;   /* int_trunc.c:116-125 copies */
     uint8_t *dst = bufs[nb];
     uint8_t meta = h->filters_meta[i];
     switch (f) {
       case FLT_SHUFFLE: or_unshuffle(meta ? meta : ts, bsize, cur, dst); break;
       case FLT_BITSHUFFLE: or_bitunshuffle(ts, bsize, cur, dst, h->version); break;
+      case FLT_BYTEDELTA: or_bytedelta_decode(meta ? meta : ts, bsize, cur, dst); break;
       case FLT_DELTA:
         memcpy(dst, cur, (size_t)bsize);
         if (offset == 0) {
@@ -731,7 +779,8 @@ int or_decompress_chunk(const void *src_, int32_t srcsize, void *dest_, int32_t 
     int32_t neblock = bsize / nstreams;
     if (neblock == 0) { rc = ERR_WRITE; break; }
     int has_filters = 0;
-    for (int i = 0; i < 6; i++) has_filters |= h.filters[i] != FLT_NONE && h.filters[i] != FLT_TRUNC;
+    for (int i = 0; i < 6; i++)
+      has_filters |= h.filters[i] != FLT_NONE && h.filters[i] != FLT_TRUNC && h.filters[i] != FLT_INT_TRUNC;
     uint8_t *stage = has_filters ? t0 : dest + (int64_t)j * bs;
     for (int32_t s = 0; s < nstreams; s++) {
       if (avail < 4) { rc = ERR_READ; break; }

@@ -34,6 +34,9 @@ void or_delta_encode(const uint8_t *dref, int32_t offset, int32_t nbytes, int32_
 void or_delta_decode(const uint8_t *dref, int32_t offset, int32_t nbytes, int32_t typesize,
                      uint8_t *dst);
 /* Mantissa truncation (reference: blosc/trunc-prec.c:23-86).  Returns <0 on bad params. */
+void or_bytedelta_encode(int32_t channels, int32_t nbytes, const uint8_t *src, uint8_t *dst);
+void or_bytedelta_decode(int32_t channels, int32_t nbytes, const uint8_t *src, uint8_t *dst);
+int or_int_trunc(int8_t prec_bits, int32_t typesize, int32_t nbytes, const uint8_t *src, uint8_t *dst);
 int or_trunc_prec(int8_t prec_bits, int32_t typesize, int32_t nbytes, const uint8_t *src,
                   uint8_t *dst);
 /* BloscLZ codec (reference: blosc/blosclz.c:320-619 encoder, 685-795 decoder). */

@@ -31,6 +31,9 @@ def oracle():
         L.or_delta_encode.argtypes, L.or_delta_encode.restype = [vp, i32, i32, i32, vp, vp], None
         L.or_delta_decode.argtypes, L.or_delta_decode.restype = [vp, i32, i32, i32, vp], None
         L.or_trunc_prec.argtypes, L.or_trunc_prec.restype = [C.c_int8, i32, i32, vp, vp], C.c_int
+        L.or_int_trunc.argtypes, L.or_int_trunc.restype = [C.c_int8, i32, i32, vp, vp], C.c_int
+        L.or_bytedelta_encode.argtypes, L.or_bytedelta_encode.restype = [i32, i32, vp, vp], None
+        L.or_bytedelta_decode.argtypes, L.or_bytedelta_decode.restype = [i32, i32, vp, vp], None
         L.or_blosclz_compress.argtypes = [C.c_int, vp, C.c_int, vp, C.c_int]
         L.or_blosclz_decompress.argtypes = [vp, C.c_int, vp, C.c_int]
         L.or_compute_blocksize.argtypes, L.or_compute_blocksize.restype = [C.POINTER(OrCParams), i32], i32
@@ -40,12 +43,30 @@ def oracle():
     return _oracle
 
 
+class Filter(C.Structure):
+    """blosc2_filter (reference include/blosc2.h:2742-2753)."""
+    _fields_ = [("id", C.c_uint8), ("name", C.c_char_p), ("version", C.c_uint8),
+                ("forward", C.c_void_p), ("backward", C.c_void_p)]
+
+
+_keep = []
+
+
 def ref():
-    """The reference library, or None when it was not built (e.g. /root/reference absent)."""
+    """The reference library, or None when it was not built (e.g. /root/reference absent).  The
+    bytedelta (35) and int_trunc (36) plugin filters compiled into it are registered the way
+    plugins/filters/filters-registry.c:43-57 does at blosc2_init (HAVE_PLUGINS is off there)."""
     global _ref
     if _ref is None and os.path.exists(REF_SO):
-        _ref = bind(C.CDLL(REF_SO))
-        _ref.blosc2_init()
+        R = bind(C.CDLL(REF_SO))
+        R.blosc2_init()
+        R.register_filter_private.argtypes, R.register_filter_private.restype = [C.POINTER(Filter)], C.c_int
+        for fid, name, fw, bw in ((35, b"bytedelta", "bytedelta_forward", "bytedelta_backward"),
+                                  (36, b"int_trunc", "int_trunc_forward", "int_trunc_backward")):
+            f = Filter(fid, name, 1, C.cast(getattr(R, fw), C.c_void_p), C.cast(getattr(R, bw), C.c_void_p))
+            _keep.append(f)
+            assert R.register_filter_private(C.byref(f)) == 0
+        _ref = R
     return _ref
 
 

@@ -332,3 +332,32 @@ def test_long_match_batches(B, bs):
     assert want.nbytes < 0.2 * src.nbytes        # long matches were taken
     dec = B.decompress(got, src.nbytes)
     assert isinstance(dec, np.ndarray) and np.array_equal(dec, src)
+
+
+@pytest.mark.parametrize("clevel", [1, 5, 9])
+def test_plugin_filters_vs_oracle(B, clevel):
+    """bytedelta (35) / int_trunc (36) pipelines on the device: chunks byte-identical to the oracle
+    (itself pinned to the reference library in test_oracle.py), decode == the oracle's decode."""
+    from test_oracle import PLUGIN_PIPES, plugin_input
+    for case, pipe in enumerate(PLUGIN_PIPES):
+        kw = dict(pipe, clevel=clevel)
+        for n, bs in ((200_000, 0), (3 * 65536 + 4096, 65536), (1 << 20, 262144)):
+            src = plugin_input(kw, n, case * 7 + clevel)
+            want = oracle_compress(src, blocksize=bs, **kw)
+            got = B.compress(src, blocksize=bs, **kw)
+            assert isinstance(got, np.ndarray) and np.array_equal(got, want), (kw, n, bs)
+            dec = B.decompress(want, src.nbytes)
+            assert isinstance(dec, np.ndarray) and np.array_equal(dec, oracle_decompress(want, src.nbytes)), (kw, n)
+            if 36 not in kw["filters"]:
+                assert np.array_equal(dec, src)
+
+
+def test_plugin_filter_errors(B):
+    """Failing plugin filters end the pipeline with BLOSC2_ERROR_FILTER_PIPELINE, as in the reference."""
+    src = gen_f32(0, 50_000).view(np.uint8)
+    for kw in (dict(typesize=4, filters=(0, 0, 0, 0, 0, 36), filters_meta=(0, 0, 0, 0, 0, 40)),
+               dict(typesize=4, filters=(0, 0, 0, 0, 0, 36), filters_meta=(0, 0, 0, 0, 0, (-32) & 0xFF)),
+               dict(typesize=3, filters=(0, 0, 0, 0, 0, 36), filters_meta=(0, 0, 0, 0, 0, 4)),
+               dict(typesize=4, filters=(0, 0, 0, 0, 1, 35), filters_meta=(0,) * 6)):   # meta 0, no schunk
+        s = src[:49_998] if kw["typesize"] == 3 else src
+        assert B.compress(s, clevel=5, **kw) == -18, kw

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 from datagen import gen_f32, int64_ramp, mixed_bytes
+from b2ctypes import dparams
 from oracle_lib import oracle, oracle_compress, oracle_decompress, p, ref, ref_compress
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -152,3 +153,66 @@ def test_blosclz_streams_vs_ref(seed):
     assert _bytes_equal(got, want), (n, cl, bs)
     dec = oracle_decompress(want, n)
     assert np.array_equal(dec, src)
+
+
+# ---- registered plugin filters the device also runs: bytedelta (35), int_trunc (36) ----
+PLUGIN_PIPES = [
+    dict(typesize=4, filters=(0, 0, 0, 0, 1, 35), filters_meta=(0, 0, 0, 0, 0, 4)),
+    dict(typesize=8, filters=(0, 0, 0, 0, 1, 35), filters_meta=(0, 0, 0, 0, 0, 8)),
+    dict(typesize=4, filters=(0, 0, 0, 0, 35, 1), filters_meta=(0, 0, 0, 0, 4, 0)),
+    dict(typesize=2, filters=(0, 0, 0, 36, 1, 35), filters_meta=(0, 0, 0, 9, 0, 2)),
+    dict(typesize=8, filters=(0, 0, 0, 0, 36, 1), filters_meta=(0, 0, 0, 0, (-20) & 0xFF, 0)),
+    dict(typesize=4, filters=(0, 0, 0, 36, 3, 35), filters_meta=(0, 0, 0, 20, 0, 3)),
+    dict(typesize=1, filters=(0, 0, 0, 0, 0, 36), filters_meta=(0, 0, 0, 0, 0, 5)),
+]
+
+
+def plugin_input(kw, n, seed):
+    from datagen import gen_f32, int64_ramp
+    ts = kw["typesize"]
+    if ts == 4:
+        return gen_f32(seed, n // 4).view(np.uint8)
+    if ts == 8:
+        return int64_ramp(seed * 1000, n // 8).view(np.uint8)
+    rng = np.random.default_rng(seed)
+    return (np.cumsum(rng.integers(-3, 4, n // ts), dtype=np.int64) & (256 ** ts - 1)).astype(
+        {1: np.uint8, 2: np.uint16}[ts]).view(np.uint8)
+
+
+@pytest.mark.parametrize("case", range(len(PLUGIN_PIPES)))
+@pytest.mark.parametrize("clevel", [1, 5, 9])
+def test_plugin_filters_oracle_vs_reference(case, clevel):
+    """bytedelta / int_trunc pipelines (plugins/filters/*/test_*.c shapes: SHUFFLE then BYTEDELTA):
+    the oracle restatement produces the reference library's chunk bytes and decodes them back."""
+    R = ref()
+    if R is None:
+        pytest.skip("reference library not built")
+    kw = dict(PLUGIN_PIPES[case], clevel=clevel)
+    for n, bs in ((200_000, 0), (3 * 65536 + 4096, 65536)):
+        src = plugin_input(kw, n, case * 7 + clevel)
+        want = ref_compress(src, blocksize=bs, **kw)
+        got = oracle_compress(src, blocksize=bs, **kw)
+        assert isinstance(want, np.ndarray) and isinstance(got, np.ndarray)
+        assert np.array_equal(got, want), (kw, n)
+        dec = oracle_decompress(want, src.nbytes)
+        rdec = np.zeros(src.nbytes, np.uint8)
+        dctx = R.blosc2_create_dctx(dparams())
+        assert R.blosc2_decompress_ctx(dctx, p(want), want.nbytes, p(rdec), rdec.nbytes) == src.nbytes
+        R.blosc2_free_ctx(dctx)
+        assert np.array_equal(dec, rdec)
+        if 36 not in kw["filters"]:
+            assert np.array_equal(dec, src)
+
+
+def test_plugin_filter_errors_match_reference():
+    """int_trunc with an impossible precision and bytedelta with meta 0 outside a super-chunk fail
+    the pipeline (BLOSC2_ERROR_FILTER_PIPELINE) in both."""
+    R = ref()
+    if R is None:
+        pytest.skip("reference library not built")
+    src = gen_f32(0, 50_000).view(np.uint8)
+    for kw in (dict(typesize=4, filters=(0, 0, 0, 0, 0, 36), filters_meta=(0, 0, 0, 0, 0, 40)),
+               dict(typesize=4, filters=(0, 0, 0, 0, 0, 36), filters_meta=(0, 0, 0, 0, 0, (-32) & 0xFF)),
+               dict(typesize=3, filters=(0, 0, 0, 0, 0, 36), filters_meta=(0, 0, 0, 0, 0, 4))):
+        assert ref_compress(src[:49_998] if kw["typesize"] == 3 else src, **kw) == -18, kw
+        assert oracle_compress(src[:49_998] if kw["typesize"] == 3 else src, **kw) == -18, kw
