@@ -1,0 +1,309 @@
+// b2h_frame.cpp -- contiguous-frame read path on the MI355X engine.
+//
+// The reference reads a frame chunk by chunk: blosc2_schunk_decompress_chunk -> frame_decompress_chunk
+// (blosc/frame.c:5248-5290) -> frame_get_chunk (3378-3480) -> get_coffset (3283-3318, the offsets
+// index is itself a Blosc chunk read with blosc2_getitem) -> a read through the stdio backend
+// (blosc/blosc2-stdio.c:241-276) -> blosc2_decompress_ctx.  Here the whole frame is read once into
+// pinned host memory, copied to HBM in one transfer, the offsets chunk is decoded on the device,
+// and every data chunk of the frame goes through ONE device decompression batch.
+//
+// Supported: contiguous frames (frame_type 0) of format version <= 3 with 64-bit offsets and
+// regular (non-VL) blocks, whose chunks use the device pipeline (BloscLZ, built-in and plugin
+// filters).  Special offsets (runs of zeros / NaNs / uninitialised values, frame.c:3320-3365)
+// are materialised with fills.  Frame layout: README_CFRAME_FORMAT.rst.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../include/b2h.h"
+#include "../../include/blosc2.h"
+#include "b2h_engine.h"
+
+namespace {
+
+// Field offsets of the msgpack header (blosc/frame.h:29-49).
+constexpr int kMagic = 2, kHeaderLen = 11, kFrameLen = 16, kFlags = 25, kType = 26, kCodecs = 27,
+              kNbytes = 30, kCbytes = 39, kTypesize = 48, kBlocksize = 53, kChunksize = 58,
+              kFilters = 70, kHeaderMin = 87, kChunkHdr = 32;
+constexpr int kFrameFormatMax = 3;   // BLOSC2_VERSION_FRAME_FORMAT (include/blosc2.h:159)
+
+int64_t be(const uint8_t* p, int n) {   // big-endian msgpack integers (frame.c from_big)
+  uint64_t v = 0;
+  for (int i = 0; i < n; i++) v = (v << 8) | p[i];
+  if (n == 4) return (int64_t)(int32_t)(uint32_t)v;
+  return (int64_t)v;
+}
+int32_t le32(const uint8_t* p) { int32_t v; memcpy(&v, p, 4); return v; }
+
+__global__ void k_fill_pattern(uint8_t* dst, int64_t nbytes, uint64_t pattern, int width) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nbytes; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = (uint8_t)(pattern >> (8 * (i % width)));
+}
+
+}  // namespace
+
+struct b2h_frame {
+  uint8_t* host = nullptr;      // pinned copy of the whole frame
+  int64_t len = 0;
+  uint8_t* dev = nullptr;       // HBM copy (uploaded on first use)
+  int32_t header_len = 0;
+  int64_t nbytes = 0, cbytes = 0, nchunks = 0;
+  int32_t typesize = 0, blocksize = 0, chunksize = 0;
+  uint8_t compcode = 0, clevel = 0;
+  uint8_t filters[6] = {0}, filters_meta[6] = {0};
+  std::vector<int64_t> offsets;  // per chunk: >= 0 offset from the header start, < 0 special
+  hipStream_t stream = nullptr;
+};
+
+namespace {
+
+void frame_release(b2h_frame* f) {
+  if (!f) return;
+  if (f->host) (void)hipHostFree(f->host);
+  if (f->dev) (void)hipFree(f->dev);
+  if (f->stream) (void)hipStreamDestroy(f->stream);
+  delete f;
+}
+
+int32_t chunk_nbytes(const b2h_frame* f, int64_t i) {
+  if (i == f->nchunks - 1 && f->chunksize > 0 && f->nbytes % f->chunksize) return (int32_t)(f->nbytes % f->chunksize);
+  return f->chunksize;
+}
+
+int upload(b2h_frame* f) {
+  if (f->dev) return 0;
+  if (hipMalloc(&f->dev, (size_t)f->len) != hipSuccess) return BLOSC2_ERROR_MEMORY_ALLOC;
+  if (hipMemcpyAsync(f->dev, f->host, (size_t)f->len, hipMemcpyHostToDevice, f->stream) != hipSuccess)
+    return BLOSC2_ERROR_FAILURE;
+  return 0;
+}
+
+// Decode `n` chunks of the frame (device copy) into device outputs; status per chunk.
+int decode_chunks(b2h_frame* f, const std::vector<int64_t>& idx, const std::vector<uint8_t*>& outs,
+                  const std::vector<int32_t>& caps, std::vector<int32_t>* status) {
+  const int32_t n = (int32_t)idx.size();
+  if (n == 0) return 0;
+  std::vector<const uint8_t*> srcs(n);
+  std::vector<int32_t> sizes(n);
+  int64_t bound = 0;
+  for (int32_t k = 0; k < n; k++) {
+    const int64_t pos = f->header_len + f->offsets[idx[k]];
+    srcs[k] = f->dev + pos;
+    sizes[k] = le32(f->host + pos + 12);   // the chunk's own cbytes field
+    if (sizes[k] < 16 || pos + sizes[k] > f->header_len + f->cbytes) return BLOSC2_ERROR_INVALID_HEADER;
+    bound += caps[k];
+  }
+  void* blob = nullptr;
+  const size_t bytes = (size_t)n * (2 * sizeof(void*) + 3 * sizeof(int32_t));
+  if (hipMalloc(&blob, bytes) != hipSuccess) return BLOSC2_ERROR_MEMORY_ALLOC;
+  uint8_t* b = static_cast<uint8_t*>(blob);
+  const uint8_t** d_srcs = reinterpret_cast<const uint8_t**>(b);
+  uint8_t** d_dsts = reinterpret_cast<uint8_t**>(b + (size_t)n * sizeof(void*));
+  int32_t* d_sizes = reinterpret_cast<int32_t*>(b + (size_t)n * 2 * sizeof(void*));
+  int32_t* d_caps = d_sizes + n;
+  int32_t* d_status = d_caps + n;
+  int rc = 0;
+  if (hipMemcpyAsync(d_srcs, srcs.data(), n * sizeof(void*), hipMemcpyHostToDevice, f->stream) != hipSuccess ||
+      hipMemcpyAsync(d_dsts, outs.data(), n * sizeof(void*), hipMemcpyHostToDevice, f->stream) != hipSuccess ||
+      hipMemcpyAsync(d_sizes, sizes.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, f->stream) != hipSuccess ||
+      hipMemcpyAsync(d_caps, caps.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, f->stream) != hipSuccess) {
+    rc = BLOSC2_ERROR_FAILURE;
+  }
+  if (!rc) rc = b2h::decompress_batch(d_srcs, d_sizes, d_dsts, d_caps, n, bound, d_status, nullptr, f->stream);
+  status->assign(n, 0);
+  if (!rc && hipMemcpyAsync(status->data(), d_status, n * sizeof(int32_t), hipMemcpyDeviceToHost, f->stream) != hipSuccess)
+    rc = BLOSC2_ERROR_FAILURE;
+  if (hipStreamSynchronize(f->stream) != hipSuccess && !rc) rc = BLOSC2_ERROR_FAILURE;
+  (void)hipFree(blob);
+  return rc;
+}
+
+// get_header_info (blosc/frame.c:895-1060) for an in-memory contiguous frame, then the offsets
+// index (get_coffsets, 2102-2155) decoded on the device.
+int parse(b2h_frame* f) {
+  const uint8_t* h = f->host;
+  if (f->len < kHeaderMin) return BLOSC2_ERROR_READ_BUFFER;
+  if (h[0] < 0x90 || h[0] > 0x9f || memcmp(h + kMagic, "b2frame", 8) != 0) return BLOSC2_ERROR_INVALID_HEADER;
+  if ((h[kType] & 0x0f) != 0) return BLOSC2_ERROR_FRAME_TYPE;                  // contiguous only
+  if ((h[kFlags] & 0x0f) > kFrameFormatMax) return BLOSC2_ERROR_VERSION_SUPPORT;
+  if (((h[kFlags] >> 4) & 3) != 1) return BLOSC2_ERROR_VERSION_SUPPORT;         // 64-bit offsets
+  if (h[kFlags] & 0x80) return BLOSC2_ERROR_VERSION_SUPPORT;                    // VL blocks
+  f->header_len = (int32_t)be(h + kHeaderLen, 4);
+  const int64_t frame_len = be(h + kFrameLen, 8);
+  if (f->header_len < kHeaderMin || f->header_len > frame_len || frame_len > f->len) return BLOSC2_ERROR_INVALID_HEADER;
+  f->nbytes = be(h + kNbytes, 8);
+  f->cbytes = be(h + kCbytes, 8);
+  f->typesize = (int32_t)be(h + kTypesize, 4);
+  f->blocksize = (int32_t)be(h + kBlocksize, 4);
+  f->chunksize = (int32_t)be(h + kChunksize, 4);
+  if (f->typesize <= 0 || f->nbytes < 0 || f->cbytes < 0) return BLOSC2_ERROR_INVALID_HEADER;
+  f->compcode = h[kCodecs] & 0x0f;
+  f->clevel = h[kCodecs] >> 4;
+  const uint8_t nf = h[kFilters];
+  if (nf > 6) return BLOSC2_ERROR_INVALID_HEADER;
+  for (int i = 0; i < nf; i++) { f->filters[i] = h[kFilters + 1 + i]; f->filters_meta[i] = h[kFilters + 1 + 8 + i]; }
+  if (f->nbytes == 0) { f->nchunks = 0; return 0; }
+  if (f->chunksize <= 0) return BLOSC2_ERROR_VERSION_SUPPORT;                   // variable chunk sizes
+  f->nchunks = f->nbytes / f->chunksize + (f->nbytes % f->chunksize ? 1 : 0);
+  // offsets index: a Blosc chunk right after the data chunks
+  const int64_t off_pos = (int64_t)f->header_len + f->cbytes;
+  if (off_pos + kChunkHdr > f->len) return BLOSC2_ERROR_INVALID_HEADER;
+  const int32_t off_nbytes = le32(h + off_pos + 4), off_cbytes = le32(h + off_pos + 12);
+  if (off_nbytes != f->nchunks * 8 || off_cbytes < 16 || off_pos + off_cbytes > f->len) return BLOSC2_ERROR_INVALID_HEADER;
+  int rc = upload(f);
+  if (rc) return rc;
+  uint8_t* d_off = nullptr;
+  if (hipMalloc(&d_off, (size_t)off_nbytes) != hipSuccess) return BLOSC2_ERROR_MEMORY_ALLOC;
+  // decode the index chunk as a one-chunk batch (its offset relative to the header start is cbytes)
+  f->offsets.assign(1, f->cbytes);
+  std::vector<int32_t> st;
+  rc = [&]() {
+    // the index lies past the data section: widen the bounds check for this one call
+    const int64_t saved = f->cbytes;
+    f->cbytes = f->len - f->header_len;
+    const int r = decode_chunks(f, {0}, {d_off}, {off_nbytes}, &st);
+    f->cbytes = saved;
+    return r;
+  }();
+  if (!rc && st[0] != off_nbytes) rc = st[0] < 0 ? st[0] : BLOSC2_ERROR_DATA;
+  if (!rc) {
+    f->offsets.resize((size_t)f->nchunks);
+    if (hipMemcpy(f->offsets.data(), d_off, (size_t)off_nbytes, hipMemcpyDeviceToHost) != hipSuccess) rc = BLOSC2_ERROR_FAILURE;
+  }
+  (void)hipFree(d_off);
+  if (rc) return rc;
+  for (int64_t i = 0; i < f->nchunks; i++) {   // get_coffset bounds (frame.c:3297-3313)
+    const int64_t o = f->offsets[i];
+    if (o >= 0 && (f->header_len + o > f->header_len + f->cbytes - kChunkHdr || f->header_len + o > f->len - kChunkHdr))
+      return BLOSC2_ERROR_INVALID_HEADER;
+  }
+  return 0;
+}
+
+b2h_frame* open_pinned(uint8_t* host, int64_t len, int* err) {
+  b2h_frame* f = new b2h_frame();
+  f->host = host;
+  f->len = len;
+  int rc = hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking) == hipSuccess ? 0 : BLOSC2_ERROR_FAILURE;
+  if (!rc) rc = parse(f);
+  if (rc) { frame_release(f); f = nullptr; }
+  if (err) *err = rc;
+  return f;
+}
+
+// Special offset (frame.c:3320-3365): byte 7 bit 7 set, kind in bits 0-2 of byte 7.
+int fill_special(b2h_frame* f, int64_t special, uint8_t* d_dst, int32_t nbytes) {
+  const int kind = (int)(((uint64_t)special >> 56) & 0x7);
+  if (kind == BLOSC2_SPECIAL_ZERO) return hipMemsetAsync(d_dst, 0, (size_t)nbytes, f->stream) == hipSuccess ? 0 : BLOSC2_ERROR_FAILURE;
+  if (kind == BLOSC2_SPECIAL_UNINIT) return 0;
+  if (kind == BLOSC2_SPECIAL_NAN) {   // set_nans (blosc/blosc2.c:1612-1636): f32 / f64 quiet NaN
+    if (f->typesize != 4 && f->typesize != 8) return BLOSC2_ERROR_DATA;
+    const uint64_t pat = f->typesize == 4 ? 0x7fc00000ull : 0x7ff8000000000000ull;
+    k_fill_pattern<<<256, 256, 0, f->stream>>>(d_dst, nbytes, pat, f->typesize);
+    return hipGetLastError() == hipSuccess ? 0 : BLOSC2_ERROR_FAILURE;
+  }
+  return BLOSC2_ERROR_DATA;
+}
+
+}  // namespace
+
+extern "C" {
+
+b2h_frame* b2h_frame_from_buffer(const void* cframe, int64_t len, int* err) {
+  if (!cframe || len <= 0) { if (err) *err = BLOSC2_ERROR_READ_BUFFER; return nullptr; }
+  uint8_t* host = nullptr;
+  if (hipHostMalloc(reinterpret_cast<void**>(&host), (size_t)len, hipHostMallocDefault) != hipSuccess) {
+    if (err) *err = BLOSC2_ERROR_MEMORY_ALLOC;
+    return nullptr;
+  }
+  memcpy(host, cframe, (size_t)len);
+  return open_pinned(host, len, err);
+}
+
+// The stdio backend's read path (blosc/blosc2-stdio.c:241-276), one read of the whole file.
+b2h_frame* b2h_frame_open(const char* urlpath, int* err) {
+  FILE* fp = urlpath ? fopen(urlpath, "rb") : nullptr;
+  if (!fp) { if (err) *err = BLOSC2_ERROR_FILE_OPEN; return nullptr; }
+  int64_t len = -1;
+  if (fseek(fp, 0, SEEK_END) == 0) len = (int64_t)ftell(fp);
+  uint8_t* host = nullptr;
+  int rc = len > 0 ? 0 : BLOSC2_ERROR_FILE_READ;
+  if (!rc && (fseek(fp, 0, SEEK_SET) != 0 || hipHostMalloc(reinterpret_cast<void**>(&host), (size_t)len, hipHostMallocDefault) != hipSuccess))
+    rc = BLOSC2_ERROR_MEMORY_ALLOC;
+  if (!rc && fread(host, 1, (size_t)len, fp) != (size_t)len) rc = BLOSC2_ERROR_FILE_READ;
+  fclose(fp);
+  if (rc) {
+    if (host) (void)hipHostFree(host);
+    if (err) *err = rc;
+    return nullptr;
+  }
+  return open_pinned(host, len, err);
+}
+
+void b2h_frame_free(b2h_frame* f) { frame_release(f); }
+
+int b2h_frame_get_info(const b2h_frame* f, b2h_frame_info* info) {
+  if (!f || !info) return BLOSC2_ERROR_NULL_POINTER;
+  info->nbytes = f->nbytes;
+  info->cbytes = f->cbytes;
+  info->nchunks = f->nchunks;
+  info->typesize = f->typesize;
+  info->blocksize = f->blocksize;
+  info->chunksize = f->chunksize;
+  info->compcode = f->compcode;
+  info->clevel = f->clevel;
+  memcpy(info->filters, f->filters, 6);
+  memcpy(info->filters_meta, f->filters_meta, 6);
+  return 0;
+}
+
+int64_t b2h_frame_decompress(b2h_frame* f, void* d_dst, int64_t dst_capacity) {
+  if (!f || (!d_dst && f->nbytes)) return BLOSC2_ERROR_NULL_POINTER;
+  if (dst_capacity < f->nbytes) return BLOSC2_ERROR_WRITE_BUFFER;
+  uint8_t* out = static_cast<uint8_t*>(d_dst);
+  std::vector<int64_t> idx;
+  std::vector<uint8_t*> outs;
+  std::vector<int32_t> caps, st;
+  for (int64_t i = 0; i < f->nchunks; i++) {
+    uint8_t* o = out + i * (int64_t)f->chunksize;
+    if (f->offsets[i] < 0) {
+      const int rc = fill_special(f, f->offsets[i], o, chunk_nbytes(f, i));
+      if (rc) return rc;
+      continue;
+    }
+    idx.push_back(i);
+    outs.push_back(o);
+    caps.push_back(chunk_nbytes(f, i));
+  }
+  int rc = decode_chunks(f, idx, outs, caps, &st);
+  if (rc) return rc;
+  for (size_t k = 0; k < idx.size(); k++)
+    if (st[k] != caps[k]) return st[k] < 0 ? st[k] : BLOSC2_ERROR_DATA;
+  return f->nbytes;
+}
+
+int b2h_frame_decompress_chunk(b2h_frame* f, int64_t nchunk, void* dest, int32_t nbytes) {
+  if (!f || !dest) return BLOSC2_ERROR_NULL_POINTER;
+  if (nchunk < 0 || nchunk >= f->nchunks) return BLOSC2_ERROR_INVALID_PARAM;
+  const int32_t need = chunk_nbytes(f, nchunk);
+  if (nbytes < need) return BLOSC2_ERROR_WRITE_BUFFER;
+  uint8_t* d_out = nullptr;
+  if (hipMalloc(&d_out, (size_t)need) != hipSuccess) return BLOSC2_ERROR_MEMORY_ALLOC;
+  int rc = 0;
+  std::vector<int32_t> st;
+  if (f->offsets[nchunk] < 0) {
+    rc = fill_special(f, f->offsets[nchunk], d_out, need);
+  } else {
+    rc = decode_chunks(f, {nchunk}, {d_out}, {need}, &st);
+    if (!rc && st[0] != need) rc = st[0] < 0 ? st[0] : BLOSC2_ERROR_DATA;
+  }
+  if (!rc && hipMemcpyAsync(dest, d_out, (size_t)need, hipMemcpyDeviceToHost, f->stream) != hipSuccess) rc = BLOSC2_ERROR_FAILURE;
+  if (hipStreamSynchronize(f->stream) != hipSuccess && !rc) rc = BLOSC2_ERROR_FAILURE;
+  (void)hipFree(d_out);
+  return rc ? rc : need;
+}
+
+}  // extern "C"

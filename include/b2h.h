@@ -48,6 +48,34 @@ BLOSC_EXPORT int32_t b2h_shuffle(int32_t typesize, int32_t nbytes, const void *d
 BLOSC_EXPORT int32_t b2h_bitshuffle(int32_t typesize, int32_t nbytes, const void *d_src, void *d_dst, int inverse,
                                     void *stream);
 
+/* ---- contiguous-frame read path ----
+ * Replaces, for contiguous in-memory / on-disk frames (README_CFRAME_FORMAT.rst):
+ *   blosc2_schunk_open / blosc2_schunk_from_buffer (blosc/schunk.c) + frame_get_chunk / get_coffset
+ *   (blosc/frame.c:3283-3480) + blosc2_schunk_decompress_chunk -> frame_decompress_chunk
+ *   (blosc/frame.c:5248-5290), with the stdio backend's reads (blosc/blosc2-stdio.c:241-276).
+ * The frame is read once into pinned memory and copied to HBM; the offsets index is decoded on the
+ * device; b2h_frame_decompress decodes every chunk in one device batch.  Read-only: frames must be
+ * contiguous, 64-bit offsets, fixed chunk size, regular blocks, device-pipeline codecs/filters.
+ * Errors: NULL + *err = BLOSC2_ERROR_* (FILE_OPEN, FILE_READ, FRAME_TYPE, VERSION_SUPPORT,
+ * INVALID_HEADER, DATA, MEMORY_ALLOC). */
+typedef struct b2h_frame b2h_frame;
+typedef struct {
+  int64_t nbytes, cbytes, nchunks;
+  int32_t typesize, blocksize, chunksize;
+  uint8_t compcode, clevel;
+  uint8_t filters[6], filters_meta[6];
+} b2h_frame_info;
+BLOSC_EXPORT b2h_frame *b2h_frame_open(const char *urlpath, int *err);
+BLOSC_EXPORT b2h_frame *b2h_frame_from_buffer(const void *cframe, int64_t len, int *err);
+BLOSC_EXPORT void b2h_frame_free(b2h_frame *frame);
+BLOSC_EXPORT int b2h_frame_get_info(const b2h_frame *frame, b2h_frame_info *info);
+/* Every chunk of the frame into device memory d_dst (chunk i at i * chunksize).  Returns nbytes or
+ * a BLOSC2_ERROR_* code.  Synchronous. */
+BLOSC_EXPORT int64_t b2h_frame_decompress(b2h_frame *frame, void *d_dst, int64_t dst_capacity);
+/* One chunk into a host buffer: blosc2_schunk_decompress_chunk semantics (returns the chunk's
+ * nbytes, BLOSC2_ERROR_WRITE_BUFFER when `nbytes` is too small). */
+BLOSC_EXPORT int b2h_frame_decompress_chunk(b2h_frame *frame, int64_t nchunk, void *dest, int32_t nbytes);
+
 /* Per-phase HIP-event timings of the last batch on this process (ms): filter, encode, finalize,
  * decode, unfilter.  Enabling adds event records only (no extra synchronisation until read). */
 BLOSC_EXPORT void b2h_enable_timing(int on);

@@ -749,9 +749,19 @@ int or_decompress_chunk(const void *src_, int32_t srcsize, void *dest_, int32_t 
   if (memcpyed && h.cbytes != h.nbytes + h.overhead) return ERR_DATA;
   if (h.nbytes == 0 && h.cbytes == h.overhead && !special) return 0;
   if (special) {
+    /* blosc_d special fills (blosc/blosc2.c:1865-1935): set_values 1644-1700 repeats the typesize
+       bytes stored after the 32-byte header; set_nans 1612-1641 writes quiet NaNs (ts 4/8 only). */
+    int32_t ts = h.typesize;
     if (special == SPECIAL_ZERO) memset(dest, 0, (size_t)h.nbytes);
     else if (special == SPECIAL_UNINIT) { /* nothing */ }
-    else return ERR_DATA;   /* NaN / value specials are outside this oracle */
+    else if (special == SPECIAL_VALUE) {
+      if (h.nbytes % ts != 0 || srcsize < h.overhead + ts) return ERR_DATA;
+      for (int32_t i = 0; i < h.nbytes; i += ts) memcpy(dest + i, src + h.overhead, (size_t)ts);
+    } else if (special == SPECIAL_NAN) {
+      if (h.nbytes % ts != 0 || (ts != 4 && ts != 8)) return ERR_DATA;
+      static const uint8_t nan4[4] = {0, 0, 0xc0, 0x7f}, nan8[8] = {0, 0, 0, 0, 0, 0, 0xf8, 0x7f};
+      for (int32_t i = 0; i < h.nbytes; i += ts) memcpy(dest + i, ts == 4 ? nan4 : nan8, (size_t)ts);
+    } else return ERR_DATA;
     return h.nbytes;
   }
   if (memcpyed) {
