@@ -448,6 +448,184 @@ int or_blosclz_decompress(const uint8_t *in, int length, uint8_t *out, int maxou
   return op;
 }
 
+/* ------------------------------------------------------------------------------ LZ4 ---- */
+/* LZ4 block format, compformat 1 (blosc/blosc2.c:450-469 lz4_wrap_compress -> LZ4_compress_fast,
+ * 500-519 lz4_wrap_decompress -> LZ4_decompress_safe).  LZ4 is a third-party dependency, absent
+ * from /root/reference: CMakeLists.txt:141 pins lz4 1.10.0; the image ships lz4 1.9.3
+ * (/opt/conda/lib/liblz4.so, the library oracle/_ref links).  Restated from the published
+ * algorithm of lz4.c LZ4_compress_generic (noDict, limitedOutput, byU16 table of 2^13 u16
+ * positions with hash4 when the input is < 64 KiB + 11, else byU32 of 2^12 with the 5-byte hash)
+ * and pinned byte-for-byte against liblz4 itself (tests/test_oracle.py::test_lz4_*). */
+enum { LZ4_MINMATCH = 4, LZ4_MFLIMIT = 12, LZ4_LASTLIT = 5, LZ4_SKIP = 6, LZ4_RUN_MASK = 15,
+       LZ4_ML_MASK = 15, LZ4_64K = 65536 + 11, LZ4_DMAX = 65535 };
+
+static inline uint32_t lz4_hash_at(const uint8_t *p, int u16tab) {
+  if (u16tab) return (ld32(p) * 2654435761U) >> (32 - 13);                  /* LZ4_hash4, log 12+1 */
+  uint64_t v; memcpy(&v, p, 8);
+  return (uint32_t)(((v << 24) * 889523592379ULL) >> (64 - 12));            /* LZ4_hash5, log 12 */
+}
+
+/* LZ4_count: equal bytes of in[a..] and in[b..] before `limit` */
+static inline int32_t lz4_count(const uint8_t *in, int32_t a, int32_t b, int32_t limit) {
+  int32_t n = 0;
+  while (a + n < limit && in[a + n] == in[b + n]) n++;
+  return n;
+}
+
+/* LZ4_compress_fast(in, out, length, maxout, accel) for maxout < LZ4_compressBound(length) (the
+ * only case blosc reaches: maxout <= neblock).  Returns the compressed size, 0 if it does not
+ * fit.  *peak (optional) = the largest `op + need` of the output checks relative to out. */
+int or_lz4_compress(int accel, const uint8_t *in, int length, uint8_t *out, int maxout) {
+  if (accel < 1) accel = 1;
+  if (accel > 65537) accel = 65537;
+  if (length < 0 || length > 0x7E000000) return 0;
+  if (length == 0) { if (maxout <= 0) return 0; out[0] = 0; return 1; }
+  const int u16tab = length < LZ4_64K;
+  uint32_t *tab = (uint32_t *)calloc(1u << 13, sizeof(uint32_t));
+  if (!tab) return -1;
+  const int32_t iend = length, mflimit1 = length - LZ4_MFLIMIT + 1, matchlimit = length - LZ4_LASTLIT;
+  int32_t ip = 0, anchor = 0, op = 0, match = 0;
+  int rc = 0;
+  if (length < LZ4_MFLIMIT + 1) goto last_literals;
+  tab[lz4_hash_at(in, u16tab)] = 0;
+  ip = 1;
+  uint32_t fwdh = lz4_hash_at(in + ip, u16tab);
+  for (;;) {
+    /* find a match: step grows by one every 2^LZ4_SKIP failed probes */
+    int32_t fwd = ip, step = 1, nb = accel << LZ4_SKIP;
+    for (;;) {
+      uint32_t h = fwdh;
+      int32_t cur = fwd;
+      int32_t mi = (int32_t)tab[h];
+      ip = fwd;
+      fwd += step;
+      step = nb++ >> LZ4_SKIP;
+      if (fwd > mflimit1) goto last_literals;
+      match = mi;
+      fwdh = lz4_hash_at(in + fwd, u16tab);
+      tab[h] = (uint32_t)cur;
+      if (!u16tab && mi + LZ4_DMAX < cur) continue;   /* too far (byU32 only) */
+      if (ld32(in + match) == ld32(in + ip)) break;
+    }
+    /* catch up */
+    while (ip > anchor && match > 0 && in[ip - 1] == in[match - 1]) { ip--; match--; }
+    int32_t token;
+    {
+      int32_t lit = ip - anchor;
+      token = op++;
+      if (op + lit + (2 + 1 + LZ4_LASTLIT) + lit / 255 > maxout) goto fail;
+      if (lit >= LZ4_RUN_MASK) {
+        int32_t len = lit - LZ4_RUN_MASK;
+        out[token] = LZ4_RUN_MASK << 4;
+        for (; len >= 255; len -= 255) out[op++] = 255;
+        out[op++] = (uint8_t)len;
+      } else {
+        out[token] = (uint8_t)(lit << 4);
+      }
+      memcpy(out + op, in + anchor, (size_t)lit);
+      op += lit;
+    }
+    for (;;) {   /* _next_match */
+      out[op] = (uint8_t)(ip - match); out[op + 1] = (uint8_t)((ip - match) >> 8);
+      op += 2;
+      int32_t mc = lz4_count(in, ip + LZ4_MINMATCH, match + LZ4_MINMATCH, matchlimit);
+      ip += mc + LZ4_MINMATCH;
+      if (op + (1 + LZ4_LASTLIT) + (mc + 240) / 255 > maxout) goto fail;
+      if (mc >= LZ4_ML_MASK) {
+        out[token] += LZ4_ML_MASK;
+        mc -= LZ4_ML_MASK;
+        for (; mc >= 255; mc -= 255) out[op++] = 255;
+        out[op++] = (uint8_t)mc;
+      } else {
+        out[token] += (uint8_t)mc;
+      }
+      anchor = ip;
+      if (ip >= mflimit1) goto last_literals;
+      tab[lz4_hash_at(in + ip - 2, u16tab)] = (uint32_t)(ip - 2);
+      /* test the next position for an immediate match */
+      uint32_t h = lz4_hash_at(in + ip, u16tab);
+      int32_t mi = (int32_t)tab[h];
+      tab[h] = (uint32_t)ip;
+      if ((u16tab || mi + LZ4_DMAX >= ip) && ld32(in + mi) == ld32(in + ip)) {
+        match = mi;
+        token = op++;
+        out[token] = 0;
+        continue;
+      }
+      break;
+    }
+    fwdh = lz4_hash_at(in + ++ip, u16tab);
+  }
+last_literals:
+  {
+    int32_t last = iend - anchor;
+    if (op + last + 1 + (last + 255 - LZ4_RUN_MASK) / 255 > maxout) goto fail;
+    if (last >= LZ4_RUN_MASK) {
+      int32_t acc = last - LZ4_RUN_MASK;
+      out[op++] = LZ4_RUN_MASK << 4;
+      for (; acc >= 255; acc -= 255) out[op++] = 255;
+      out[op++] = (uint8_t)acc;
+    } else {
+      out[op++] = (uint8_t)(last << 4);
+    }
+    memcpy(out + op, in + anchor, (size_t)last);
+    op += last;
+  }
+  rc = op;
+fail:
+  free(tab);
+  return rc;
+}
+
+/* LZ4_decompress_safe: the decoded size, or < 0 for a malformed stream.  Rejections: truncated
+ * input, output overflow, a reference before the output start, a match reaching into the last
+ * LASTLITERALS bytes of the output, a stream that does not end on a literal run. */
+int or_lz4_decompress(const uint8_t *in, int length, uint8_t *out, int maxout) {
+  if (length <= 0) return -1;
+  if (maxout == 0) return (length == 1 && in[0] == 0) ? 0 : -1;
+  int32_t ip = 0, op = 0;
+  for (;;) {
+    if (ip >= length) return -1;
+    uint32_t token = in[ip++];
+    int32_t lit = (int32_t)(token >> 4);
+    if (lit == LZ4_RUN_MASK) {
+      uint32_t s;
+      do {
+        if (ip >= length) return -1;
+        s = in[ip++];
+        lit += (int32_t)s;
+        if (lit > maxout) return -1;
+      } while (s == 255);
+    }
+    if (op + lit > maxout - LZ4_MFLIMIT || ip + lit > length - (2 + 1 + LZ4_LASTLIT)) {
+      /* the last sequence: literals only, consuming the input exactly */
+      if (ip + lit != length || op + lit > maxout) return -1;
+      memcpy(out + op, in + ip, (size_t)lit);
+      return op + lit;
+    }
+    memcpy(out + op, in + ip, (size_t)lit);
+    op += lit; ip += lit;
+    int32_t off = in[ip] | (in[ip + 1] << 8);
+    ip += 2;
+    if (off > op) return -1;   /* offset 0 is accepted by liblz4 1.9.3 (it copies zeros) */
+    int32_t ml = (int32_t)(token & 15u);
+    if (ml == LZ4_ML_MASK) {
+      uint32_t s;
+      do {
+        if (ip >= length - LZ4_LASTLIT) return -1;
+        s = in[ip++];
+        ml += (int32_t)s;
+        if (ml > maxout) return -1;
+      } while (s == 255);
+    }
+    ml += LZ4_MINMATCH;
+    if (op + ml > maxout - LZ4_LASTLIT) return -1;
+    if (off == 0) memset(out + op, 0, (size_t)ml);
+    else for (int32_t i = 0; i < ml; i++) out[op + i] = out[op - off + i];
+    op += ml;
+  }
+}
+
 /* ----------------------------------------------------------------------- chunk framing ---- */
 /* blosc/stune.c:186-215 */
 int or_split_block(const or_cparams *cp, int32_t typesize, int32_t blocksize) {
@@ -455,7 +633,7 @@ int or_split_block(const or_cparams *cp, int32_t typesize, int32_t blocksize) {
   if (cp->splitmode == SPLIT_NEVER) return 0;
   int shuffle_on = 0;
   for (int i = 0; i < 6; i++) shuffle_on |= cp->filters[i] == FLT_SHUFFLE;
-  return cp->compcode == 0 && shuffle_on && typesize <= 16 && (blocksize / typesize) >= MIN_BUF;
+  return (cp->compcode == 0 || cp->compcode == 1) && shuffle_on && typesize <= 16 && (blocksize / typesize) >= MIN_BUF;
 }
 
 static int32_t eff_typesize(const or_cparams *cp) { return cp->typesize > 255 ? 1 : cp->typesize; }
@@ -572,7 +750,9 @@ static int32_t compress_block(const or_cparams *cp, int32_t ts, int split, uint8
       maxout = destsize - ntbytes;
       if (maxout <= 0) return 0;
     }
-    int32_t cb = or_blosclz_compress(cp->clevel, s, neblock, dest + written, maxout);
+    /* the codec call (blosc/blosc2.c:1357-1366); LZ4's acceleration is 10 - clevel (get_accel 619-629) */
+    int32_t cb = cp->compcode == 1 ? or_lz4_compress(10 - cp->clevel, s, neblock, dest + written, maxout)
+                                   : or_blosclz_compress(cp->clevel, s, neblock, dest + written, maxout);
     if (cb < 0) return ERR_DATA;
     if (cb == 0) cb = neblock;
     if (cb == neblock) {
@@ -591,7 +771,7 @@ int or_compress_chunk(const or_cparams *cp, const void *src_, int32_t srcsize, v
                       int32_t destsize) {
   const uint8_t *src = (const uint8_t *)src_;
   uint8_t *dest = (uint8_t *)dest_;
-  if (cp->compcode != 0) return ERR_CODEC;
+  if (cp->compcode != 0 && cp->compcode != 1) return ERR_CODEC;   /* BloscLZ, LZ4 */
   if (srcsize > 0x7fffffff - 32) return -9;
   if (destsize < 32) return -9;
   if (cp->clevel < 0 || cp->clevel > 9) return -10;
@@ -614,7 +794,8 @@ int or_compress_chunk(const or_cparams *cp, const void *src_, int32_t srcsize, v
       if (cp->filters[i] == FLT_DELTA) flags |= F_DELTA;
     }
     split = or_split_block(cp, ts, bs);
-    flags |= (uint8_t)((!split) << 4);       /* dont_split, bit 4; compformat 0 in bits 5-7 */
+    flags |= (uint8_t)((!split) << 4);       /* dont_split, bit 4 */
+    flags |= (uint8_t)(cp->compcode << 5);  /* compformat: BLOSCLZ 0, LZ4 1 (blosc2.c:2990-2991) */
   }
   /* header: blosc2_initialize_header_from_context, blosc/blosc2.c:1000-1046 */
   memset(dest, 0, HDR_EXT);
@@ -768,7 +949,8 @@ int or_decompress_chunk(const void *src_, int32_t srcsize, void *dest_, int32_t 
     memcpy(dest, src + h.overhead, (size_t)h.nbytes);
     return h.nbytes;
   }
-  if ((h.flags >> 5) != 0) return ERR_CODEC;   /* only BloscLZ */
+  const int compformat = h.flags >> 5;
+  if (compformat > 1) return ERR_CODEC;   /* BloscLZ and LZ4 */
   int32_t bstarts_end = h.overhead + 4 * h.nblocks;
   if (srcsize < bstarts_end) return ERR_READ;
   int dont_split = (h.flags >> 4) & 1;
@@ -808,7 +990,8 @@ int or_decompress_chunk(const void *src_, int32_t srcsize, void *dest_, int32_t 
         if (avail < cb) { rc = ERR_READ; break; }
         if (cb == neblock) {
           memcpy(d, p, (size_t)neblock);
-        } else if (or_blosclz_decompress(p, cb, d, neblock) != neblock) {
+        } else if ((compformat == 1 ? or_lz4_decompress(p, cb, d, neblock)
+                                    : or_blosclz_decompress(p, cb, d, neblock)) != neblock) {
           rc = ERR_DATA; break;
         }
         p += cb; avail -= cb;

@@ -43,6 +43,11 @@ int or_trunc_prec(int8_t prec_bits, int32_t typesize, int32_t nbytes, const uint
 int or_blosclz_compress(int clevel, const uint8_t *in, int length, uint8_t *out, int maxout);
 int or_blosclz_decompress(const uint8_t *in, int length, uint8_t *out, int maxout);
 
+/* LZ4 block codec, compformat 1 (blosc/blosc2.c:450-519 -> lz4 1.9.3 LZ4_compress_fast /
+ * LZ4_decompress_safe).  compress returns 0 when the output does not fit in maxout. */
+int or_lz4_compress(int accel, const uint8_t *in, int length, uint8_t *out, int maxout);
+int or_lz4_decompress(const uint8_t *in, int length, uint8_t *out, int maxout);
+
 /* Chunk engine, serial (nthreads == 1) layout, BloscLZ codec only.
  * cparams mirror blosc2_cparams (include/blosc2.h of the reference, 1173-1211). */
 typedef struct {

@@ -71,9 +71,9 @@ def ref():
 
 
 def or_cparams(clevel=5, typesize=4, filters=(0, 0, 0, 0, 0, 1), filters_meta=(0,) * 6,
-               blocksize=0, splitmode=4):
+               blocksize=0, splitmode=4, compcode=0):
     p = OrCParams()
-    p.compcode, p.clevel, p.typesize, p.blocksize, p.splitmode = 0, clevel, typesize, blocksize, splitmode
+    p.compcode, p.clevel, p.typesize, p.blocksize, p.splitmode = compcode, clevel, typesize, blocksize, splitmode
     for i in range(6):
         p.filters[i], p.filters_meta[i] = filters[i], filters_meta[i] & 0xFF
     return p
@@ -103,7 +103,8 @@ def ref_compress(src: np.ndarray, **kw):
     cp = cparams(clevel=kw.get("clevel", 5), typesize=kw.get("typesize", 4),
                  filters=kw.get("filters", (0, 0, 0, 0, 0, 1)),
                  filters_meta=kw.get("filters_meta", (0,) * 6),
-                 blocksize=kw.get("blocksize", 0), splitmode=kw.get("splitmode", 4))
+                 blocksize=kw.get("blocksize", 0), splitmode=kw.get("splitmode", 4),
+                 compcode=kw.get("compcode", 0))
     ctx = R.blosc2_create_cctx(cp)
     raw = src.view(np.uint8).reshape(-1).copy()   # the reference may rewrite its input
     out = np.zeros(raw.nbytes + 64, np.uint8)

@@ -216,3 +216,113 @@ def test_plugin_filter_errors_match_reference():
                dict(typesize=3, filters=(0, 0, 0, 0, 0, 36), filters_meta=(0, 0, 0, 0, 0, 4))):
         assert ref_compress(src[:49_998] if kw["typesize"] == 3 else src, **kw) == -18, kw
         assert oracle_compress(src[:49_998] if kw["typesize"] == 3 else src, **kw) == -18, kw
+
+
+# ---------------------------------------------------------------------------------- LZ4 ----
+# LZ4 (compformat 1) is a third-party dependency absent from /root/reference; the image ships
+# lz4 1.9.3 (/opt/conda/lib/liblz4.so.1, the library oracle/_ref links).  The restatement is
+# pinned byte-for-byte against that library directly, and at chunk level against oracle/_ref.
+LZ4_SO = "/opt/conda/lib/liblz4.so.1"
+needs_lz4 = pytest.mark.skipif(not os.path.exists(LZ4_SO), reason="liblz4 not in this image")
+
+
+def _lz4_inputs():
+    f = gen_f32(0, 1 << 16).view(np.uint8)
+    sh = np.ascontiguousarray(f[:262144].reshape(-1, 4).T).reshape(-1)
+    rng = np.random.default_rng(11)
+    yield from (f[:65536], f[:65536 + 11], f[:200_000], sh[:65536], sh[196608:], sh)
+    yield int64_ramp(0, 16384).view(np.uint8)
+    for n in (0, 1, 12, 13, 14, 100, 4096, 70_000):
+        yield rng.integers(0, 4, n, dtype=np.uint8)
+        yield rng.integers(0, 256, n, dtype=np.uint8)
+    yield np.zeros(65536, np.uint8)
+    yield np.tile(np.arange(7, dtype=np.uint8), 20_000)
+
+
+@needs_lz4
+def test_lz4_codec_vs_liblz4():
+    """or_lz4_compress == LZ4_compress_fast for every acceleration blosc uses (10 - clevel) and
+    output limits below and above LZ4_compressBound; or_lz4_decompress inverts it."""
+    L, O = C.CDLL(LZ4_SO), oracle()
+    for a in _lz4_inputs():
+        a = np.ascontiguousarray(a)
+        for accel in (1, 2, 5, 9):
+            for maxout in (a.nbytes, a.nbytes // 2, max(a.nbytes // 8, 1), a.nbytes + a.nbytes // 255 + 16):
+                o1, o2 = np.zeros(maxout + 64, np.uint8), np.zeros(maxout + 64, np.uint8)
+                r1 = L.LZ4_compress_fast(p(a), p(o1), a.nbytes, maxout, accel)
+                r2 = O.or_lz4_compress(accel, p(a), a.nbytes, p(o2), maxout)
+                assert r1 == r2 and np.array_equal(o1[:r1], o2[:r2]), (a.nbytes, accel, maxout)
+                if r1 > 0 and a.nbytes:
+                    d = np.zeros(a.nbytes + 8, np.uint8)
+                    assert O.or_lz4_decompress(p(o1), r1, p(d), a.nbytes) == a.nbytes
+                    assert np.array_equal(d[:a.nbytes], a)
+
+
+@needs_lz4
+def test_lz4_decoder_rejections_vs_liblz4():
+    """Corrupted / truncated streams: the restatement accepts exactly what LZ4_decompress_safe
+    accepts, with the same output."""
+    L, O = C.CDLL(LZ4_SO), oracle()
+    rng = np.random.default_rng(5)
+    for a in (gen_f32(3, 1 << 14).view(np.uint8), int64_ramp(0, 8192).view(np.uint8)):
+        o = np.zeros(a.nbytes * 2 + 64, np.uint8)
+        r = L.LZ4_compress_fast(p(a), p(o), a.nbytes, o.nbytes, 1)
+        for t in range(400):
+            c = o[:r].copy()
+            if t % 3 == 0:
+                c[rng.integers(0, r)] = rng.integers(0, 256)
+            elif t % 3 == 1:
+                c = c[:rng.integers(1, r)].copy()
+            else:
+                for _ in range(3):
+                    c[rng.integers(0, r)] ^= 1 << rng.integers(0, 8)
+            for cap in (a.nbytes, a.nbytes + 7):
+                d1, d2 = np.zeros(cap + 64, np.uint8), np.zeros(cap + 64, np.uint8)
+                r1 = L.LZ4_decompress_safe(p(c), p(d1), c.nbytes, cap)
+                r2 = O.or_lz4_decompress(p(c), c.nbytes, p(d2), cap)
+                assert (r1 >= 0) == (r2 >= 0), (t, cap, r1, r2)
+                if r1 >= 0:
+                    assert r1 == r2 and np.array_equal(d1[:r1], d2[:r2])
+
+
+@needs_ref
+@pytest.mark.parametrize("clevel", [1, 5, 9])
+@pytest.mark.parametrize("filters", [(0, 0, 0, 0, 0, 1), (0, 0, 0, 0, 0, 2), (0, 0, 0, 0, 3, 1),
+                                     (0, 0, 0, 0, 0, 0)])
+def test_lz4_chunks_vs_ref(clevel, filters):
+    """Whole chunks with compcode BLOSC_LZ4: the oracle's bytes are the reference library's."""
+    for name, src, ts in _inputs():
+        want = ref_compress(src, clevel=clevel, typesize=ts, filters=filters, compcode=1)
+        got = oracle_compress(src, clevel=clevel, typesize=ts, filters=filters, compcode=1)
+        assert _bytes_equal(got, want), (name, clevel, filters)
+        back = oracle_decompress(got, src.nbytes)
+        assert np.array_equal(back, src.view(np.uint8).reshape(-1)), name
+
+
+LZ4_KATS = ["blosc-lz4-3.0.0.cdata", "blosc-1.11.1-lz4.cdata", "blosc-1.14.0-lz4.cdata",
+            "blosc-1.17.1-lz4-bitshuffle4-memcpy.cdata", "blosc-1.17.1-lz4-bitshuffle8-nomemcpy.cdata",
+            "blosc-1.18.0-lz4-bitshuffle4-memcpy.cdata", "blosc-1.18.0-lz4-bitshuffle8-nomemcpy.cdata"]
+
+
+@pytest.mark.parametrize("name", LZ4_KATS)
+def test_lz4_decode_kats(name):
+    """compat/*lz4*.cdata (the int32 ramp of compat/filegen.c:178-180, written by Blosc 1.11 .. 3.0
+    with LZ4) decode to the ramp (compat/CMakeLists.txt:15-33 `filegen decompress`)."""
+    gold = np.fromfile(os.path.join(GOLD, name), np.uint8)
+    nbytes, ts = int(gold[4:8].view(np.int32)[0]), int(gold[3])
+    out = oracle_decompress(gold, nbytes)
+    assert isinstance(out, np.ndarray)
+    # The 1.17/1.18 bitshuffle files hold the first 641 09x bytes of the ramp.  Their last block is
+    # a format-version-2 bitshuffle whose trailing nbytes % ts bytes the reference never writes
+    # (blosc/shuffle.c:489-500 un-bitshuffles n elements and copies no tail; the caller's buffer
+    # keeps its old bytes there): only whole elements are compared.
+    whole = nbytes - nbytes % ts if gold[0] == 2 and gold[2] & 4 else nbytes
+    assert np.array_equal(out[:whole], RAMP.view(np.uint8)[:whole])
+
+
+def test_lz4_chunk_kat():
+    """compat/blosc-lz4-3.0.0.cdata == blosc1_compress(9, SHUFFLE, 4, ramp) with LZ4, 1 thread
+    (compat/filegen.c:91): the oracle re-encodes it byte-identically."""
+    gold = np.fromfile(os.path.join(GOLD, "blosc-lz4-3.0.0.cdata"), np.uint8)
+    got = oracle_compress(RAMP, clevel=9, typesize=4, compcode=1, splitmode=4)
+    assert isinstance(got, np.ndarray) and np.array_equal(got, gold)
