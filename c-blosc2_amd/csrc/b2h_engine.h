@@ -22,6 +22,7 @@ struct CompressPlan {
   uint8_t filters[6];
   uint8_t filters_meta[6];
   uint8_t header[32];      // header template (cbytes patched per chunk)
+  int32_t compcode;        // BLOSC_BLOSCLZ (0) or BLOSC_LZ4 (1)
 };
 
 // Fill the plan from cparams-level values the way blosc2_compress_ctx does (initialize_context_
@@ -29,7 +30,8 @@ struct CompressPlan {
 // invalid parameters.  `ctx_blocksize` is the blocksize the context currently holds (0 = auto).
 int make_compress_plan(CompressPlan* p, int32_t nbytes, int32_t destsize, int clevel, int32_t typesize,
                        int32_t ctx_blocksize, int32_t splitmode, const uint8_t* filters,
-                       const uint8_t* filters_meta, int32_t* computed_blocksize, bool extended = true);
+                       const uint8_t* filters_meta, int32_t* computed_blocksize, bool extended = true,
+                       int compcode = 0);
 
 // Compress `nchunks` chunks: chunk i is d_src + i*src_stride, its output goes to
 // d_dst + i*dst_stride (capacity plan.destsize), its cbytes (>0, 0 = does not fit) to d_cbytes[i].

@@ -70,7 +70,8 @@ struct Scratch {
 };
 
 struct Workspace {
-  Scratch t1, t2, work, sbuf, res, place, mode, qctr, gtab;    // compress
+  Scratch t1, t2, work, sbuf, res, place, mode, qctr, gtab, lz4tab;    // compress
+  size_t lz4_lanes = 0;
   Scratch dchunks, dstreams, dblocks, dtotals, stage, stage2, ptrs, dqctr, ddbg;  // decompress
   std::mutex mu;
 };
@@ -154,7 +155,7 @@ static EvPair ev_filter, ev_encode, ev_final, ev_decode, ev_unfilter;
 
 // ================================================================ compression: geometry ====
 struct CGeom {
-  int32_t nbytes, bs, nblocks, leftover, spb, nsc, neblock, ts, destsize, clevel, overhead;
+  int32_t nbytes, bs, nblocks, leftover, spb, nsc, neblock, ts, destsize, clevel, overhead, compcode;
   int64_t src_stride, wstride, dst_stride;
 };
 
@@ -270,6 +271,225 @@ __global__ __launch_bounds__(64 * (NLDS + NGLB)) void k_encode(CGeom g, const ui
   }
 }
 
+// ------------------------------------------------------------------------ LZ4 encoder ----
+// LZ4_compress_fast (lz4 1.9.3, noDict, limited output; restated in oracle/blosc2_oracle.c
+// or_lz4_compress) with acceleration 10 - clevel (blosc/blosc2.c:619-629).  LZ4's parse skips
+// ahead by a step that grows with every 64 failed probes and has no window structure to share
+// across a wave, so every LANE owns one stream: 64 streams per wave advance in lockstep through
+// the probe loop, each lane pulling its next stream from the device counter when it finishes.
+// The per-lane hash table (2^13 u32 entries = 32 KiB, global memory, private to the lane) holds
+// `tag << 24 | position`: a stale tag reads as position 0, i.e. the zeroed table LZ4_initStream
+// starts each call with, so no per-stream clearing is needed.
+constexpr int kLz4TabLog = 13;
+constexpr int32_t kLz4MaxStream = 1 << 24;   // positions must fit below the tag
+
+__device__ __forceinline__ uint32_t lz4_hash_at(gin_t p, bool u16tab) {
+  const uint32_t lo = ldu32(p);
+  if (u16tab) return (lo * 2654435761u) >> (32 - 13);                           // LZ4_hash4, log 12+1
+  const uint64_t v = (uint64_t)lo | ((uint64_t)ldu32(p + 4) << 32);
+  return (uint32_t)(((v << 24) * 889523592379ull) >> (64 - 12));                // LZ4_hash5, log 12
+}
+
+struct Lz4Tab {
+  B2H_GLB uint32_t* t;
+  uint32_t tag;
+  __device__ __forceinline__ int32_t get(uint32_t h) const {
+    const uint32_t e = t[h];
+    return (e >> 24) == tag ? (int32_t)(e & 0xffffffu) : 0;
+  }
+  __device__ __forceinline__ void put(uint32_t h, int32_t pos) const { t[h] = (tag << 24) | (uint32_t)pos; }
+};
+
+// Encode one stream with olimit = n (the stream's own size); returns the encoded size, or 0 when
+// an output check fails (then the stream is stored raw).  *peak = the largest `op + need` tested.
+__device__ int32_t lz4_encode_lane(gin_t in, int32_t n, int accel, B2H_GLB uint8_t* out, const Lz4Tab& tab,
+                                   int32_t* peak_out) {
+  constexpr int32_t kMfLimit = 12, kLastLit = 5, kRunMask = 15, kDMax = 65535;
+  const bool u16tab = n < 65536 + 11;
+  const int32_t mflimit1 = n - kMfLimit + 1, matchlimit = n - kLastLit;
+  int32_t ip = 0, anchor = 0, op = 0, match = 0, peak = 0;
+  auto need = [&](int32_t v) { peak = max(peak, v); return v <= n; };
+  if (n >= kMfLimit + 1) {
+    tab.put(lz4_hash_at(in, u16tab), 0);
+    ip = 1;
+    uint32_t fwdh = lz4_hash_at(in + ip, u16tab);
+    for (;;) {
+      int32_t fwd = ip, step = 1, nb = accel << 6;
+      bool found = false;
+      for (;;) {
+        const uint32_t h = fwdh;
+        const int32_t cur = fwd;
+        const int32_t mi = tab.get(h);
+        ip = fwd;
+        fwd += step;
+        step = nb++ >> 6;
+        if (fwd > mflimit1) break;
+        match = mi;
+        fwdh = lz4_hash_at(in + fwd, u16tab);
+        tab.put(h, cur);
+        if (!u16tab && mi + kDMax < cur) continue;
+        if (ldu32(in + match) == ldu32(in + ip)) { found = true; break; }
+      }
+      if (!found) break;
+      while (ip > anchor && match > 0 && in[ip - 1] == in[match - 1]) { ip--; match--; }
+      int32_t token = op++;
+      {
+        const int32_t lit = ip - anchor;
+        if (!need(op + lit + (2 + 1 + kLastLit) + lit / 255)) { *peak_out = peak; return 0; }
+        if (lit >= kRunMask) {
+          int32_t len = lit - kRunMask;
+          out[token] = kRunMask << 4;
+          for (; len >= 255; len -= 255) out[op++] = 255;
+          out[op++] = (uint8_t)len;
+        } else {
+          out[token] = (uint8_t)(lit << 4);
+        }
+        for (int32_t i = 0; i < lit; i++) out[op + i] = in[anchor + i];
+        op += lit;
+      }
+      bool done = false;
+      for (;;) {
+        const int32_t d = ip - match;
+        out[op] = (uint8_t)d;
+        out[op + 1] = (uint8_t)(d >> 8);
+        op += 2;
+        int32_t mc = 0;
+        {
+          int32_t a = ip + 4, b = match + 4;
+          while (a + 4 <= matchlimit) {
+            const uint32_t x = ldu32(in + a) ^ ldu32(in + b);
+            if (x) { mc += __builtin_ctz(x) >> 3; goto counted; }
+            a += 4; b += 4; mc += 4;
+          }
+          while (a < matchlimit && in[a] == in[b]) { a++; b++; mc++; }
+        }
+      counted:
+        ip += mc + 4;
+        if (!need(op + (1 + kLastLit) + (mc + 240) / 255)) { *peak_out = peak; return 0; }
+        uint8_t tk = out[token];
+        if (mc >= 15) {
+          tk += 15;
+          mc -= 15;
+          for (; mc >= 255; mc -= 255) out[op++] = 255;
+          out[op++] = (uint8_t)mc;
+        } else {
+          tk += (uint8_t)mc;
+        }
+        out[token] = tk;
+        anchor = ip;
+        if (ip >= mflimit1) { done = true; break; }
+        tab.put(lz4_hash_at(in + ip - 2, u16tab), ip - 2);
+        const uint32_t h = lz4_hash_at(in + ip, u16tab);
+        const int32_t mi = tab.get(h);
+        tab.put(h, ip);
+        if ((u16tab || mi + kDMax >= ip) && ldu32(in + mi) == ldu32(in + ip)) {
+          match = mi;
+          token = op++;
+          out[token] = 0;
+          continue;
+        }
+        break;
+      }
+      if (done) break;
+      fwdh = lz4_hash_at(in + ++ip, u16tab);
+    }
+  }
+  const int32_t last = n - anchor;
+  if (!need(op + last + 1 + (last + 255 - kRunMask) / 255)) { *peak_out = peak; return 0; }
+  if (last >= kRunMask) {
+    int32_t acc = last - kRunMask;
+    out[op++] = kRunMask << 4;
+    for (; acc >= 255; acc -= 255) out[op++] = 255;
+    out[op++] = (uint8_t)acc;
+  } else {
+    out[op++] = (uint8_t)(last << 4);
+  }
+  for (int32_t i = 0; i < last; i++) out[op + i] = in[anchor + i];
+  op += last;
+  *peak_out = peak;
+  return op;
+}
+
+// Is the whole stream one repeated byte? (blosc/blosc2.c:1184-1206), one lane.
+__device__ __forceinline__ bool lane_is_run(gin_t s, int32_t n) {
+  const uint32_t rep = s[0] * 0x01010101u;
+  int32_t i = 0;
+  for (; i + 4 <= n; i += 4) if (ldu32(s + i) != rep) return false;
+  for (; i < n; i++) if (s[i] != (uint8_t)rep) return false;
+  return true;
+}
+
+__global__ __launch_bounds__(64) void k_encode_lz4(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
+                                                   StreamResult* __restrict__ res, int32_t nstreams_total,
+                                                   int32_t* __restrict__ next, uint32_t* __restrict__ tabs,
+                                                   uint32_t* __restrict__ tags) {
+  const int32_t slot = blockIdx.x * 64 + lane_id();
+  Lz4Tab tab;
+  tab.t = (B2H_GLB uint32_t*)(tabs + ((size_t)slot << kLz4TabLog));
+  uint32_t tag = tags[slot];
+  const int accel = 10 - g.clevel;
+  for (;;) {
+    const int32_t s = atomicAdd(next, 1);
+    if (s >= nstreams_total) break;
+    const int32_t c = s / g.nsc, l = s - c * g.nsc;
+    int32_t off, len, blk;
+    stream_locate(g, l, &off, &len, &blk);
+    gin_t in = (gin_t)(filt + (int64_t)c * g.wstride + off);
+    B2H_GLB uint8_t* out = (B2H_GLB uint8_t*)(sbuf + (int64_t)c * g.wstride + off);
+    StreamResult r;
+    r.windows = 0;
+    r.cycles = 0;
+    r.t_start = 0;
+    r.peak = 0;
+    r.size = 0;
+    if (g.overhead == kHdrExt && lane_is_run(in, len)) {
+      r.size = in[0];
+      r.kind = r.size ? kStreamByteRun : kStreamZeroRun;
+    } else {
+      // a fresh tag per stream; on wrap-around the lane clears its table once
+      tag = (tag + 1) & 0xffu;
+      if (tag == 0) {
+        for (int i = 0; i < (1 << kLz4TabLog); i++) tab.t[i] = 0;
+        tag = 1;
+      }
+      tab.tag = tag;
+      int32_t peak = 0;
+      const int32_t cb = lz4_encode_lane(in, len, accel, out, tab, &peak);
+      r.kind = cb > 0 ? kStreamLz : kStreamRaw;
+      r.size = cb;
+      r.peak = peak;
+    }
+    res[s] = r;
+  }
+  tags[slot] = tag;
+}
+
+static int launch_encode_lz4(Workspace* ws, const CGeom& g, const uint8_t* filt, StreamResult* res, int64_t ntot,
+                             int32_t* next, hipStream_t st) {
+  if (std::max(g.neblock, g.leftover) >= kLz4MaxStream) {
+    snprintf(g_err, sizeof g_err, "LZ4 streams of 16 MiB or more are not supported on the device");
+    return E_PARAM;
+  }
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 256;
+  // 8 single-wave workgroups per CU (512 lanes = 16 MiB of tables per CU); lanes pull streams
+  const int64_t waves = std::min<int64_t>((ntot + 63) / 64, (int64_t)std::max(1, ncu) * 8);
+  const size_t lanes = (size_t)waves * 64;
+  const size_t tab_bytes = lanes * (sizeof(uint32_t) << kLz4TabLog);
+  const bool fresh = ws->lz4tab.cap < tab_bytes + lanes * sizeof(uint32_t) + 256;
+  if (ws->lz4tab.ensure(tab_bytes + lanes * sizeof(uint32_t))) return E_MEMORY;
+  uint32_t* tabs = ws->lz4tab.as<uint32_t>();
+  uint32_t* tags = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(ws->lz4tab.p) + tab_bytes);
+  if (fresh || ws->lz4_lanes != lanes) {   // new layout: tables and tags start zeroed (tag 0 = never used)
+    HIPCHK(hipMemsetAsync(ws->lz4tab.p, 0, tab_bytes + lanes * sizeof(uint32_t), st));
+    ws->lz4_lanes = lanes;
+  }
+  k_encode_lz4<<<(uint32_t)waves, 64, 0, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tabs, tags);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 struct Place {
   int32_t off;    // payload offset inside the chunk output (csize word sits at off - 4)
   int32_t csize;  // csize word
@@ -317,7 +537,9 @@ __global__ void k_finalize(CGeom g, const StreamResult* __restrict__ res, Place*
         maxout = destsize - ntbytes;
         if (maxout <= 0) { ok = false; break; }
       }
-      int32_t cb = (sr.kind == kStreamLz && maxout >= 66 && sr.peak <= maxout) ? sr.size : 0;
+      // BloscLZ returns 0 below maxout 66 (blosc/blosclz.c:480-482); LZ4's limited-output checks
+      // are all captured by `peak`
+      int32_t cb = (sr.kind == kStreamLz && (g.compcode == 1 || maxout >= 66) && sr.peak <= maxout) ? sr.size : 0;
       if (cb == 0) cb = nl;
       if (cb == nl && ntbytes + nl > destsize) { ok = false; break; }
       pl[l].off = ntbytes;
@@ -430,8 +652,10 @@ static int32_t split_block(int32_t splitmode, int compcode, const uint8_t* filte
 
 int make_compress_plan(CompressPlan* p, int32_t nbytes, int32_t destsize, int clevel, int32_t typesize,
                        int32_t ctx_blocksize, int32_t splitmode, const uint8_t* filters,
-                       const uint8_t* filters_meta, int32_t* computed_blocksize, bool extended) {
+                       const uint8_t* filters_meta, int32_t* computed_blocksize, bool extended, int compcode) {
   memset(p, 0, sizeof *p);
+  if (compcode != 0 && compcode != 1) return -7;   // BLOSC2_ERROR_CODEC_SUPPORT: BloscLZ and LZ4 only
+  p->compcode = compcode;
   p->overhead = extended ? kHdrExt : kHdrMin;
   if (nbytes > 0x7fffffff - kHdrExt) return E_MAXBUF;
   if (destsize < kHdrExt) return E_MAXBUF;
@@ -483,8 +707,9 @@ int make_compress_plan(CompressPlan* p, int32_t nbytes, int32_t destsize, int cl
       if (filters[i] == kBitshuffle) flags |= kFlagBitshuffle;
       if (filters[i] == kDelta) flags |= kFlagDelta;
     }
-    p->split = split_block(splitmode, 0, filters, ts, bs) != 0;
+    p->split = split_block(splitmode, compcode, filters, ts, bs) != 0;
     if (!p->split) flags |= kFlagDontSplit;
+    flags |= (uint8_t)(compcode << 5);   // compformat (blosc/blosc2.c:2990-2991)
   }
   p->memcpyed = memcpyed;
   int32_t hb = ctx_blocksize > 0 ? ctx_blocksize : bs;
@@ -495,7 +720,7 @@ int make_compress_plan(CompressPlan* p, int32_t nbytes, int32_t destsize, int cl
   h[0] = 5; h[1] = 1; h[2] = flags; h[3] = (uint8_t)ts;
   for (int k = 0; k < 4; k++) { h[4 + k] = (uint8_t)(nbytes >> (8 * k)); h[8 + k] = (uint8_t)(hb >> (8 * k)); }
   for (int i = 0; i < 6; i++) { h[16 + i] = filters[i]; h[24 + i] = filters_meta[i]; }
-  h[22] = 0;   // udcompcode = BLOSCLZ
+  h[22] = (uint8_t)compcode;   // udcompcode = the codec (blosc/blosc2.c:1030)
   return 0;
 }
 
@@ -589,6 +814,7 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
   g.clevel = P.clevel;
   g.destsize = P.destsize;
   g.overhead = P.overhead;
+  g.compcode = P.compcode;
   g.src_stride = src_stride;
   g.dst_stride = dst_stride;
   g.wstride = ((int64_t)n + 255) / 256 * 256 + 256;
@@ -694,7 +920,10 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
   if (rc) return rc;
   int32_t* next = ws->qctr.as<int32_t>();
   HIPCHK(hipMemsetAsync(next, 0, sizeof(int32_t), st));
-  {
+  if (g.compcode == 1) {
+    rc = launch_encode_lz4(ws, g, filt, res, ntot, next, st);
+    if (rc) return rc;
+  } else {
     rc = small ? launch_encode<uint16_t>(ws, g, hashlog, filt, res, ntot, next, st)
                : launch_encode<uint32_t>(ws, g, hashlog, filt, res, ntot, next, st);
     if (rc) return rc;
@@ -950,6 +1179,10 @@ __device__ __forceinline__ void decode_stream(const uint8_t* const* __restrict__
   } else if (st.csize == nb) {
     wave_copy(out, in, nb);
     *kind_out = 2;
+  } else if ((d.flags >> 5) == 1) {   // LZ4 (blosc/blosc2.c:2062-2067)
+    const int32_t got = wave_lz4_decode_ring<RLOG>(in, st.csize, out, nb, ring);
+    if (got != nb && lane == 0) atomicMin(&ch[c].status, E_DATA);
+    *kind_out = 4;
   } else if ((d.flags >> 5) != 0) {
     if (lane == 0) atomicMin(&ch[c].status, E_CODEC);
   } else {

@@ -938,6 +938,96 @@ __device__ __forceinline__ int32_t wave_lz_decode_ring(gin_t in, int32_t length,
   return op;
 }
 
+// ------------------------------------------------------------------------ LZ4 decoder ----
+// Bytes into the ring from global memory (`zero`: zero bytes), 1 KiB per step, flushing ahead.
+template <int RLOG>
+__device__ __noinline__ int32_t ring_put(B2H_LDS uint8_t* ring, gout_t out, int32_t op, gin_t src, int32_t len,
+                                         bool zero, int32_t F) {
+  constexpr int32_t RM = (1 << RLOG) - 1;
+  const int lane = lane_id();
+  for (int32_t done = 0; done < len; done += 1024) {
+    const int32_t n = min(len - done, 1024);
+    F = flush_to<RLOG>(ring, out, op + done + n, F);
+    for (int32_t i = done + lane; i < done + n; i += 64) ring[(op + i) & RM] = zero ? (uint8_t)0 : src[i];
+  }
+  return F;
+}
+
+// LZ4 block decode, compformat 1 (blosc/blosc2.c:500-519 -> LZ4_decompress_safe of lz4 1.9.3;
+// the grammar, bounds and rejections restated in oracle/blosc2_oracle.c or_lz4_decompress).
+// Sequence = token (literal length << 4 | match length - 4, 15 = extension bytes until one != 255),
+// literals, LE16 offset, match; the last sequence is literals only.  Same LDS-ring machinery as
+// the BloscLZ decoder: token bytes by readlane from the register window, literal runs and matches
+// copied by 64 lanes through the ring.  Returns decoded bytes, or -1.
+template <int RLOG>
+__device__ __forceinline__ int32_t wave_lz4_decode_ring(gin_t in, int32_t length, gout_t out, int32_t maxout,
+                                                        B2H_LDS uint8_t* ring) {
+  constexpr int32_t R = 1 << RLOG, RM = R - 1;
+  constexpr int32_t kMfLimit = 12, kLastLit = 5;
+  const int lane = lane_id();
+  if (length <= 0) return -1;
+  if (maxout == 0) return (length == 1 && in[0] == 0) ? 0 : -1;
+  InWin W;
+  inwin_reload(W, in, length, 0);
+  int32_t ip = 0, op = 0, F = 0;
+  asm volatile("" : "+s"(ip), "+s"(W.wpos));
+  for (;;) {
+    if (ip >= length) return -1;
+    const uint32_t token = inwin_byte(W, in, length, ip++);
+    int32_t lit = (int32_t)(token >> 4);
+    if (lit == 15) {
+      uint32_t s;
+      do {
+        if (ip >= length) return -1;
+        s = inwin_byte(W, in, length, ip++);
+        lit += (int32_t)s;
+        if (lit > maxout) return -1;
+      } while (s == 255);
+    }
+    const bool last = op + lit > maxout - kMfLimit || ip + lit > length - (2 + 1 + kLastLit);
+    if (last && (ip + lit != length || op + lit > maxout)) return -1;
+    if (lit > 0) {
+      if (lit <= 64 && op + lit - F <= R) {
+        if (lane < lit) ring[(op + lane) & RM] = in[ip + lane];
+      } else {
+        F = ring_put<RLOG>(ring, out, op, in + ip, lit, false, F);
+      }
+    }
+    op += lit;
+    ip += lit;
+    if (last) break;
+    const int32_t off = (int32_t)(inwin_byte(W, in, length, ip) | (inwin_byte(W, in, length, ip + 1) << 8));
+    ip += 2;
+    if (off > op) return -1;
+    int32_t ml = (int32_t)(token & 15u);
+    if (ml == 15) {
+      uint32_t s;
+      do {
+        if (ip >= length - kLastLit) return -1;
+        s = inwin_byte(W, in, length, ip++);
+        ml += (int32_t)s;
+        if (ml > maxout) return -1;
+      } while (s == 255);
+    }
+    ml += 4;
+    if (op + ml > maxout - kLastLit) return -1;
+    if (off == 0) {   // accepted by liblz4 1.9.3, which writes zeros (see or_lz4_decompress)
+      F = ring_put<RLOG>(ring, out, op, in, ml, true, F);
+    } else {
+      const int32_t src = op - off;
+      if (ml <= 64 && src >= F && op + ml - F <= R) {
+        const int32_t yl = off < ml ? lane % off : lane;
+        if (lane < ml) ring[(op + lane) & RM] = ring[(src + yl) & RM];
+      } else {
+        F = copy_general<RLOG>(ring, out, op, src, ml, off, F);
+      }
+    }
+    op += ml;
+  }
+  ring_flush<RLOG>(ring, out, F, op);
+  return op;
+}
+
 // ------------------------------------------------------------- window-parallel decoder ----
 // Four bytes at (lane-varying) offset q of the 512-byte register window w0|w1 (q <= 504).
 __device__ __forceinline__ uint32_t win_dword(const InWin& W, int32_t q) {

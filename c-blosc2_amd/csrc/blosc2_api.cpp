@@ -167,8 +167,8 @@ int compname_to_code(const char* name) {
 
 // Pipelines the device path executes: built-in filters and BloscLZ.
 int check_supported(const blosc2_context* c) {
-  if (c->compcode != BLOSC_BLOSCLZ) {
-    TRACE_ERROR("codec %d is not implemented by the MI355X engine (BloscLZ only)", c->compcode);
+  if (c->compcode != BLOSC_BLOSCLZ && c->compcode != BLOSC_LZ4) {
+    TRACE_ERROR("codec %d is not implemented by the MI355X engine (BloscLZ and LZ4 only)", c->compcode);
     return BLOSC2_ERROR_CODEC_SUPPORT;
   }
   if (c->use_dict) {
@@ -202,7 +202,7 @@ int compress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void* d
   b2h::CompressPlan plan;
   int32_t computed = 0;
   int rc = b2h::make_compress_plan(&plan, srcsize, destsize, ctx->clevel, ctx->typesize, blocksize_in, ctx->splitmode,
-                                   ctx->filters, ctx->filters_meta, &computed, extended);
+                                   ctx->filters, ctx->filters_meta, &computed, extended, ctx->compcode);
   if (rc < 0) return rc;
   if (sticky) ctx->blocksize = computed;
   if ((rc = check_supported(ctx)) < 0) return rc;
@@ -624,17 +624,22 @@ int blosc2_compcode_to_compname(int compcode, const char** compname) {
     }
   }
   *compname = name;
-  if (compcode == BLOSC_BLOSCLZ) return compcode;
+  if (compcode == BLOSC_BLOSCLZ || compcode == BLOSC_LZ4) return compcode;
   // other built-in codecs exist in the format but are not implemented by this engine
   return name ? (compcode < BLOSC_LAST_CODEC ? -1 : compcode) : -1;
 }
 
 int blosc2_compname_to_compcode(const char* compname) { return compname_to_code(compname); }
 
-const char* blosc2_list_compressors(void) { return BLOSC_BLOSCLZ_COMPNAME; }
+const char* blosc2_list_compressors(void) { return BLOSC_BLOSCLZ_COMPNAME "," BLOSC_LZ4_COMPNAME; }
 
 int blosc2_get_complib_info(const char* compname, char** complib, char** version) {
   const int code = compname_to_code(compname);
+  if (code == BLOSC_LZ4) {   // the LZ4 block format as produced by lz4 1.9.3 (the image's liblz4)
+    if (complib) *complib = strdup(BLOSC_LZ4_LIBNAME);
+    if (version) *version = strdup("1.9.3");
+    return BLOSC_LZ4_LIB;
+  }
   if (code != BLOSC_BLOSCLZ) {
     if (complib) *complib = nullptr;
     if (version) *version = nullptr;
@@ -800,7 +805,7 @@ int b2h_compress_batch(const blosc2_cparams* cp, const void* d_src, int32_t chun
   b2h::CompressPlan plan;
   int32_t computed = 0;
   rc = b2h::make_compress_plan(&plan, chunk_nbytes, dst_capacity, cp->clevel, cp->typesize, cp->blocksize,
-                               cp->splitmode, cp->filters, cp->filters_meta, &computed, true);
+                               cp->splitmode, cp->filters, cp->filters_meta, &computed, true, cp->compcode);
   if (rc < 0) return rc;
   return b2h::compress_batch(plan, static_cast<const uint8_t*>(d_src), src_stride, nchunks,
                              static_cast<uint8_t*>(d_dst), dst_stride, d_cbytes, static_cast<hipStream_t>(stream));
