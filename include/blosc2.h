@@ -4,11 +4,12 @@
  * names, same struct layouts, same argument meaning, same return / error conventions.  Each
  * declaration cites the reference declaration it replaces (c-blosc2 include/blosc2.h:line).
  *
- * What runs where: every built-in filter (SHUFFLE, BITSHUFFLE, DELTA, TRUNC_PREC) and the BloscLZ
- * codec execute as HIP kernels on the GPU; host code only parses/writes headers, stages buffers
- * and keeps context state.  Chunks needing another codec (LZ4, ZLIB, ZSTD, user codecs) or user
- * filters / pre- / postfilters return BLOSC2_ERROR_CODEC_SUPPORT / BLOSC2_ERROR_FILTER_PIPELINE
- * ("Out of scope").
+ * What runs where: every built-in filter (SHUFFLE, BITSHUFFLE, DELTA, TRUNC_PREC), the registered
+ * filters bytedelta (35) and int_trunc (36), and the BloscLZ and LZ4 codecs execute as HIP kernels
+ * on the GPU; host code only parses/writes headers, stages buffers and keeps context state.
+ * Chunks needing another codec (LZ4HC, ZLIB, ZSTD, user codecs) or user filters / pre- /
+ * postfilters return BLOSC2_ERROR_CODEC_SUPPORT / BLOSC2_ERROR_FILTER_PIPELINE (see DESIGN.md,
+ * "Out of scope").
  */
 #ifndef BLOSC2_AMD_BLOSC2_H
 #define BLOSC2_AMD_BLOSC2_H

@@ -177,6 +177,17 @@ def e2e(steps):
             "GiBps_c_plus_d": round(N / GiB / (tcm + tdm), 3)}
 
 
+def lz4t(steps):
+    """T's workload with the LZ4 codec: float32 ts=4 SHUFFLE+LZ4 clevel 5,
+    256 KiB blocks (4 x 64 KiB streams), 4 MiB chunks x 1024."""
+    chunk, nch = 4 << 20, 1024
+    src = gen_f32_device(0, nch * chunk // 4, torch.device("cuda")).view(torch.uint8)
+    kw = dict(clevel=5, typesize=4, filters=(0, 0, 0, 0, 0, B.SHUFFLE), compcode=1)
+    cp = B.cparams(**kw)
+    return _batch_roundtrip("T-LZ4: float32 ts=4 SHUFFLE+LZ4 clevel 5, 256 KiB blocks, 4 MiB x 1024 (gen_f32)",
+                            src, chunk, nch, cp, steps, _oracle_check(src, chunk, (0, 1, 511, 1023), kw))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="C2,C3,C4,E2E")
@@ -184,7 +195,7 @@ def main():
     args = ap.parse_args()
     torch.cuda.set_device(0)
     for name in args.only.split(","):
-        r = {"C2": c2, "C3": c3, "C4": c4, "E2E": e2e}[name](args.steps)
+        r = {"C2": c2, "C3": c3, "C4": c4, "E2E": e2e, "LZ4": lz4t}[name](args.steps)
         print(json.dumps(r), flush=True)
         torch.cuda.empty_cache()
 
