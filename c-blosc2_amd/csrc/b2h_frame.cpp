@@ -13,6 +13,7 @@
 // are materialised with fills.  Frame layout: README_CFRAME_FORMAT.rst.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -304,6 +305,52 @@ int b2h_frame_decompress_chunk(b2h_frame* f, int64_t nchunk, void* dest, int32_t
   if (hipStreamSynchronize(f->stream) != hipSuccess && !rc) rc = BLOSC2_ERROR_FAILURE;
   (void)hipFree(d_out);
   return rc ? rc : need;
+}
+
+// blosc2_schunk_get_slice_buffer (blosc/schunk.c:1662-1760): items [start, stop) of the frame into
+// device memory.  The reference walks the touched chunks one by one (getitem for partial chunks);
+// here the chunks wholly inside the slice decode straight into place and the (at most two) partial
+// edge chunks decode into scratch, all in ONE device batch, then the edges are copied in.
+int b2h_frame_get_slice(b2h_frame* f, int64_t start, int64_t stop, void* d_dst) {
+  if (!f || !d_dst) return BLOSC2_ERROR_NULL_POINTER;
+  const int64_t ts = f->typesize > 0 ? f->typesize : 1;
+  if (start < 0 || stop < start || stop * ts > f->nbytes) return BLOSC2_ERROR_INVALID_PARAM;
+  if (stop == start) return 0;
+  const int64_t b0 = start * ts, b1 = stop * ts, cs = f->chunksize;
+  const int64_t c0 = b0 / cs, c1 = (b1 - 1) / cs;
+  uint8_t* out = static_cast<uint8_t*>(d_dst);
+  uint8_t* scratch = nullptr;
+  if (hipMalloc(&scratch, (size_t)(2 * cs)) != hipSuccess) return BLOSC2_ERROR_MEMORY_ALLOC;
+  std::vector<int64_t> idx;
+  std::vector<uint8_t*> outs;
+  std::vector<int32_t> caps, st;
+  struct Edge { uint8_t* from; uint8_t* to; int64_t n; };
+  std::vector<Edge> edges;
+  int rc = 0;
+  for (int64_t i = c0; i <= c1 && !rc; i++) {
+    const int64_t lo = i * cs, n = chunk_nbytes(f, i);
+    const int64_t a = std::max(b0, lo), b = std::min(b1, lo + n);
+    const bool whole = a == lo && b == lo + n;
+    if (f->offsets[i] < 0) {   // special chunk: fill the touched range directly
+      rc = fill_special(f, f->offsets[i], out + (a - b0), (int32_t)(b - a));
+      continue;
+    }
+    uint8_t* o = whole ? out + (lo - b0) : scratch + (i == c0 ? 0 : cs);
+    if (!whole) edges.push_back({o + (a - lo), out + (a - b0), b - a});
+    idx.push_back(i);
+    outs.push_back(o);
+    caps.push_back((int32_t)n);
+  }
+  if (!rc) rc = decode_chunks(f, idx, outs, caps, &st);
+  for (size_t k = 0; !rc && k < idx.size(); k++)
+    if (st[k] != caps[k]) rc = st[k] < 0 ? st[k] : BLOSC2_ERROR_DATA;
+  for (const Edge& e : edges) {
+    if (rc) break;
+    if (hipMemcpyAsync(e.to, e.from, (size_t)e.n, hipMemcpyDeviceToDevice, f->stream) != hipSuccess) rc = BLOSC2_ERROR_FAILURE;
+  }
+  if (hipStreamSynchronize(f->stream) != hipSuccess && !rc) rc = BLOSC2_ERROR_FAILURE;
+  (void)hipFree(scratch);
+  return rc;
 }
 
 }  // extern "C"

@@ -75,6 +75,11 @@ BLOSC_EXPORT int64_t b2h_frame_decompress(b2h_frame *frame, void *d_dst, int64_t
 /* One chunk into a host buffer: blosc2_schunk_decompress_chunk semantics (returns the chunk's
  * nbytes, BLOSC2_ERROR_WRITE_BUFFER when `nbytes` is too small). */
 BLOSC_EXPORT int b2h_frame_decompress_chunk(b2h_frame *frame, int64_t nchunk, void *dest, int32_t nbytes);
+/* Items [start, stop) (typesize units) of the frame into device memory d_dst: replaces
+ * blosc2_schunk_get_slice_buffer (blosc/schunk.c:1662-1760).  Chunks inside the slice decode in
+ * place, partial edge chunks through scratch, all in one device batch.  Returns 0 or a
+ * BLOSC2_ERROR_* code (INVALID_PARAM for a range outside the frame).  Synchronous. */
+BLOSC_EXPORT int b2h_frame_get_slice(b2h_frame *frame, int64_t start, int64_t stop, void *d_dst);
 
 /* Per-phase HIP-event timings of the last batch on this process (ms): filter, encode, finalize,
  * decode, unfilter.  Enabling adds event records only (no extra synchronisation until read). */

@@ -92,6 +92,7 @@ def L():
     L.b2h_frame_get_info.argtypes, L.b2h_frame_get_info.restype = [vp, C.POINTER(FrameInfo)], C.c_int
     L.b2h_frame_decompress.argtypes, L.b2h_frame_decompress.restype = [vp, vp, C.c_int64], C.c_int64
     L.b2h_frame_decompress_chunk.argtypes, L.b2h_frame_decompress_chunk.restype = [vp, C.c_int64, vp, C.c_int32], C.c_int
+    L.b2h_frame_get_slice.argtypes, L.b2h_frame_get_slice.restype = [vp, C.c_int64, C.c_int64, vp], C.c_int
     return L
 
 
@@ -140,3 +141,31 @@ def test_frame_from_buffer_and_damage(L):
     assert not L.b2h_frame_from_buffer(bad.ctypes.data, bad.nbytes, C.byref(err)) and err.value == -24
     assert not L.b2h_frame_from_buffer(f.ctypes.data, 60, C.byref(err)) and err.value == -5
     assert not L.b2h_frame_open(b"/nonexistent/frame.b2frame", C.byref(err)) and err.value == -15
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", MANIFEST, ids=[c["name"] for c in MANIFEST])
+def test_frame_get_slice(L, case):
+    """b2h_frame_get_slice == blosc2_schunk_get_slice_buffer (blosc/schunk.c:1662-1760): item
+    ranges inside one block, across block and chunk boundaries, whole chunks, the ragged tail."""
+    import torch
+    want = source_data(case)
+    ts = case["cparams"]["typesize"]
+    nitems = case["nbytes"] // ts
+    cs = case["chunksize"] // ts
+    err = C.c_int(0)
+    fr = L.b2h_frame_open(os.path.join(GOLD, case["name"] + ".b2frame").encode(), C.byref(err))
+    assert fr, err.value
+    ranges = [(0, 1), (5, 17), (cs - 3, cs + 9), (cs, 2 * cs), (cs // 2, 3 * cs + 11),
+              (nitems - 7, nitems), (0, nitems), (nitems // 3, nitems // 3)]
+    for a, b in ranges:
+        a, b = max(0, min(a, nitems)), max(0, min(b, nitems))
+        d = torch.full(((b - a) * ts + 64,), 0xEE, dtype=torch.uint8, device="cuda")
+        assert L.b2h_frame_get_slice(fr, a, b, d.data_ptr()) == 0, (a, b)
+        got = d.cpu().numpy()
+        assert np.array_equal(got[:(b - a) * ts], want[a * ts:b * ts]), (a, b)
+        assert (got[(b - a) * ts:] == 0xEE).all(), (a, b)      # nothing written past the slice
+    d = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    assert L.b2h_frame_get_slice(fr, 0, nitems + 1, d.data_ptr()) == -12
+    assert L.b2h_frame_get_slice(fr, 5, 4, d.data_ptr()) == -12
+    L.b2h_frame_free(fr)
