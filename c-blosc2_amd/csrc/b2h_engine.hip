@@ -70,8 +70,7 @@ struct Scratch {
 };
 
 struct Workspace {
-  Scratch t1, t2, work, sbuf, res, place, mode, qctr, gtab, lz4tab;    // compress
-  size_t lz4_lanes = 0;
+  Scratch t1, t2, work, sbuf, res, place, mode, qctr, gtab;    // compress
   Scratch dchunks, dstreams, dblocks, dtotals, stage, stage2, ptrs, dqctr, ddbg;  // decompress
   std::mutex mu;
 };
@@ -273,164 +272,230 @@ __global__ __launch_bounds__(64 * (NLDS + NGLB)) void k_encode(CGeom g, const ui
 
 // ------------------------------------------------------------------------ LZ4 encoder ----
 // LZ4_compress_fast (lz4 1.9.3, noDict, limited output; restated in oracle/blosc2_oracle.c
-// or_lz4_compress) with acceleration 10 - clevel (blosc/blosc2.c:619-629).  LZ4's parse skips
-// ahead by a step that grows with every 64 failed probes and has no window structure to share
-// across a wave, so every LANE owns one stream: 64 streams per wave advance in lockstep through
-// the probe loop, each lane pulling its next stream from the device counter when it finishes.
-// The per-lane hash table (2^13 u32 entries = 32 KiB, global memory, private to the lane) holds
-// `tag << 24 | position`: a stale tag reads as position 0, i.e. the zeroed table LZ4_initStream
-// starts each call with, so no per-stream clearing is needed.
-constexpr int kLz4TabLog = 13;
-constexpr int32_t kLz4MaxStream = 1 << 24;   // positions must fit below the tag
+// or_lz4_compress) with acceleration 10 - clevel (blosc/blosc2.c:619-629), one wave per stream,
+// hash table in LDS (byU16: 2^13 u16 positions; byU32: 2^12 u32 -- 16 KiB either way).
+//
+// LZ4's match search probes positions on a schedule fixed in advance: after probe k the walk
+// steps by 1 (k = 0) or (accel*64 + k - 1) >> 6, whatever the data.  So a WINDOW of 64 consecutive
+// probes is mapped onto the lanes (positions by a prefix sum of the steps): every lane hashes its
+// position and reads its table entry at once.  Serially, probe k reads the table after the
+// inserts of probes < k, so the window is cut before the first lane whose bucket already occurs
+// at an earlier lane (one LDS atomic-or per lane on a bit-per-bucket table); below that cut every
+// lane's entry is exact.  The first lane whose candidate matches ends the search; the inserts of
+// the lanes up to it are committed (distinct buckets: one store each), the rest are dropped.  The
+// sequence after a match (catch-up, literals, offset, match length, the insert at ip - 2 and the
+// immediate re-probe) is wave-uniform scalar logic with 64-lane compares and copies.
 
-__device__ __forceinline__ uint32_t lz4_hash_at(gin_t p, bool u16tab) {
-  const uint32_t lo = ldu32(p);
+__device__ __forceinline__ uint32_t lz4_hash_seq(uint32_t lo, uint32_t hi, bool u16tab) {
   if (u16tab) return (lo * 2654435761u) >> (32 - 13);                           // LZ4_hash4, log 12+1
-  const uint64_t v = (uint64_t)lo | ((uint64_t)ldu32(p + 4) << 32);
+  const uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
   return (uint32_t)(((v << 24) * 889523592379ull) >> (64 - 12));                // LZ4_hash5, log 12
 }
+__device__ __forceinline__ uint32_t lz4_hash_at(gin_t p, bool u16tab) {
+  return lz4_hash_seq(ldu32(p), u16tab ? 0u : ldu32(p + 4), u16tab);
+}
 
-struct Lz4Tab {
-  B2H_GLB uint32_t* t;
-  uint32_t tag;
+template <bool U16>
+struct Lz4Lds {
+  B2H_LDS uint8_t* base;
   __device__ __forceinline__ int32_t get(uint32_t h) const {
-    const uint32_t e = t[h];
-    return (e >> 24) == tag ? (int32_t)(e & 0xffffffu) : 0;
+    if (U16) return ((B2H_LDS uint16_t*)base)[h];
+    return (int32_t)((B2H_LDS uint32_t*)base)[h];
   }
-  __device__ __forceinline__ void put(uint32_t h, int32_t pos) const { t[h] = (tag << 24) | (uint32_t)pos; }
+  __device__ __forceinline__ void put(uint32_t h, int32_t pos) const {
+    if (U16) ((B2H_LDS uint16_t*)base)[h] = (uint16_t)pos;
+    else ((B2H_LDS uint32_t*)base)[h] = (uint32_t)pos;
+  }
 };
+constexpr int32_t kLz4TabBytes = 16384, kLz4BitsBytes = 1024;
 
-// Encode one stream with olimit = n (the stream's own size); returns the encoded size, or 0 when
-// an output check fails (then the stream is stored raw).  *peak = the largest `op + need` tested.
-__device__ int32_t lz4_encode_lane(gin_t in, int32_t n, int accel, B2H_GLB uint8_t* out, const Lz4Tab& tab,
-                                   int32_t* peak_out) {
+// first index i in [0, lim) with in[a + i] != in[b + i], or lim (64 lanes x 1 byte per step)
+__device__ __forceinline__ int32_t wave_common_fwd(gin_t in, int32_t a, int32_t b, int32_t lim) {
+  const int lane = lane_id();
+  for (int32_t x = 0; x < lim; x += 64) {
+    const int32_t i = x + lane;
+    const bool diff = i < lim && in[a + i] != in[b + i];
+    const uint64_t m = __ballot(diff);
+    if (m) return x + __builtin_ctzll(m);
+  }
+  return lim;
+}
+// number of bytes k in [0, lim) with in[a - 1 - i] == in[b - 1 - i] for all i <= k (catch-up)
+__device__ __forceinline__ int32_t wave_common_back(gin_t in, int32_t a, int32_t b, int32_t lim) {
+  const int lane = lane_id();
+  for (int32_t x = 0; x < lim; x += 64) {
+    const int32_t i = x + lane;
+    const bool diff = i < lim && in[a - 1 - i] != in[b - 1 - i];
+    const uint64_t m = __ballot(diff);
+    if (m) return x + __builtin_ctzll(m);
+  }
+  return lim;
+}
+__device__ __forceinline__ void wave_bytes(B2H_GLB uint8_t* o, gin_t s, int32_t n) {
+  for (int32_t i = lane_id(); i < n; i += 64) o[i] = s[i];
+}
+__device__ __forceinline__ void wave_fill255(B2H_GLB uint8_t* o, int32_t n) {
+  for (int32_t i = lane_id(); i < n; i += 64) o[i] = 255;
+}
+
+// Encode one stream with olimit = n (its own size).  Returns the encoded size, or 0 when an output
+// check fails (the stream is then stored raw); *peak = the largest `op + need` tested.
+template <bool U16>
+__device__ int32_t lz4_encode_wave(gin_t in, int32_t n, int accel, B2H_GLB uint8_t* out, Lz4Lds<U16> tab,
+                                   B2H_LDS uint32_t* bits, int32_t* peak_out) {
   constexpr int32_t kMfLimit = 12, kLastLit = 5, kRunMask = 15, kDMax = 65535;
-  const bool u16tab = n < 65536 + 11;
+  const int lane = lane_id();
   const int32_t mflimit1 = n - kMfLimit + 1, matchlimit = n - kLastLit;
-  int32_t ip = 0, anchor = 0, op = 0, match = 0, peak = 0;
+  int32_t anchor = 0, op = 0, peak = 0;
+  bool fail = false;
   auto need = [&](int32_t v) { peak = max(peak, v); return v <= n; };
+  {  // LZ4_initStream: zeroed table
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    B2H_LDS u32x4* t = (B2H_LDS u32x4*)tab.base;
+    for (int i = lane; i < kLz4TabBytes / 16; i += 64) t[i] = u32x4{0, 0, 0, 0};
+    for (int i = lane; i < kLz4BitsBytes / 4; i += 64) bits[i] = 0u;
+  }
   if (n >= kMfLimit + 1) {
-    tab.put(lz4_hash_at(in, u16tab), 0);
-    ip = 1;
-    uint32_t fwdh = lz4_hash_at(in + ip, u16tab);
-    for (;;) {
-      int32_t fwd = ip, step = 1, nb = accel << 6;
-      bool found = false;
+    if (lane == 0) tab.put(lz4_hash_at(in, U16), 0);
+    int32_t ip = 1;
+    for (;;) {   // one match search (step schedule restarts) ... one match sequence
+      // ---- search: windows of 64 probes ----
+      int32_t pos = ip;          // position of the window's first probe
+      int32_t k0 = 0;            // its probe index in this search
+      int32_t match = 0;
+      bool last = false;
       for (;;) {
-        const uint32_t h = fwdh;
-        const int32_t cur = fwd;
-        const int32_t mi = tab.get(h);
-        ip = fwd;
-        fwd += step;
-        step = nb++ >> 6;
-        if (fwd > mflimit1) break;
-        match = mi;
-        fwdh = lz4_hash_at(in + fwd, u16tab);
-        tab.put(h, cur);
-        if (!u16tab && mi + kDMax < cur) continue;
-        if (ldu32(in + match) == ldu32(in + ip)) { found = true; break; }
+        const int32_t k = k0 + lane;
+        const int32_t stp = k == 0 ? 1 : ((accel << 6) + k - 1) >> 6;   // step after probe k
+        const int32_t incl = wave_scan_add(stp);
+        const int32_t p = pos + incl - stp;                              // this lane's probe
+        const bool valid = p + stp <= mflimit1;                          // else: last literals
+        const uint64_t vmask = __ballot(valid);
+        const int32_t E = vmask == ~0ull ? 64 : __builtin_ctzll(~vmask);
+        uint32_t seq = 0, h = 0;
+        if (valid) {
+          seq = ldu32(in + p);
+          h = lz4_hash_seq(seq, U16 ? 0u : ldu32(in + p + 4), U16);
+        }
+        int32_t cand = valid ? tab.get(h) : 0;
+        uint32_t old = 0;
+        if (valid) {
+          old = __hip_atomic_fetch_or(&bits[h >> 5], 1u << (h & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          bits[h >> 5] = 0u;
+        }
+        const uint64_t dup = __ballot(valid && ((old >> (h & 31)) & 1u));
+        const int32_t W = min(E, dup ? __builtin_ctzll(dup) : 64);     // exact lanes: [0, W)
+        bool ok = false;
+        if (lane < W && (U16 || cand + kDMax >= p)) ok = ldu32(in + cand) == seq;
+        const uint64_t om = __ballot(ok);
+        const int32_t f = om ? __builtin_ctzll(om) : W;                  // lanes [0, f] insert
+        if (lane < W && lane <= f) tab.put(h, p);
+        if (om) {
+          ip = __builtin_amdgcn_readlane(p, f);
+          match = __builtin_amdgcn_readlane(cand, f);
+          break;
+        }
+        if (W >= E && E < 64) { last = true; break; }
+        pos = __builtin_amdgcn_readlane(p, W - 1) + __builtin_amdgcn_readlane(stp, W - 1);
+        k0 += W;
       }
-      if (!found) break;
-      while (ip > anchor && match > 0 && in[ip - 1] == in[match - 1]) { ip--; match--; }
+      if (last) break;
+      // ---- catch up ----
+      {
+        const int32_t back = wave_common_back(in, ip, match, min(ip - anchor, match));
+        ip -= back;
+        match -= back;
+      }
       int32_t token = op++;
+      uint32_t tokv;
       {
         const int32_t lit = ip - anchor;
-        if (!need(op + lit + (2 + 1 + kLastLit) + lit / 255)) { *peak_out = peak; return 0; }
+        if (!need(op + lit + (2 + 1 + kLastLit) + lit / 255)) { fail = true; break; }
         if (lit >= kRunMask) {
-          int32_t len = lit - kRunMask;
-          out[token] = kRunMask << 4;
-          for (; len >= 255; len -= 255) out[op++] = 255;
-          out[op++] = (uint8_t)len;
+          const int32_t len = lit - kRunMask;
+          tokv = kRunMask << 4;
+          wave_fill255(out + op, len / 255);
+          op += len / 255;
+          if (lane == 0) out[op] = (uint8_t)(len % 255);
+          op++;
         } else {
-          out[token] = (uint8_t)(lit << 4);
+          tokv = (uint32_t)lit << 4;
         }
-        for (int32_t i = 0; i < lit; i++) out[op + i] = in[anchor + i];
+        wave_bytes(out + op, in + anchor, lit);
         op += lit;
       }
       bool done = false;
-      for (;;) {
+      for (;;) {   // _next_match
         const int32_t d = ip - match;
-        out[op] = (uint8_t)d;
-        out[op + 1] = (uint8_t)(d >> 8);
+        if (lane == 0) { out[op] = (uint8_t)d; out[op + 1] = (uint8_t)(d >> 8); }
         op += 2;
-        int32_t mc = 0;
-        {
-          int32_t a = ip + 4, b = match + 4;
-          while (a + 4 <= matchlimit) {
-            const uint32_t x = ldu32(in + a) ^ ldu32(in + b);
-            if (x) { mc += __builtin_ctz(x) >> 3; goto counted; }
-            a += 4; b += 4; mc += 4;
-          }
-          while (a < matchlimit && in[a] == in[b]) { a++; b++; mc++; }
-        }
-      counted:
+        int32_t mc = wave_common_fwd(in, ip + 4, match + 4, max(0, matchlimit - (ip + 4)));
         ip += mc + 4;
-        if (!need(op + (1 + kLastLit) + (mc + 240) / 255)) { *peak_out = peak; return 0; }
-        uint8_t tk = out[token];
+        if (!need(op + (1 + kLastLit) + (mc + 240) / 255)) { fail = true; break; }
         if (mc >= 15) {
-          tk += 15;
+          tokv += 15;
           mc -= 15;
-          for (; mc >= 255; mc -= 255) out[op++] = 255;
-          out[op++] = (uint8_t)mc;
+          wave_fill255(out + op, mc / 255);
+          op += mc / 255;
+          if (lane == 0) out[op] = (uint8_t)(mc % 255);
+          op++;
         } else {
-          tk += (uint8_t)mc;
+          tokv += (uint32_t)mc;
         }
-        out[token] = tk;
+        if (lane == 0) out[token] = (uint8_t)tokv;
         anchor = ip;
         if (ip >= mflimit1) { done = true; break; }
-        tab.put(lz4_hash_at(in + ip - 2, u16tab), ip - 2);
-        const uint32_t h = lz4_hash_at(in + ip, u16tab);
+        if (lane == 0) tab.put(lz4_hash_at(in + ip - 2, U16), ip - 2);
+        const uint32_t h = lz4_hash_at(in + ip, U16);
         const int32_t mi = tab.get(h);
-        tab.put(h, ip);
-        if ((u16tab || mi + kDMax >= ip) && ldu32(in + mi) == ldu32(in + ip)) {
+        if (lane == 0) tab.put(h, ip);
+        if ((U16 || mi + kDMax >= ip) && ldu32(in + mi) == ldu32(in + ip)) {
           match = mi;
           token = op++;
-          out[token] = 0;
+          tokv = 0;
           continue;
         }
         break;
       }
-      if (done) break;
-      fwdh = lz4_hash_at(in + ++ip, u16tab);
+      if (fail || done) break;
+      ip++;
     }
   }
-  const int32_t last = n - anchor;
-  if (!need(op + last + 1 + (last + 255 - kRunMask) / 255)) { *peak_out = peak; return 0; }
-  if (last >= kRunMask) {
-    int32_t acc = last - kRunMask;
-    out[op++] = kRunMask << 4;
-    for (; acc >= 255; acc -= 255) out[op++] = 255;
-    out[op++] = (uint8_t)acc;
-  } else {
-    out[op++] = (uint8_t)(last << 4);
+  if (!fail) {
+    const int32_t last = n - anchor;
+    if (!need(op + last + 1 + (last + 255 - kRunMask) / 255)) {
+      fail = true;
+    } else {
+      if (last >= kRunMask) {
+        const int32_t acc = last - kRunMask;
+        if (lane == 0) out[op] = kRunMask << 4;
+        op++;
+        wave_fill255(out + op, acc / 255);
+        op += acc / 255;
+        if (lane == 0) out[op] = (uint8_t)(acc % 255);
+        op++;
+      } else {
+        if (lane == 0) out[op] = (uint8_t)(last << 4);
+        op++;
+      }
+      wave_bytes(out + op, in + anchor, last);
+      op += last;
+    }
   }
-  for (int32_t i = 0; i < last; i++) out[op + i] = in[anchor + i];
-  op += last;
   *peak_out = peak;
-  return op;
-}
-
-// Is the whole stream one repeated byte? (blosc/blosc2.c:1184-1206), one lane.
-__device__ __forceinline__ bool lane_is_run(gin_t s, int32_t n) {
-  const uint32_t rep = s[0] * 0x01010101u;
-  int32_t i = 0;
-  for (; i + 4 <= n; i += 4) if (ldu32(s + i) != rep) return false;
-  for (; i < n; i++) if (s[i] != (uint8_t)rep) return false;
-  return true;
+  return fail ? 0 : op;
 }
 
 __global__ __launch_bounds__(64) void k_encode_lz4(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
                                                    StreamResult* __restrict__ res, int32_t nstreams_total,
-                                                   int32_t* __restrict__ next, uint32_t* __restrict__ tabs,
-                                                   uint32_t* __restrict__ tags) {
-  const int32_t slot = blockIdx.x * 64 + lane_id();
-  Lz4Tab tab;
-  tab.t = (B2H_GLB uint32_t*)(tabs + ((size_t)slot << kLz4TabLog));
-  uint32_t tag = tags[slot];
+                                                   int32_t* __restrict__ next) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  B2H_LDS uint8_t* lds = (B2H_LDS uint8_t*)smem;
+  B2H_LDS uint32_t* bits = (B2H_LDS uint32_t*)(lds + kLz4TabBytes);
   const int accel = 10 - g.clevel;
   for (;;) {
-    const int32_t s = atomicAdd(next, 1);
-    if (s >= nstreams_total) break;
+    const int32_t s = __builtin_amdgcn_readfirstlane(atomicAdd(next, lane_id() == 0 ? 1 : 0));
+    if (s >= nstreams_total) return;
     const int32_t c = s / g.nsc, l = s - c * g.nsc;
     int32_t off, len, blk;
     stream_locate(g, l, &off, &len, &blk);
@@ -442,50 +507,39 @@ __global__ __launch_bounds__(64) void k_encode_lz4(CGeom g, const uint8_t* __res
     r.t_start = 0;
     r.peak = 0;
     r.size = 0;
-    if (g.overhead == kHdrExt && lane_is_run(in, len)) {
+    if (g.overhead == kHdrExt && wave_is_run(in, len)) {
       r.size = in[0];
       r.kind = r.size ? kStreamByteRun : kStreamZeroRun;
     } else {
-      // a fresh tag per stream; on wrap-around the lane clears its table once
-      tag = (tag + 1) & 0xffu;
-      if (tag == 0) {
-        for (int i = 0; i < (1 << kLz4TabLog); i++) tab.t[i] = 0;
-        tag = 1;
-      }
-      tab.tag = tag;
       int32_t peak = 0;
-      const int32_t cb = lz4_encode_lane(in, len, accel, out, tab, &peak);
+      int32_t cb;
+      if (len < 65536 + 11) {
+        Lz4Lds<true> t{lds};
+        cb = lz4_encode_wave<true>(in, len, accel, out, t, bits, &peak);
+      } else {
+        Lz4Lds<false> t{lds};
+        cb = lz4_encode_wave<false>(in, len, accel, out, t, bits, &peak);
+      }
       r.kind = cb > 0 ? kStreamLz : kStreamRaw;
       r.size = cb;
       r.peak = peak;
     }
-    res[s] = r;
+    if (lane_id() == 0) res[s] = r;
   }
-  tags[slot] = tag;
 }
 
 static int launch_encode_lz4(Workspace* ws, const CGeom& g, const uint8_t* filt, StreamResult* res, int64_t ntot,
                              int32_t* next, hipStream_t st) {
-  if (std::max(g.neblock, g.leftover) >= kLz4MaxStream) {
-    snprintf(g_err, sizeof g_err, "LZ4 streams of 16 MiB or more are not supported on the device");
-    return E_PARAM;
-  }
-  int dev = 0, ncu = 0;
+  (void)ws;
+  const size_t lds = kLz4TabBytes + kLz4BitsBytes;
+  int dev = 0, ncu = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 256;
-  // 8 single-wave workgroups per CU (512 lanes = 16 MiB of tables per CU); lanes pull streams
-  const int64_t waves = std::min<int64_t>((ntot + 63) / 64, (int64_t)std::max(1, ncu) * 8);
-  const size_t lanes = (size_t)waves * 64;
-  const size_t tab_bytes = lanes * (sizeof(uint32_t) << kLz4TabLog);
-  const bool fresh = ws->lz4tab.cap < tab_bytes + lanes * sizeof(uint32_t) + 256;
-  if (ws->lz4tab.ensure(tab_bytes + lanes * sizeof(uint32_t))) return E_MEMORY;
-  uint32_t* tabs = ws->lz4tab.as<uint32_t>();
-  uint32_t* tags = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(ws->lz4tab.p) + tab_bytes);
-  if (fresh || ws->lz4_lanes != lanes) {   // new layout: tables and tags start zeroed (tag 0 = never used)
-    HIPCHK(hipMemsetAsync(ws->lz4tab.p, 0, tab_bytes + lanes * sizeof(uint32_t), st));
-    ws->lz4_lanes = lanes;
-  }
-  k_encode_lz4<<<(uint32_t)waves, 64, 0, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tabs, tags);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_encode_lz4), 64, lds) !=
+      hipSuccess) per_cu = 1;
+  const int64_t slots = (int64_t)std::max(1, per_cu) * std::max(1, ncu);
+  const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(ntot, slots));
+  k_encode_lz4<<<grid, 64, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next);
   HIPCHK(hipGetLastError());
   return 0;
 }
