@@ -421,7 +421,8 @@ __device__ int32_t lz4_encode_wave(gin_t in, int32_t n, int accel, B2H_GLB uint8
         } else {
           tokv = (uint32_t)lit << 4;
         }
-        wave_bytes(out + op, in + anchor, lit);
+        if (lit > 64) wave_copy(out + op, in + anchor, lit);
+        else wave_bytes(out + op, in + anchor, lit);
         op += lit;
       }
       bool done = false;
@@ -478,7 +479,8 @@ __device__ int32_t lz4_encode_wave(gin_t in, int32_t n, int accel, B2H_GLB uint8
         if (lane == 0) out[op] = (uint8_t)(last << 4);
         op++;
       }
-      wave_bytes(out + op, in + anchor, last);
+      if (last > 64) wave_copy(out + op, in + anchor, last);
+      else wave_bytes(out + op, in + anchor, last);
       op += last;
     }
   }
