@@ -669,7 +669,11 @@ __global__ __launch_bounds__(kBlockThreads) void k_scatter(CGeom g, const Place*
   }
   if (pl.csize <= 0) return;
   const uint8_t* src = (pl.csize == len) ? filt + (int64_t)c * g.wstride + off : sbuf + (int64_t)c * g.wstride + off;
-  wg_copy(d + pl.off, src, pl.csize);
+  // each wave moves a contiguous quarter with 16-byte aligned stores (wave_copy)
+  const int32_t nw = kBlockThreads / 64, w = threadIdx.x >> 6;
+  const int32_t q = ((pl.csize + nw - 1) / nw + 15) & ~15;
+  const int32_t a = min(pl.csize, w * q), b = min(pl.csize, a + q);
+  if (b > a) wave_copy((gout_t)(d + pl.off + a), (gin_t)(src + a), b - a);
 }
 
 // memcpyed chunks: header + raw bytes.  `only_mode1`: fallback chunks only (mode[] == 1).
