@@ -207,6 +207,7 @@ struct LzPassOut {
   int32_t pos;     // final parse position (probe ratio numerator)
   int32_t peak;
   bool fail;
+  bool early;      // probe stopped once its ratio could no longer reach the threshold
   int32_t windows;
 };
 
@@ -273,7 +274,14 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
   bool fail = false;
   EPROF_DECL;
 
+  // probe early exit: the final ratio is pos / o with pos <= limit + 2 and o never decreasing in
+  // the probe, so once (limit + 64) / o < threshold (with margin) the stream is incompressible
+  // whatever the rest of the probe finds (blosc/blosclz.c:463-468 decides on that ratio alone)
+  const double thr_o = PROBE ? 0.999 * (clevel == 1 ? 2.0 : clevel == 2 ? 1.5 : clevel <= 6 ? 1.2
+                                        : clevel == 7 ? 1.15 : clevel == 8 ? 1.1 : 1.0) : 0.0;
+  bool early = false;
   while (pos < loop_end) {
+    if (PROBE && (double)(limit + 64) < thr_o * (double)o) { early = true; break; }
     windows++;
     if (!PROBE && o - F >= 1024) flush(F + 512);   // a window emits < 512 bytes
     EPROF_T(t0);
@@ -592,6 +600,7 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
   r.pos = pos;
   r.peak = peak;
   r.fail = fail;
+  r.early = early;
   r.windows = windows;
   return r;
 }
@@ -645,7 +654,7 @@ __device__ __forceinline__ StreamResult encode_stream(gin_t in, int32_t n, int c
   const double ratio = (double)pr.pos / (double)pr.o;
   // cratio_ thresholds of blosc/blosclz.c:465 (compared in double, as the reference does)
   const double thr = clevel == 1 ? 2.0 : clevel == 2 ? 1.5 : clevel <= 6 ? 1.2 : clevel == 7 ? 1.15 : clevel == 8 ? 1.1 : 1.0;
-  if (ratio < thr || n < 16 || n < 66) return res;
+  if (pr.early || ratio < thr || n < 16 || n < 66) return res;
   const LzPassOut em = lz_pass<false, TAB>(in, n, hashlog, clevel, out, n, htab, dbits, oring);
   res.windows += em.windows;
   if (em.fail) return res;
