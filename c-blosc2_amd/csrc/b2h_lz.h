@@ -208,6 +208,7 @@ struct LzPassOut {
   int32_t peak;
   bool fail;
   bool early;      // probe stopped once its ratio could no longer reach the threshold
+  bool sure;       // probe stopped once its ratio could no longer fall below the threshold
   int32_t windows;
 };
 
@@ -279,9 +280,19 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
   // whatever the rest of the probe finds (blosc/blosclz.c:463-468 decides on that ratio alone)
   const double thr_o = PROBE ? 0.999 * (clevel == 1 ? 2.0 : clevel == 2 ? 1.5 : clevel <= 6 ? 1.2
                                         : clevel == 7 ? 1.15 : clevel == 8 ? 1.1 : 1.0) : 0.0;
-  bool early = false;
+  bool early = false, sure = false;
+  // and the converse: the probe ends at pos >= loop_end, and the R positions left add at most
+  // R + R/32 + 1 to o as literals (LITERAL2 of blosclz.c), less as matches (a match of len >= 4
+  // consumes len + 2 positions for at most 5 + (len - 7)/255 + 1 bytes) except one final match
+  // running past loop_end (at most 7 + (R + 12)/255): so once loop_end / (o + R + R/16 + 16) >=
+  // threshold the stream is compressed whatever the rest of the probe finds
+  const double thr_s = thr_o * (1.001 / 0.999);
   while (pos < loop_end) {
-    if (PROBE && (double)(limit + 64) < thr_o * (double)o) { early = true; break; }
+    if (PROBE) {
+      if ((double)(limit + 64) < thr_o * (double)o) { early = true; break; }
+      const int32_t R = loop_end - pos;
+      if ((double)loop_end >= thr_s * (double)(o + R + R / 16 + 16)) { sure = true; break; }
+    }
     windows++;
     if (!PROBE && o - F >= 1024) flush(F + 512);   // a window emits < 512 bytes
     EPROF_T(t0);
@@ -601,6 +612,7 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
   r.peak = peak;
   r.fail = fail;
   r.early = early;
+  r.sure = sure;
   r.windows = windows;
   return r;
 }
@@ -654,7 +666,7 @@ __device__ __forceinline__ StreamResult encode_stream(gin_t in, int32_t n, int c
   const double ratio = (double)pr.pos / (double)pr.o;
   // cratio_ thresholds of blosc/blosclz.c:465 (compared in double, as the reference does)
   const double thr = clevel == 1 ? 2.0 : clevel == 2 ? 1.5 : clevel <= 6 ? 1.2 : clevel == 7 ? 1.15 : clevel == 8 ? 1.1 : 1.0;
-  if (pr.early || ratio < thr || n < 16 || n < 66) return res;
+  if (pr.early || (!pr.sure && ratio < thr) || n < 16 || n < 66) return res;
   const LzPassOut em = lz_pass<false, TAB>(in, n, hashlog, clevel, out, n, htab, dbits, oring);
   res.windows += em.windows;
   if (em.fail) return res;

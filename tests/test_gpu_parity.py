@@ -361,3 +361,26 @@ def test_plugin_filter_errors(B):
                dict(typesize=4, filters=(0, 0, 0, 0, 1, 35), filters_meta=(0,) * 6)):   # meta 0, no schunk
         s = src[:49_998] if kw["typesize"] == 3 else src
         assert B.compress(s, clevel=5, **kw) == -18, kw
+
+
+def _tunable(seed, n, q):
+    """Random bytes where a fraction q of 16-byte groups repeat the group 64 bytes earlier: the
+    entropy probe's ratio sweeps across the clevel thresholds (blosc/blosclz.c:463-468) as q varies."""
+    rng = np.random.default_rng(seed)
+    a = rng.integers(0, 256, n, dtype=np.uint8)
+    for g in np.nonzero(rng.random(n // 16) < q)[0]:
+        if g >= 4:
+            a[16 * g:16 * g + 16] = a[16 * (g - 4):16 * (g - 4) + 16]
+    return a
+
+
+@pytest.mark.parametrize("clevel", [1, 2, 3, 5, 7, 8, 9])
+def test_probe_threshold_sweep(B, clevel):
+    """Streams whose probe ratio lands on either side of the threshold: the device's exact early
+    decisions of the probe (early reject / early accept) give the oracle's chunks."""
+    for i, q in enumerate(np.linspace(0.0, 0.9, 19)):
+        src = _tunable(clevel * 100 + i, 4 * 65536 + 999, float(q))
+        kw = dict(clevel=clevel, typesize=1, filters=(0, 0, 0, 0, 0, 0), blocksize=65536, splitmode=2)
+        want = oracle_compress(src, **kw)
+        got = B.compress(src, **kw)
+        assert isinstance(got, np.ndarray) and np.array_equal(got, want), (clevel, q)
