@@ -12,6 +12,7 @@ and RCCL-scatters the shards over xGMI (timed separately, excluded from `value`)
 import argparse
 import ctypes as C
 import json
+import re
 import os
 import sys
 import time
@@ -134,7 +135,9 @@ def pmc_traffic(kernel, workload):
     rocprofv3 passes over this same bench command); (None, None) when there is none."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), key=os.path.getmtime):
+    def version(f):   # r1_v8_pmc_traffic.json -> (1, 8): newest round/version wins (mtimes do not survive a checkout)
+        return tuple(int(x) for x in re.findall(r"\d+", os.path.basename(f).split("_pmc")[0]))
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), key=version):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):

@@ -373,41 +373,83 @@ __device__ void block_delta_decode_rest(const uint8_t* __restrict__ s, const uin
 }
 
 // Decoder for block 0: running XOR over w-byte words = inclusive XOR-scan (blosc/delta.c:96-161).
-// Each thread scans a contiguous run of 16-byte pieces, the run totals are XOR-scanned through
-// LDS, then each run is re-walked with its carry.  Scalar word path when unaligned.
+// Coalesced tiles: each pass the workgroup reads kDeltaScanU x blockDim 16-byte pieces (piece
+// u * blockDim + tid of the tile, so every load instruction is contiguous across the wave), scans
+// each piece's words in registers, XOR-scans the piece totals across the wave with shuffles and
+// across waves through LDS (one barrier per tile: the wave totals are double-buffered), and adds
+// the carry of all earlier tiles.  XOR of words replicated over a u64 (xor_last_word64) is
+// linear, so carries combine by plain XOR.  Scalar word path when unaligned.
+constexpr int kDeltaScanU = 4;
+
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t x, int d) {
+  const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)x, d), hi = (uint32_t)__shfl_up((int)(uint32_t)(x >> 32), d);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ void delta_scan_tiles(const uint8_t* __restrict__ s, uint8_t* __restrict__ d, int32_t n16, int w) {
+  constexpr int U = kDeltaScanU;
+  __shared__ uint64_t wt[2][U][kBlockThreads / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
+  const int32_t T = blockDim.x;
+  const ulonglong2* s16 = reinterpret_cast<const ulonglong2*>(s);
+  ulonglong2* d16 = reinterpret_cast<ulonglong2*>(d);
+  uint64_t carry = 0;   // XOR of every word before this tile, replicated over the u64
+  int buf = 0;
+  for (int32_t base = 0; base < n16; base += U * T, buf ^= 1) {
+    ulonglong2 v[U];
+    uint64_t t[U], x[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int32_t i = base + u * T + (int32_t)threadIdx.x;
+      v[u] = i < n16 ? s16[i] : make_ulonglong2(0ull, 0ull);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      v[u].x = xor_prefix64(v[u].x, w);
+      v[u].y = xor_prefix64(v[u].y, w) ^ xor_last_word64(v[u].x, w);
+      t[u] = xor_last_word64(v[u].y, w);   // the piece's XOR, replicated
+      x[u] = t[u];
+    }
+#pragma unroll
+    for (int dd = 1; dd < 64; dd <<= 1) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t y = shfl_up64(x[u], dd);
+        if (lane >= dd) x[u] ^= y;
+      }
+    }
+    if (lane == 63) {
+#pragma unroll
+      for (int u = 0; u < U; u++) wt[buf][u][wv] = x[u];
+    }
+    __syncthreads();
+    uint64_t c = carry;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      uint64_t before = 0, all = 0;
+      for (int i = 0; i < nw; i++) {
+        const uint64_t tt = wt[buf][u][i];
+        before ^= i < wv ? tt : 0ull;
+        all ^= tt;
+      }
+      const uint64_t ex = c ^ before ^ x[u] ^ t[u];   // everything before this piece
+      const int32_t i = base + u * T + (int32_t)threadIdx.x;
+      if (i < n16) d16[i] = make_ulonglong2(v[u].x ^ ex, v[u].y ^ ex);
+      c ^= all;
+    }
+    carry = c;
+  }
+  __syncthreads();   // wt is reused by the next call
+}
+
 __device__ void block_delta_decode_first(const uint8_t* __restrict__ s, uint8_t* __restrict__ d, int32_t bsize,
                                          int32_t ts) {
   __shared__ uint64_t carry[kBlockThreads];
   const int w = delta_width(ts);
   const int32_t nb = bsize / w * w;
   if ((nb % 16) == 0 && aligned16(s) && aligned16(d)) {
-    const int32_t n16 = nb / 16;
-    const int32_t per = (n16 + blockDim.x - 1) / blockDim.x;
-    const int32_t lo = min(n16, (int32_t)threadIdx.x * per), hi = min(n16, lo + per);
-    const ulonglong2* s16 = reinterpret_cast<const ulonglong2*>(s);
-    uint64_t run = 0;
-    for (int32_t i = lo; i < hi; i++) {
-      const ulonglong2 v = s16[i];
-      run = xor_last_word64(xor_prefix64(v.x, w) ^ run, w);
-      run = xor_last_word64(xor_prefix64(v.y, w) ^ run, w);
-    }
-    carry[threadIdx.x] = run;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      uint64_t acc = 0;
-      for (int t = 0; t < (int)blockDim.x; t++) { const uint64_t v = carry[t]; carry[t] = acc; acc ^= v; }
-    }
-    __syncthreads();
-    run = carry[threadIdx.x];
-    for (int32_t i = lo; i < hi; i++) {
-      const ulonglong2 v = s16[i];
-      ulonglong2 o;
-      o.x = xor_prefix64(v.x, w) ^ run;
-      run = xor_last_word64(o.x, w);
-      o.y = xor_prefix64(v.y, w) ^ run;
-      run = xor_last_word64(o.y, w);
-      reinterpret_cast<ulonglong2*>(d)[i] = o;
-    }
+    delta_scan_tiles(s, d, nb / 16, w);
+    for (int32_t i = nb + threadIdx.x; i < bsize; i += blockDim.x) d[i] = s[i];   // past the last word
     __syncthreads();
     return;
   }
