@@ -204,6 +204,32 @@ __global__ __launch_bounds__(kBlockThreads) void k_ffilter(CGeom g, int pass, ui
   }
 }
 
+// Fused forward (DELTA, SHUFFLE) pipeline (exactly these two filters, typesize 2/4/8): one pass
+// over the input, delta in registers, planes stored once.  Blocks that are not whole quads or not
+// 16-byte aligned run the two stages through `tmp` (the first stage's usual buffer) instead.
+__global__ __launch_bounds__(kBlockThreads) void k_ffilter_ds(CGeom g, const uint8_t* __restrict__ raw, int64_t raw_stride,
+                                                              uint8_t* __restrict__ tmp, uint8_t* __restrict__ out,
+                                                              int64_t out_stride) {
+  const int32_t c = blockIdx.y, b = blockIdx.x;
+  if (b >= g.nblocks) return;
+  const int32_t off = b * g.bs;
+  const int32_t bsize = (b == g.nblocks - 1 && g.leftover) ? g.leftover : g.bs;
+  const uint8_t* s = raw + (int64_t)c * raw_stride + off;
+  const uint8_t* dref = raw + (int64_t)c * raw_stride;
+  uint8_t* t = tmp + (int64_t)c * out_stride + off;
+  uint8_t* d = out + (int64_t)c * out_stride + off;
+  if (bsize % (4 * g.ts) == 0 && aligned16(s) && aligned16(d) && aligned16(dref)) {
+    const int32_t n = bsize / g.ts;
+    if (g.ts == 4) delta_shuffle_fast<4>(s, dref, d, n, b == 0);
+    else if (g.ts == 8) delta_shuffle_fast<8>(s, dref, d, n, b == 0);
+    else delta_shuffle_fast<2>(s, dref, d, n, b == 0);
+  } else {
+    block_delta_encode(s, dref, t, bsize, g.ts, b == 0);
+    __syncthreads();
+    block_shuffle(t, d, bsize, g.ts);
+  }
+}
+
 // Persistent encoder: as many workgroups as fit on the chip, every wave pulling stream indices
 // from a device counter until the batch is exhausted.  Stream cost varies ~100x (a float32
 // mantissa plane vs an all-zero exponent plane) and the hardware deals workgroups to XCDs / shader
@@ -938,7 +964,16 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
   bool has_delta = false;
   for (int k = 0; k < nact; k++) has_delta |= P.filters[act[k]] == kDelta;
   const bool two_pass = clobber && has_delta && g.nblocks > 1;
-  for (int pass = two_pass ? 1 : 0; pass <= (two_pass ? 2 : 0); pass++) {
+  const bool fuse_ds = nact == 2 && P.filters[act[0]] == kDelta && P.filters[act[1]] == kShuffle &&
+                       (P.filters_meta[act[1]] == 0 || P.filters_meta[act[1]] == g.ts) &&
+                       (g.ts == 2 || g.ts == 4 || g.ts == 8);
+  if (fuse_ds) {   // output where the two-launch loop leaves it: ring[1], stride wstride
+    dim3 grid(g.nblocks, nchunks);
+    k_ffilter_ds<<<grid, kBlockThreads, 0, st>>>(g, raw, raw_stride, ring[0], ring[1], g.wstride);
+    filt = ring[1];
+    filt_stride = g.wstride;
+  }
+  for (int pass = two_pass ? 1 : 0; pass <= (two_pass ? 2 : 0) && !fuse_ds; pass++) {
     const uint8_t* cur = raw;
     int64_t cur_stride = raw_stride;
     for (int k = 0; k < nact; k++) {
@@ -1274,6 +1309,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RLOG == 12 ?
   }
 }
 
+// filters = (noop x4, DELTA, SHUFFLE) with the shuffle over the chunk's typesize in {2,4,8} and a
+// block of whole quads: decoded by one fused pass (b2h_filters.h, unshuffle_scan/xor_fast).
+__device__ __forceinline__ bool fused_delta_shuffle(const DChunk& d, int32_t bsize) {
+  if (d.filters[5] != kShuffle || d.filters[4] != kDelta || d.fsrc[5] != 0 || d.fdst[4] != 2) return false;
+  for (int i = 0; i < 4; i++) if (!bwd_noop(d.filters[i])) return false;
+  const int32_t ts = d.typesize;
+  if (d.filters_meta[5] != 0 && d.filters_meta[5] != ts) return false;
+  if (ts != 2 && ts != 4 && ts != 8) return false;
+  return bsize % (4 * ts) == 0;
+}
+
 // Backward filter for filter slot `slot`; pass 0: all blocks, 1: block 0 only, 2: blocks >= 1.
 __global__ __launch_bounds__(kBlockThreads) void k_dfilter(DChunk* __restrict__ ch, const DBlock* __restrict__ blocks,
                                                            uint8_t* const* __restrict__ dsts, uint8_t* __restrict__ stage,
@@ -1293,6 +1339,22 @@ __global__ __launch_bounds__(kBlockThreads) void k_dfilter(DChunk* __restrict__ 
   const int32_t bsize = lo ? d.leftover : d.blocksize;
   const int64_t off = (int64_t)bk.block * d.blocksize;
   uint8_t* bufs[3] = {stage + d.stage_off + off, stage2 + d.stage_off + off, dsts[bk.chunk] + off};
+  // (DELTA, SHUFFLE) pipelines: the slot-5 launch unshuffles and un-deltas in one pass (stage ->
+  // dst), the slot-4 launch then has nothing left to do; both launches take the same decision.
+  if (fused_delta_shuffle(d, bsize) && aligned16(bufs[0]) && aligned16(bufs[2]) && aligned16(dsts[bk.chunk])) {
+    if (slot != 5) return;
+    const int32_t ne = bsize / d.typesize;
+    if (bk.block == 0) {
+      if (d.typesize == 4) unshuffle_scan_fast<4>(bufs[0], bufs[2], ne);
+      else if (d.typesize == 8) unshuffle_scan_fast<8>(bufs[0], bufs[2], ne);
+      else unshuffle_scan_fast<2>(bufs[0], bufs[2], ne);
+    } else {
+      if (d.typesize == 4) unshuffle_xor_fast<4>(bufs[0], dsts[bk.chunk], bufs[2], ne);
+      else if (d.typesize == 8) unshuffle_xor_fast<8>(bufs[0], dsts[bk.chunk], bufs[2], ne);
+      else unshuffle_xor_fast<2>(bufs[0], dsts[bk.chunk], bufs[2], ne);
+    }
+    return;
+  }
   const uint8_t* s = bufs[d.fsrc[slot]];
   uint8_t* o = bufs[d.fdst[slot]];
   const uint8_t meta = d.filters_meta[slot];

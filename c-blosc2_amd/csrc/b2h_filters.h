@@ -473,6 +473,194 @@ __device__ void block_delta_decode_first(const uint8_t* __restrict__ s, uint8_t*
   __syncthreads();
 }
 
+// ------------------------------------------------- fused DELTA -> SHUFFLE (one pass per block) ----
+// filters = (..., DELTA, SHUFFLE) with TS in {2,4,8}: the delta word is the element, so delta
+// covers exactly the n * TS shuffled bytes and the (de)shuffle and the XOR run in registers on the
+// same quad (4 elements = 4 * TS bytes), with no intermediate block in HBM.  Same results as the
+// two stages one after the other (blosc/delta.c:18-161, blosc/shuffle-generic.h:34-83).
+
+// Planes -> element-order u32 words of one quad (the byte permutation of store_quad).
+template <int TS>
+__device__ __forceinline__ void planes_to_words(const uint32_t (&p)[TS], uint32_t (&w)[TS]) {
+#pragma unroll
+  for (int k = 0; k < TS; k++) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const int byte = 4 * k + b;
+      o |= byte_of(p[byte % TS], byte / TS) << (8 * b);
+    }
+    w[k] = o;
+  }
+}
+
+template <int TS>
+__device__ __forceinline__ void load_words(const uint8_t* __restrict__ src, int32_t q, uint32_t (&w)[TS]) {
+  load_quad<TS>(src, q, w);
+}
+
+template <int TS>
+__device__ __forceinline__ void store_words(uint8_t* __restrict__ dst, int32_t q, const uint32_t (&w)[TS]) {
+  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + (int64_t)q * 4 * TS);
+  if constexpr (TS % 4 == 0) {
+#pragma unroll
+    for (int k = 0; k < TS / 4; k++) reinterpret_cast<uint4*>(d32)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+  } else {
+    *reinterpret_cast<uint2*>(d32) = make_uint2(w[0], w[1]);
+  }
+}
+
+// Decode, blocks >= 1: dst = unshuffle(src) ^ dref (dref = the chunk's decoded block 0).
+template <int TS>
+__device__ void unshuffle_xor_fast(const uint8_t* __restrict__ src, const uint8_t* __restrict__ dref,
+                                   uint8_t* __restrict__ dst, int32_t n) {
+  const int32_t quads = n / 4, T = blockDim.x;
+  int32_t q = threadIdx.x;
+  for (; q + (kQuadUnroll - 1) * T < quads; q += kQuadUnroll * T) {
+    uint32_t p[kQuadUnroll][TS], r[kQuadUnroll][TS];
+#pragma unroll
+    for (int u = 0; u < kQuadUnroll; u++) {
+      load_planes<TS>(src, q + u * T, n, p[u]);
+      load_words<TS>(dref, q + u * T, r[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kQuadUnroll; u++) {
+      uint32_t w[TS];
+      planes_to_words<TS>(p[u], w);
+#pragma unroll
+      for (int k = 0; k < TS; k++) w[k] ^= r[u][k];
+      store_words<TS>(dst, q + u * T, w);
+    }
+  }
+  for (; q < quads; q += T) {
+    uint32_t p[TS], r[TS], w[TS];
+    load_planes<TS>(src, q, n, p);
+    load_words<TS>(dref, q, r);
+    planes_to_words<TS>(p, w);
+#pragma unroll
+    for (int k = 0; k < TS; k++) w[k] ^= r[k];
+    store_words<TS>(dst, q, w);
+  }
+}
+
+// Decode, block 0: dst = inclusive XOR-scan over elements of unshuffle(src).  The tiles of
+// delta_scan_tiles with a quad (TS / 2 u64 words) as each lane's piece.
+template <int TS>
+__device__ void unshuffle_scan_fast(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t n) {
+  constexpr int U = 2, K = TS / 2;
+  __shared__ uint64_t wt[2][U][kBlockThreads / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
+  const int32_t quads = n / 4, T = blockDim.x;
+  uint64_t carry = 0;
+  int buf = 0;
+  // the next tile's planes are loaded before this tile's scan and barrier (the loads are the
+  // latency this loop would otherwise expose once per tile)
+  uint32_t pn[U][TS];
+  auto load_tile = [&](int32_t base) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int32_t q = base + u * T + (int32_t)threadIdx.x;
+      if (q < quads) {
+        load_planes<TS>(src, q, n, pn[u]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < TS; k++) pn[u][k] = 0u;
+      }
+    }
+  };
+  load_tile(0);
+  for (int32_t base = 0; base < quads; base += U * T, buf ^= 1) {
+    uint64_t x[U][K], t[U], sc[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      uint32_t w[TS];
+      planes_to_words<TS>(pn[u], w);
+#pragma unroll
+      for (int k = 0; k < K; k++) x[u][k] = (uint64_t)w[2 * k] | ((uint64_t)w[2 * k + 1] << 32);
+    }
+    if (base + U * T < quads) load_tile(base + U * T);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      x[u][0] = xor_prefix64(x[u][0], TS);
+#pragma unroll
+      for (int k = 1; k < K; k++) x[u][k] = xor_prefix64(x[u][k], TS) ^ xor_last_word64(x[u][k - 1], TS);
+      t[u] = xor_last_word64(x[u][K - 1], TS);
+      sc[u] = t[u];
+    }
+#pragma unroll
+    for (int dd = 1; dd < 64; dd <<= 1) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t y = shfl_up64(sc[u], dd);
+        if (lane >= dd) sc[u] ^= y;
+      }
+    }
+    if (lane == 63) {
+#pragma unroll
+      for (int u = 0; u < U; u++) wt[buf][u][wv] = sc[u];
+    }
+    __syncthreads();
+    uint64_t c = carry;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      uint64_t before = 0, all = 0;
+      for (int i = 0; i < nw; i++) {
+        const uint64_t tt = wt[buf][u][i];
+        before ^= i < wv ? tt : 0ull;
+        all ^= tt;
+      }
+      const uint64_t ex = c ^ before ^ sc[u] ^ t[u];
+      const int32_t q = base + u * T + (int32_t)threadIdx.x;
+      if (q < quads) {
+        uint32_t w[TS];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+          const uint64_t o = x[u][k] ^ ex;
+          w[2 * k] = (uint32_t)o;
+          w[2 * k + 1] = (uint32_t)(o >> 32);
+        }
+        store_words<TS>(dst, q, w);
+      }
+      c ^= all;
+    }
+    carry = c;
+  }
+  __syncthreads();
+}
+
+// Encode: dst = shuffle(delta(src)); block 0 XORs each element with the previous one, other
+// blocks with the same element of dref (the chunk's block 0 of the pipeline input).
+template <int TS>
+__device__ void delta_shuffle_fast(const uint8_t* __restrict__ src, const uint8_t* __restrict__ dref,
+                                   uint8_t* __restrict__ dst, int32_t n, bool first_block) {
+  const int32_t quads = n / 4, T = blockDim.x;
+  for (int32_t q = threadIdx.x; q < quads; q += T) {
+    uint32_t w[TS], r[TS];
+    load_words<TS>(src, q, w);
+    if (first_block) {
+      // previous element of every element of the quad: the quad shifted up by one element,
+      // the element before the quad (0 for element 0) entering at the bottom
+      uint32_t prev[TS / 4 > 0 ? TS / 4 : 1];
+      constexpr int EW = TS / 4 > 0 ? TS / 4 : 1;   // u32 words per element (TS=2: half a word)
+      if constexpr (TS == 2) {
+        const uint32_t pe = q ? (uint32_t)reinterpret_cast<const uint16_t*>(src)[4 * (int64_t)q - 1] : 0u;
+        r[0] = (w[0] << 16) | pe;
+        r[1] = (w[1] << 16) | (w[0] >> 16);
+      } else {
+#pragma unroll
+        for (int k = 0; k < EW; k++) prev[k] = q ? reinterpret_cast<const uint32_t*>(src)[(int64_t)q * TS - EW + k] : 0u;
+#pragma unroll
+        for (int k = 0; k < TS; k++) r[k] = k < EW ? prev[k] : w[k - EW];
+      }
+    } else {
+      load_words<TS>(dref, q, r);
+    }
+#pragma unroll
+    for (int k = 0; k < TS; k++) w[k] ^= r[k];
+    store_planes<TS>(dst, q, n, w);
+  }
+}
+
 // ---------------------------------------------------------------------------- trunc-prec ----
 // dst = src & ~((1 << zeroed) - 1) per element; returns false on invalid parameters.
 __device__ __forceinline__ bool trunc_zeroed_bits(int8_t prec, int32_t ts, int* zeroed) {

@@ -384,3 +384,31 @@ def test_probe_threshold_sweep(B, clevel):
         want = oracle_compress(src, **kw)
         got = B.compress(src, **kw)
         assert isinstance(got, np.ndarray) and np.array_equal(got, want), (clevel, q)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ts", [2, 4, 8])
+def test_fused_delta_shuffle_vs_oracle(B, ts):
+    """(DELTA, SHUFFLE) pipelines run as one fused pass per block in both directions (k_ffilter_ds,
+    unshuffle_scan/xor_fast); blocks that are not whole quads fall back to the two stages.  Sizes
+    cover whole-quad leftovers, ragged leftovers, one-block chunks and several blocks; the chunks
+    must be byte-identical to the oracle and round-trip."""
+    rng = np.random.default_rng(ts)
+    sizes = [4 * ts, 4 * ts * 1000, 65536, 65536 + 4 * ts * 7, 65536 + ts * 3, 300_000 // ts * ts,
+             (1 << 20) + 4 * ts, (1 << 20) - ts]
+    for n in sizes:
+        for kind in range(3):
+            if kind == 0:
+                src = int64_ramp(int(rng.integers(0, 1 << 40)), -(-n // 8)).view(np.uint8)[:n].copy()
+            elif kind == 1:
+                src = gen_f32(int(rng.integers(0, 1 << 30)), -(-n // 4)).view(np.uint8)[:n].copy()
+            else:
+                src = mixed_bytes(int(rng.integers(0, 1 << 30)), n)
+            for meta in (0, ts):
+                kw = dict(clevel=int(rng.integers(1, 10)), typesize=ts, filters=(0, 0, 0, 0, 3, 1),
+                          filters_meta=(0, 0, 0, 0, 0, meta), blocksize=int(rng.choice([0, 16384, 65536])))
+                want = oracle_compress(src, **kw)
+                got = B.compress(src, **kw)
+                assert isinstance(got, np.ndarray) and np.array_equal(got, want), (n, kind, kw)
+                dec = B.decompress(got, src.nbytes)
+                assert np.array_equal(dec, src), (n, kind, kw)
