@@ -70,7 +70,8 @@ struct Scratch {
 };
 
 struct Workspace {
-  Scratch t1, t2, work, sbuf, res, place, mode, qctr, gtab;    // compress
+  Scratch t1, t2, work, sbuf, res, place, mode, qctr, gtab, porder;    // compress
+  bool porder_init = false;
   Scratch dchunks, dstreams, dblocks, dtotals, stage, stage2, ptrs, dqctr, ddbg;  // decompress
   std::mutex mu;
 };
@@ -155,6 +156,7 @@ static EvPair ev_filter, ev_encode, ev_final, ev_decode, ev_unfilter;
 // ================================================================ compression: geometry ====
 struct CGeom {
   int32_t nbytes, bs, nblocks, leftover, spb, nsc, neblock, ts, destsize, clevel, overhead, compcode;
+  int32_t front;   // encoder pull schedule (pull_to_stream), 0 = stream order
   int64_t src_stride, wstride, dst_stride;
 };
 
@@ -241,17 +243,83 @@ __global__ __launch_bounds__(kBlockThreads) void k_ffilter_ds(CGeom g, const uin
 // global memory (`gtab`, one per wave slot, see GlbTab in b2h_lz.h).  LDS tables cost 32 KiB per
 // wave (4 waves per CU); global tables cost L2/MALL traffic instead.  Dynamic LDS layout:
 // [NLDS tables][per wave: bucket bitset + output ring].
+// Pull index -> stream index.  With the plane costs learned from the previous batch of the same
+// split (k_plane_cost: porder[0] = spb, porder[1] = costliest plane, porder[2..spb] = the others),
+// the costliest plane's full-block streams are pulled `front` at a time per round of
+// front + spb - 1 pulls (one of every other plane per round), so they are all started well before
+// the end of the launch instead of uniformly up to it (T: the smooth plane's streams take ~3.5 ms,
+// 10x the others; started last they left most slots idle for the final milliseconds), while every
+// round still mixes the cheap planes in (grouping planes outright made the cheap, memory-bound
+// probe streams contend with each other: measured slower).  After the costliest plane runs out,
+// the other planes continue round-robin, then the leftover-block streams.  The mapping is a
+// bijection on [0, ntot): scheduling only, outputs do not depend on it.
+__device__ __forceinline__ int32_t pull_to_stream(const CGeom& g, const int32_t* __restrict__ porder, int32_t front,
+                                                  int32_t i, int32_t ntot) {
+  if (porder == nullptr || front <= 0 || g.spb < 2 || g.spb > 16 || porder[0] != g.spb) return i;
+  const int32_t full = g.nblocks - (g.leftover ? 1 : 0);
+  const int32_t P = (ntot / g.nsc) * full;   // streams per plane
+  const int32_t F = P * g.spb;
+  if (i >= F) return (i - F) * g.nsc + full * g.spb;
+  const int32_t no = g.spb - 1, R = front + no;
+  const int32_t Q = P / front;               // rounds of phase 1
+  int32_t plane, item;
+  if (i < Q * R) {
+    const int32_t r = i / R, k = i - r * R;
+    if (k < front) { plane = porder[1]; item = r * front + k; }
+    else { plane = porder[2 + (k - front)]; item = r; }
+  } else {
+    const int32_t j = i - Q * R, left = P - Q * front;
+    if (j < left) { plane = porder[1]; item = Q * front + j; }
+    else { const int32_t jj = j - left; plane = porder[2 + jj % no]; item = Q + jj / no; }
+  }
+  const int32_t c = item / full, b = item - c * full;
+  return c * g.nsc + b * g.spb + plane;
+}
+
+// Per-plane encode cost of a finished batch (sum of the streams' s_memtime cycles) -> the pull
+// order of the next batch with the same split (see pull_to_stream).  Scheduling only: outputs
+// do not depend on it.
+__global__ __launch_bounds__(1024) void k_plane_cost(CGeom g, const StreamResult* __restrict__ res, int32_t ntot,
+                                                     int32_t* __restrict__ porder) {
+  __shared__ unsigned long long sum[16];
+  if (g.spb < 2 || g.spb > 16) {
+    if (threadIdx.x == 0) porder[0] = 0;
+    return;
+  }
+  if (threadIdx.x < 16) sum[threadIdx.x] = 0ull;
+  __syncthreads();
+  const int32_t full = g.nblocks - (g.leftover ? 1 : 0);
+  for (int32_t s = threadIdx.x; s < ntot; s += blockDim.x) {
+    const int32_t l = s % g.nsc;
+    if (l < full * g.spb) atomicAdd(&sum[l % g.spb], (unsigned long long)res[s].cycles);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t ord[16];
+    for (int j = 0; j < g.spb; j++) ord[j] = j;
+    for (int a = 1; a < g.spb; a++) {   // insertion sort, costliest first, ties keep plane order
+      const int32_t v = ord[a];
+      int b = a;
+      while (b > 0 && sum[ord[b - 1]] < sum[v]) { ord[b] = ord[b - 1]; b--; }
+      ord[b] = v;
+    }
+    for (int j = 0; j < g.spb; j++) porder[1 + j] = ord[j];
+    porder[0] = g.spb;
+  }
+}
+
 template <typename TAB>
 __device__ __forceinline__ void encode_loop(const CGeom& g, TAB htab, B2H_LDS uint32_t* dbits, B2H_LDS uint8_t* oring,
                                             const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
                                             StreamResult* __restrict__ res, int32_t nstreams_total,
-                                            int32_t* __restrict__ next) {
+                                            int32_t* __restrict__ next, const int32_t* __restrict__ porder) {
   for (;;) {
     // branch-free grab: every lane takes part (lane 0 adds 1, the others 0), so no divergent
     // region sits between the atomic and the broadcast -- with a lane-0 branch the structurizer
     // let lanes 1..63 run ahead into the next iteration and re-read a stale index.
-    const int32_t s = __builtin_amdgcn_readfirstlane(atomicAdd(next, lane_id() == 0 ? 1 : 0));
-    if (s >= nstreams_total) return;
+    const int32_t i = __builtin_amdgcn_readfirstlane(atomicAdd(next, lane_id() == 0 ? 1 : 0));
+    if (i >= nstreams_total) return;
+    const int32_t s = __builtin_amdgcn_readfirstlane(pull_to_stream(g, porder, g.front, i, nstreams_total));
     const int32_t c = s / g.nsc, l = s - c * g.nsc;
     int32_t off, len, blk;
     stream_locate(g, l, &off, &len, &blk);
@@ -277,7 +345,7 @@ template <typename POS, int NLDS, int NGLB>
 __global__ __launch_bounds__(64 * (NLDS + NGLB)) void k_encode(CGeom g, const uint8_t* __restrict__ filt,
                                                                uint8_t* __restrict__ sbuf, StreamResult* __restrict__ res,
                                                                int32_t nstreams_total, int32_t* __restrict__ next,
-                                                               POS* __restrict__ gtab) {
+                                                               POS* __restrict__ gtab, const int32_t* __restrict__ porder) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -288,11 +356,11 @@ __global__ __launch_bounds__(64 * (NLDS + NGLB)) void k_encode(CGeom g, const ui
   if (NLDS > 0 && w < NLDS) {
     LdsTab<POS> t;
     t.t = (volatile B2H_LDS POS*)(smem + w * tabsz);
-    encode_loop(g, t, dbits, oring, filt, sbuf, res, nstreams_total, next);
+    encode_loop(g, t, dbits, oring, filt, sbuf, res, nstreams_total, next, porder);
   } else if (NGLB > 0) {
     GlbTab<POS> t;
     t.t = (B2H_GLB POS*)(gtab + (((size_t)blockIdx.x * NGLB + (w - NLDS)) << hashlog));
-    encode_loop(g, t, dbits, oring, filt, sbuf, res, nstreams_total, next);
+    encode_loop(g, t, dbits, oring, filt, sbuf, res, nstreams_total, next, porder);
   }
 }
 
@@ -849,7 +917,7 @@ static void enc_mode(int* nlds, int* nglb) {
 
 template <typename POS, int NL, int NG>
 static int launch_encode_shape(Workspace* ws, const CGeom& g, int hashlog, const uint8_t* filt, StreamResult* res,
-                               int64_t ntot, int32_t* next, hipStream_t st) {
+                               int64_t ntot, int32_t* next, const int32_t* porder, hipStream_t st) {
   const void* fn = reinterpret_cast<const void*>(&k_encode<POS, NL, NG>);
   const size_t lds = enc_wg_lds<POS>(hashlog, NL, NG);
   static bool attr_set = false;
@@ -868,22 +936,22 @@ static int launch_encode_shape(Workspace* ws, const CGeom& g, int hashlog, const
     if (ws->gtab.ensure(((size_t)grid * NG << hashlog) * sizeof(POS))) return E_MEMORY;
     gt = ws->gtab.as<POS>();
   }
-  k_encode<POS, NL, NG><<<grid, 64 * (NL + NG), lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, gt);
+  k_encode<POS, NL, NG><<<grid, 64 * (NL + NG), lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, gt, porder);
   HIPCHK(hipGetLastError());
   return 0;
 }
 
 template <typename POS>
 static int launch_encode(Workspace* ws, const CGeom& g, int hashlog, const uint8_t* filt, StreamResult* res,
-                         int64_t ntot, int32_t* next, hipStream_t st) {
+                         int64_t ntot, int32_t* next, const int32_t* porder, hipStream_t st) {
   int nl, ng;
   enc_mode(&nl, &ng);
-  if (nl == 1 && ng == 0) return launch_encode_shape<POS, 1, 0>(ws, g, hashlog, filt, res, ntot, next, st);
-  if (nl == 0) return launch_encode_shape<POS, 0, 1>(ws, g, hashlog, filt, res, ntot, next, st);
-  if (ng == 1) return launch_encode_shape<POS, 1, 1>(ws, g, hashlog, filt, res, ntot, next, st);
-  if (ng == 2) return launch_encode_shape<POS, 1, 2>(ws, g, hashlog, filt, res, ntot, next, st);
-  if (ng == 3) return launch_encode_shape<POS, 1, 3>(ws, g, hashlog, filt, res, ntot, next, st);
-  return launch_encode_shape<POS, 1, 4>(ws, g, hashlog, filt, res, ntot, next, st);
+  if (nl == 1 && ng == 0) return launch_encode_shape<POS, 1, 0>(ws, g, hashlog, filt, res, ntot, next, porder, st);
+  if (nl == 0) return launch_encode_shape<POS, 0, 1>(ws, g, hashlog, filt, res, ntot, next, porder, st);
+  if (ng == 1) return launch_encode_shape<POS, 1, 1>(ws, g, hashlog, filt, res, ntot, next, porder, st);
+  if (ng == 2) return launch_encode_shape<POS, 1, 2>(ws, g, hashlog, filt, res, ntot, next, porder, st);
+  if (ng == 3) return launch_encode_shape<POS, 1, 3>(ws, g, hashlog, filt, res, ntot, next, porder, st);
+  return launch_encode_shape<POS, 1, 4>(ws, g, hashlog, filt, res, ntot, next, porder, st);
 }
 
 int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stride, int32_t nchunks, uint8_t* d_dst,
@@ -1019,9 +1087,18 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
     rc = launch_encode_lz4(ws, g, filt, res, ntot, next, st);
     if (rc) return rc;
   } else {
-    rc = small ? launch_encode<uint16_t>(ws, g, hashlog, filt, res, ntot, next, st)
-               : launch_encode<uint32_t>(ws, g, hashlog, filt, res, ntot, next, st);
+    static const int front = [] { const char* e = getenv("B2H_ENC_FRONT"); return e ? std::max(0, atoi(e)) : 2; }();
+    g.front = front;
+    if (ws->porder.ensure(32 * sizeof(int32_t))) return E_MEMORY;
+    int32_t* porder = ws->porder.as<int32_t>();
+    if (!ws->porder_init) {   // no learned order yet: stream order
+      HIPCHK(hipMemsetAsync(porder, 0, 32 * sizeof(int32_t), st));
+      ws->porder_init = true;
+    }
+    rc = small ? launch_encode<uint16_t>(ws, g, hashlog, filt, res, ntot, next, porder, st)
+               : launch_encode<uint32_t>(ws, g, hashlog, filt, res, ntot, next, porder, st);
     if (rc) return rc;
+    k_plane_cost<<<1, 1024, 0, st>>>(g, res, (int32_t)ntot, porder);
   }
   ev_encode.stop(st);
   HIPCHK(hipGetLastError());

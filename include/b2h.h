@@ -57,7 +57,10 @@ BLOSC_EXPORT int32_t b2h_bitshuffle(int32_t typesize, int32_t nbytes, const void
  * device; b2h_frame_decompress decodes every chunk in one device batch.  Read-only: frames must be
  * contiguous, 64-bit offsets, fixed chunk size, regular blocks, device-pipeline codecs/filters.
  * Errors: NULL + *err = BLOSC2_ERROR_* (FILE_OPEN, FILE_READ, FRAME_TYPE, VERSION_SUPPORT,
- * INVALID_HEADER, DATA, MEMORY_ALLOC). */
+ * INVALID_HEADER, DATA, MEMORY_ALLOC).
+ * Device destinations are written on the frame's own non-blocking HIP stream, and the calls return
+ * after that stream has drained: work that produces a d_dst buffer on another stream must be
+ * finished (or synchronised) before the call. */
 typedef struct b2h_frame b2h_frame;
 typedef struct {
   int64_t nbytes, cbytes, nchunks;

@@ -111,6 +111,7 @@ def test_frame_device_read(L, case):
     assert info.typesize == case["cparams"]["typesize"]
     assert list(info.filters) == list(case["cparams"]["filters"])
     d = torch.full((info.nbytes + 64,), 0xEE, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()   # the frame runs on its own non-blocking stream
     assert L.b2h_frame_decompress(fr, d.data_ptr(), d.numel()) == info.nbytes
     got = d[:info.nbytes].cpu().numpy()
     assert np.array_equal(got, want)
@@ -161,11 +162,13 @@ def test_frame_get_slice(L, case):
     for a, b in ranges:
         a, b = max(0, min(a, nitems)), max(0, min(b, nitems))
         d = torch.full(((b - a) * ts + 64,), 0xEE, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()   # the frame runs on its own non-blocking stream
         assert L.b2h_frame_get_slice(fr, a, b, d.data_ptr()) == 0, (a, b)
         got = d.cpu().numpy()
         assert np.array_equal(got[:(b - a) * ts], want[a * ts:b * ts]), (a, b)
         assert (got[(b - a) * ts:] == 0xEE).all(), (a, b)      # nothing written past the slice
     d = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()   # the frame runs on its own non-blocking stream
     assert L.b2h_frame_get_slice(fr, 0, nitems + 1, d.data_ptr()) == -12
     assert L.b2h_frame_get_slice(fr, 5, 4, d.data_ptr()) == -12
     L.b2h_frame_free(fr)

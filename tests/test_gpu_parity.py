@@ -412,3 +412,19 @@ def test_fused_delta_shuffle_vs_oracle(B, ts):
                 assert isinstance(got, np.ndarray) and np.array_equal(got, want), (n, kind, kw)
                 dec = B.decompress(got, src.nbytes)
                 assert np.array_equal(dec, src), (n, kind, kw)
+
+
+@pytest.mark.gpu
+def test_learned_pull_order_keeps_chunks(B):
+    """The encoder pulls streams plane by plane in the cost order learned from the previous batch
+    of the same split (k_plane_cost -> pull_to_stream).  Scheduling only: a repeated compression
+    (second call runs on the learned order), other splits in between, and ragged leftover blocks
+    must all give the oracle's chunk."""
+    for n, ts in ((4 << 20, 4), (3_000_000, 4), (1 << 20, 8), (777_777 // 2 * 2, 2), (1 << 20, 16),
+                  (4 << 20, 4)):
+        src = gen_f32(n, n // 4).view(np.uint8)[: n // ts * ts].copy() if ts == 4 else mixed_bytes(n, n // ts * ts)
+        kw = dict(clevel=5, typesize=ts, filters=(0, 0, 0, 0, 0, 1), blocksize=65536)
+        want = oracle_compress(src, **kw)
+        for _ in range(2):
+            got = B.compress(src, **kw)
+            assert isinstance(got, np.ndarray) and np.array_equal(got, want), (n, ts)
