@@ -1209,6 +1209,7 @@ struct DTotals {
   int32_t nblocks, nstreams;
   int32_t any_delta, max_filters;
   int32_t slot_mask;   // filter slots with a backward filter in any chunk (bit i = slot i)
+  int32_t any_special; // some chunk is memcpyed / special (k_dspecial has work)
 };
 
 // Single-workgroup exclusive scans (block_base, stream_base, stage_off) + totals.
@@ -1225,6 +1226,7 @@ __global__ __launch_bounds__(1024) void k_dscan(DChunk* __restrict__ ch, int32_t
     bk += ch[i].nblocks;
     st += ch[i].nstreams;
     dl |= ch[i].has_delta ? 0x100 : 0;
+    dl |= (ch[i].nstreams == 0 && ch[i].nbytes != 0) ? 0x200 : 0;   // k_dspecial's chunks
     for (int f = 0; f < 6; f++)
       if (!bwd_noop(ch[i].filters[f])) dl |= 1 << f;
     mf = max(mf, (int32_t)ch[i].nfilters_bwd);
@@ -1240,6 +1242,7 @@ __global__ __launch_bounds__(1024) void k_dscan(DChunk* __restrict__ ch, int32_t
       ra += va; rb += vb; rs += vs; rd |= sdl[t]; rm = max(rm, smf[t]);
     }
     tot->stage_bytes = ra; tot->nblocks = rb; tot->nstreams = rs; tot->any_delta = (rd >> 8) & 1; tot->slot_mask = rd & 0x3f; tot->max_filters = rm;
+    tot->any_special = (rd >> 9) & 1;
   }
   __syncthreads();
   int64_t ra = sb[threadIdx.x];
@@ -1553,7 +1556,7 @@ int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint
     }
     ev_unfilter.stop(st);
   }
-  {
+  if (h.any_special) {
     dim3 grid(64, n);
     k_dspecial<<<grid, 256, 0, st>>>(d_src, d_dst, ch, d_srcsize);
   }
