@@ -1,19 +1,27 @@
 """Headline benchmark: device-resident GiB/s compress+decompress, float32 shuffle+BloscLZ.
 
-Workload (BASELINE.json / SURVEY.md §8d config "T"): float32, typesize 4, filters = SHUFFLE,
-BloscLZ clevel 5, stune blocksize (256 KiB), 4 MiB chunks x 1024 = 4 GiB per GPU, gen_f32 data.
+Workloads (BASELINE.json / SURVEY.md §8d):
+  T   (default) float32, typesize 4, filters = SHUFFLE, BloscLZ clevel 5, stune blocksize
+      (256 KiB), 4 MiB chunks x 1024 = 4 GiB per GPU, gen_f32 data.  Weak scaling: every rank
+      owns 4 GiB (global element offset rank*N); for N > 1 rank 0 builds the whole super-chunk and
+      RCCL-scatters the shards over xGMI (timed apart, excluded from `value`).
+  C5  the C4 super-chunk (10 000 x 1 MiB int64 ramp, DELTA + SHUFFLE + BloscLZ clevel 5) sharded
+      across the ranks in contiguous chunk ranges (strong scaling: the total is fixed).  Rank 0
+      builds it, RCCL-scatters the shards, and after the timed steps gathers the compressed chunks
+      back in chunk order (the schunk_dist gatherv); both transfers are timed apart.
 One step = compress every chunk of the rank's shard with b2h_compress_batch and decompress them
-all again with b2h_decompress_batch; inputs and outputs stay in HBM.  Weak scaling: every rank
-owns 4 GiB (global element offset rank*N); for N > 1 rank 0 builds the whole super-chunk input
-and RCCL-scatters the shards over xGMI (timed separately, excluded from `value`).
+all again with b2h_decompress_batch; inputs and outputs stay in HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload T|C5]
+
+`--gpus N` without torch.distributed.run spawns the N ranks itself (the parent touches no GPU).
 """
 import argparse
 import ctypes as C
 import json
-import re
 import os
+import re
+import socket
 import sys
 import time
 
@@ -24,10 +32,10 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "c-blosc2_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
-import blosc2_amd as B  # noqa: E402
+import blosc2_amd as B  # noqa: E402  (does not load the library: no GPU call at import)
 
-MASK64 = (1 << 64) - 1
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "device-resident GiB/s compress+decompress, f32 shuffle+blosclz, 1/2/4/8 GPU"
 
 
 def _lsr(x, k):
@@ -37,7 +45,8 @@ def _lsr(x, k):
 
 def gen_f32_device(start, count, device):
     """gen_f32 on the GPU: same formula as tests/datagen.py:gen_f32 (device sinf may
-    differ from numpy in the last ulp; the data is synthetic either way)."""
+    differ from numpy in the last ulp; the data is synthetic either way, and the CPU baseline
+    compresses a host copy of exactly these bytes)."""
     out = torch.empty(count, dtype=torch.float32, device=device)
     step = 1 << 26
     c1 = np.int64(np.uint64(0x9E3779B97F4A7C15).view(np.int64))
@@ -56,62 +65,111 @@ def gen_f32_device(start, count, device):
     return out
 
 
-def _cpu_roundtrip(R, raw, nchunks, chunk_nbytes, threads, reps):
-    """Median-of-`reps` compress and decompress seconds of the reference library over `nchunks`
-    chunks of `raw` with blosc2_compress_ctx / blosc2_decompress_ctx (nthreads = threads)."""
-    import oracle_lib
-    out = np.zeros(chunk_nbytes + 64, np.uint8)
-    tc, td = [], []
+# ------------------------------------------------------------------------ CPU baseline ----
+def host_cores():
+    """(P, note): the physical cores this process may use -- the affinity set without SMT
+    siblings, capped by the cgroup CPU quota and by the box's CPU share (OMP_NUM_THREADS, 16
+    per GPU on the pool) -- for the reference's nthreads = P leg (BASELINE.md plan step 2)."""
+    aff = len(os.sched_getaffinity(0))
+    smt = 1
+    try:
+        sib = open("/sys/devices/system/cpu/cpu0/topology/thread_siblings_list").read().strip()
+        smt = sum((int(b) - int(a) + 1) if "-" in part else 1
+                  for part in sib.split(",") for a, b in [part.split("-") if "-" in part else (part, part)])
+    except (OSError, ValueError):
+        pass
+    phys = max(1, aff // max(1, smt))
+    caps = [phys]
+    note = f"{aff} CPUs in the affinity set, {smt} thread(s) per core -> {phys} physical"
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            caps.append(max(1, int(int(q) / int(per))))
+            note += f", cgroup quota {caps[-1]} CPUs"
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        caps.append(int(omp))
+        note += f", CPU share (OMP_NUM_THREADS) {omp}"
+    return min(caps), note
+
+
+def host_isa():
+    """What the reference build dispatches here: shuffle AVX2 (shuffle-avx2.c), bitshuffle AVX2
+    (the oracle/_ref recipe compiles the SSE2 + AVX2 kernels; blosc/shuffle.c picks the best the
+    CPU reports), BloscLZ scalar C."""
+    flags = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("flags"):
+                flags = line
+                break
+    except OSError:
+        pass
+    avx2 = " avx2" in flags
+    return ("shuffle/bitshuffle: AVX2 kernels" if avx2 else "shuffle/bitshuffle: SSE2/generic") + \
+        ", BloscLZ: scalar C (blosclz.c); AVX-512 variants not compiled into the reference build"
+
+
+def _ref_roundtrip(R, raw, chunk, nchunks, cparams, threads, reps, keep=False):
+    """Median-of-`reps` compress / decompress seconds of the reference library over `nchunks`
+    chunks of `raw` (uint8) with blosc2_compress_ctx / blosc2_decompress_ctx at nthreads =
+    threads.  keep: also return the compressed chunks of the last rep."""
+    from b2ctypes import cparams as rcp, dparams as rdp
+    tc, td, outs = [], [], []
+    dec = np.empty(chunk, np.uint8)
     for _ in range(reps):
+        cctx = R.blosc2_create_cctx(rcp(nthreads=threads, **cparams))
+        dctx = R.blosc2_create_dctx(rdp(nthreads=threads))
+        buf = np.empty(chunk + 64, np.uint8)
         outs = []
-        if R is not None:
-            from b2ctypes import cparams as rcp, dparams as rdp
-            cctx = R.blosc2_create_cctx(rcp(clevel=5, typesize=4, nthreads=threads))
-            dctx = R.blosc2_create_dctx(rdp(nthreads=threads))
-            t0 = time.perf_counter()
-            for i in range(nchunks):
-                n = R.blosc2_compress_ctx(cctx, C.c_void_p(raw.ctypes.data + i * chunk_nbytes), chunk_nbytes,
-                                          C.c_void_p(out.ctypes.data), chunk_nbytes + 32)
-                outs.append(out[:n].copy())
-            t1 = time.perf_counter()
-            dec = np.empty(chunk_nbytes, np.uint8)
-            for ch in outs:
-                R.blosc2_decompress_ctx(dctx, C.c_void_p(ch.ctypes.data), ch.nbytes,
-                                        C.c_void_p(dec.ctypes.data), chunk_nbytes)
-            t2 = time.perf_counter()
-            R.blosc2_free_ctx(cctx)
-            R.blosc2_free_ctx(dctx)
-        else:
-            src = raw.view(np.float32)
-            t0 = time.perf_counter()
-            for i in range(nchunks):
-                outs.append(oracle_lib.oracle_compress(src[i * chunk_nbytes // 4:(i + 1) * chunk_nbytes // 4],
-                                                       clevel=5, typesize=4))
-            t1 = time.perf_counter()
-            for ch in outs:
-                oracle_lib.oracle_decompress(ch, chunk_nbytes)
-            t2 = time.perf_counter()
+        t0 = time.perf_counter()
+        for i in range(nchunks):
+            n = R.blosc2_compress_ctx(cctx, C.c_void_p(raw.ctypes.data + i * chunk), chunk,
+                                      C.c_void_p(buf.ctypes.data), chunk + 32)
+            outs.append(buf[:n].copy())
+        t1 = time.perf_counter()
+        for ch in outs:
+            R.blosc2_decompress_ctx(dctx, C.c_void_p(ch.ctypes.data), ch.nbytes, C.c_void_p(dec.ctypes.data), chunk)
+        t2 = time.perf_counter()
+        R.blosc2_free_ctx(cctx)
+        R.blosc2_free_ctx(dctx)
         tc.append(t1 - t0)
         td.append(t2 - t1)
-    return float(np.median(tc)), float(np.median(td))
+    return float(np.median(tc)), float(np.median(td)), (outs if keep else None)
 
 
-def cpu_baseline(nchunks_sample, chunk_nbytes, threads, reps=5):
-    """The reference library (oracle/_ref, built from /root/reference sources) timed on the host
-    cores on a bounded sample of the same workload (median of `reps`), at nthreads = threads
-    (the headline `value`) and at nthreads = 1 on a smaller sample.  Falls back to the oracle
-    port (single thread) if the reference build is absent.  Returns dict for the JSON line."""
-    from datagen import gen_f32
+def cpu_baseline(host_src, chunk, nchunks, cparams, gpu_chunks, reps=5, single_sample=128):
+    """The reference library (oracle/_ref, built from /root/reference sources) on the host cores,
+    over the same bytes the GPU compressed: every chunk at nthreads = P, a `single_sample`-chunk
+    sample at nthreads = 1 whose outputs are byte-compared with the GPU's chunks (`gpu_chunks(i)`
+    -> uint8 array).  Without the reference build: the oracle port, 1 thread."""
     import oracle_lib
     R = oracle_lib.ref()
+    nbytes = nchunks * chunk
+    P, core_note = host_cores()
     if R is None:
-        threads = 1
-    raw = gen_f32(0, nchunks_sample * chunk_nbytes // 4).view(np.uint8)
-    nbytes = nchunks_sample * chunk_nbytes
-    tc, td = _cpu_roundtrip(R, raw, nchunks_sample, chunk_nbytes, threads, reps)
-    n1 = max(1, nchunks_sample // 16)
-    tc1, td1 = _cpu_roundtrip(R, raw, n1, chunk_nbytes, 1, max(1, reps // 2))
-    b1 = n1 * chunk_nbytes
+        src = host_src
+        t0 = time.perf_counter()
+        outs = [oracle_lib.oracle_compress(src[i * chunk:(i + 1) * chunk], **cparams) for i in range(nchunks)]
+        t1 = time.perf_counter()
+        for ch in outs:
+            oracle_lib.oracle_decompress(ch, chunk)
+        t2 = time.perf_counter()
+        same = sum(int(np.array_equal(outs[i], gpu_chunks(i))) for i in range(nchunks))
+        return {"value": round(nbytes / (t2 - t0) / 2 ** 30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+                "sample": f"oracle port, {nchunks} chunks, 1 thread; {same}/{nchunks} chunks byte-identical to the GPU"}
+    tc, td, _ = _ref_roundtrip(R, host_src, chunk, nchunks, cparams, P, reps)
+    # nthreads = 1 on an evenly spaced sample; these chunks are also the byte-exactness check (with
+    # nthreads > 1 the reference appends blocks in completion order, blosc2.c:5031-5045, so only
+    # its serial output is a fixed byte string)
+    n1 = min(nchunks, single_sample)
+    pick = np.linspace(0, nchunks - 1, n1).astype(np.int64)
+    sample = np.concatenate([host_src[i * chunk:(i + 1) * chunk] for i in pick])
+    tc1, td1, outs1 = _ref_roundtrip(R, sample, chunk, n1, cparams, 1, 3, keep=True)
+    same = sum(int(np.array_equal(outs1[k], gpu_chunks(int(i)))) for k, i in enumerate(pick))
+    b1 = n1 * chunk
     cpu = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -120,22 +178,25 @@ def cpu_baseline(nchunks_sample, chunk_nbytes, threads, reps=5):
                 break
     except OSError:
         pass
-    return {"value": round(nbytes / (tc + td) / 2 ** 30, 4), "unit": "GiB/s",
-            "cores": threads, "kind": "reference" if R is not None else "port",
-            "sample": f"{nchunks_sample} x {chunk_nbytes >> 20} MiB gen_f32 chunks (same cparams), median of "
-                      f"{reps}: compress {nbytes / tc / 2**30:.3f} GiB/s + decompress {nbytes / td / 2**30:.3f} GiB/s "
-                      f"at nthreads={threads}; nthreads=1 on {n1} chunks: "
-                      f"{b1 / (tc1 + td1) / 2**30:.3f} GiB/s (c {b1 / tc1 / 2**30:.3f}, d {b1 / td1 / 2**30:.3f}); "
-                      f"host CPU: {cpu}"}
+    return {"value": round(nbytes / (tc + td) / 2 ** 30, 4), "unit": "GiB/s", "cores": P, "kind": "reference",
+            "nthreads1_value": round(b1 / (tc1 + td1) / 2 ** 30, 4),
+            "byte_identical_chunks": f"{same}/{n1}",
+            "sample": f"all {nchunks} x {chunk >> 20} MiB chunks of this run's input (host copy of the device "
+                      f"bytes, same cparams), median of {reps}: compress {nbytes / tc / 2**30:.3f} GiB/s + "
+                      f"decompress {nbytes / td / 2**30:.3f} GiB/s at nthreads={P} ({core_note}); nthreads=1 on "
+                      f"{n1} chunks: {b1 / (tc1 + td1) / 2**30:.3f} GiB/s (c {b1 / tc1 / 2**30:.3f}, "
+                      f"d {b1 / td1 / 2**30:.3f}); {host_isa()}; host CPU: {cpu}; the reference's serial "
+                      f"(nthreads=1) chunks are byte-identical to the GPU's for {same} of the {n1} sampled"}
 
 
 def pmc_traffic(kernel, workload):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary of this workload
     (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from the FETCH_SIZE/WRITE_SIZE
-    rocprofv3 passes over this same bench command); (None, None) when there is none."""
+    rocprofv3 passes over this same bench command); (None, None, None) when there is none."""
     import glob
     best = None
-    def version(f):   # r1_v8_pmc_traffic.json -> (1, 8): newest round/version wins (mtimes do not survive a checkout)
+
+    def version(f):   # r1_v8_pmc_traffic.json -> (1, 8): newest round/version wins
         return tuple(int(x) for x in re.findall(r"\d+", os.path.basename(f).split("_pmc")[0]))
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), key=version):
         try:
@@ -146,22 +207,91 @@ def pmc_traffic(kernel, workload):
             continue
         for k, v in d.get("kernels", {}).items():
             if k.split("<")[0].endswith(kernel) and "hbm_bytes_per_launch" in v:
-                best = (v["hbm_bytes_per_launch"], os.path.basename(f))
-    return best if best else (None, None)
+                best = (v["hbm_bytes_per_launch"], os.path.basename(f), v.get("correction"))
+    return best if best else (None, None, None)
 
 
-def main():
+def copy_peak_gbps(dev, nbytes=2 << 30, reps=10):
+    """Achievable device-copy bandwidth (read + write bytes / time): the faster of torch's D2D
+    copy and the engine's streaming copy kernel (b2h_device_copy, 16 B/lane, 4 loads in flight)."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    st = torch.cuda.current_stream().cuda_stream
+    best = 0.0
+    for fn in (lambda: b.copy_(a), lambda: B.device_copy(b.data_ptr(), a.data_ptr(), nbytes, st)):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        best = max(best, 2 * nbytes / (ms * 1e-3) / 1e9)
+    del a, b
+    torch.cuda.empty_cache()
+    return best
+
+
+# ------------------------------------------------------------------------------ ranks ----
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _spawned(i, n, port, argv):
+    os.environ.update({"RANK": str(i), "LOCAL_RANK": str(i), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    run(parse(argv))
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--chunks", type=int, default=1024)
-    ap.add_argument("--chunk-mib", type=int, default=4)
+    ap.add_argument("--workload", default="T", choices=["T", "C5"])
+    ap.add_argument("--chunks", type=int, default=None, help="chunks per GPU (T) / in the super-chunk (C5)")
+    ap.add_argument("--chunk-mib", type=int, default=None)
     ap.add_argument("--clevel", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-chunks", type=int, default=256)
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU, spawned from a parent that has made no GPU call (never re-exec)
+        import torch.multiprocessing as mp
+        mp.spawn(_spawned, args=(args.gpus, _free_port(), sys.argv[1:]), nprocs=args.gpus, join=True)
+        return
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
+    run(args)
+
+
+class Timer:
+    """HIP events on torch's current stream (the stream every batch call below is issued on)."""
+
+    def __init__(self):
+        self.ev = []
+
+    def mark(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.ev.append(e)
+
+    def spans(self):
+        torch.cuda.synchronize()
+        return [self.ev[i].elapsed_time(self.ev[i + 1]) for i in range(len(self.ev) - 1)]
+
+
+def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -169,31 +299,47 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-
+    import schunk_dist as SD
     L = B.lib()
-    chunk = args.chunk_mib << 20
-    nch = args.chunks
-    shard = nch * chunk
     stream = torch.cuda.current_stream().cuda_stream
 
+    if args.workload == "T":
+        chunk = (args.chunk_mib or 4) << 20
+        nch_total = (args.chunks or 1024) * world
+        kw = dict(clevel=args.clevel, typesize=4, filters=(0, 0, 0, 0, 0, B.SHUFFLE))
+        workload = ("T: float32 ts=4 SHUFFLE+BloscLZ clevel 5, 256 KiB blocks, "
+                    f"{chunk >> 20} MiB chunks x {nch_total // world} per GPU")
+        scaling = "weak"
+    else:
+        chunk = (args.chunk_mib or 1) << 20
+        nch_total = args.chunks or 10000
+        kw = dict(clevel=args.clevel, typesize=8, filters=(0, 0, 0, 0, B.DELTA, B.SHUFFLE))
+        workload = (f"C5: super-chunk of {nch_total} x {chunk >> 20} MiB int64 ramp, DELTA+SHUFFLE+BloscLZ "
+                    f"clevel 5, contiguous chunk ranges over {world} GPU(s)")
+        scaling = "strong"
+    lo, hi = SD.shard_range(nch_total, world, rank)
+    nch = hi - lo
+    shard = nch * chunk
+
     # ---- input: rank-local shard of the super-chunk (RCCL scatter from rank 0 when N > 1)
+    def build(a, b):
+        if args.workload == "T":
+            return gen_f32_device(a * chunk // 4, (b - a) * chunk // 4, dev).view(torch.uint8)
+        return torch.arange(a * chunk // 8, b * chunk // 8, dtype=torch.int64, device=dev).view(torch.uint8)
+
     scatter_s = None
     if world > 1:
-        recv = torch.empty(shard // 4, dtype=torch.float32, device=dev)
-        parts = None
-        if rank == 0:
-            parts = [gen_f32_device(r * (shard // 4), shard // 4, dev) for r in range(world)]
+        full = build(0, nch_total) if rank == 0 else None
         dist.barrier()
         torch.cuda.synchronize()
         t = time.perf_counter()
-        dist.scatter(recv, parts, src=0)
+        src_u8 = SD.scatter_chunks(full, chunk, nch_total, dev)
         torch.cuda.synchronize()
         scatter_s = time.perf_counter() - t
-        del parts
-        src = recv
+        del full
+        torch.cuda.empty_cache()
     else:
-        src = gen_f32_device(0, shard // 4, dev)
-    src_u8 = src.view(torch.uint8)
+        src_u8 = build(0, nch_total)
 
     cap = chunk + 32
     stride = (cap + 255) // 256 * 256
@@ -201,74 +347,118 @@ def main():
     cbytes = torch.zeros(nch, dtype=torch.int32, device=dev)
     out = torch.empty(shard, dtype=torch.uint8, device=dev)
     status = torch.zeros(nch, dtype=torch.int32, device=dev)
-    cp = B.cparams(clevel=args.clevel, typesize=4, filters=(0, 0, 0, 0, 0, B.SHUFFLE))
+    cp = B.cparams(**kw)
 
-    def step():
+    def compress():
         B.compress_batch(cp, src_u8.data_ptr(), chunk, nch, chunk, comp.data_ptr(), stride, cap,
                          cbytes.data_ptr(), stream)
+
+    def decompress():
         B.decompress_batch(comp.data_ptr(), stride, cbytes.data_ptr(), nch, out.data_ptr(), chunk, chunk,
                            status.data_ptr(), stream)
 
-    for _ in range(args.warmup):
-        step()
+    for _ in range(max(1, args.warmup)):    # at least one pass: the check below reads its output
+        compress()
+        decompress()
     torch.cuda.synchronize()
     # correctness of the measured configuration (outside the timed region)
     assert torch.equal(out, src_u8), "round trip mismatch"
     assert bool((status == chunk).all()), "decompress status"
-    total_c = int(cbytes.sum().item())
+    total_c = int(cbytes.to(torch.int64).sum().item())
+    out.zero_()
 
     L.b2h_enable_timing(1)
     enc_ms, dec_ms = [], []
+    tm = Timer()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-        t = B.last_times()          # waits on this step's events only
-        enc_ms.append(t["encode_ms"])
-        dec_ms.append(t["decode_ms"])
+        tm.mark()
+        compress()
+        enc_ms.append(B.last_times()["encode_ms"])   # waits on this call's k_encode events only
+        tm.mark()
+        decompress()
+        dec_ms.append(B.last_times()["decode_ms"])
+    tm.mark()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     L.b2h_enable_timing(0)
+    spans = tm.spans()
+    t_c = float(np.mean(spans[0::2]))
+    t_d = float(np.mean(spans[1::2]))
+    assert torch.equal(out, src_u8), "round trip mismatch (timed steps)"
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
 
+    gather_s = None
+    if args.workload == "C5" and world > 1:   # chunk-ordered collection on rank 0 (gatherv)
+        dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        res = SD.gather_compressed(comp, stride, cbytes, nch_total)
+        torch.cuda.synchronize()
+        gather_s = time.perf_counter() - t
+        tot = torch.tensor([total_c], dtype=torch.int64, device=dev)
+        dist.all_reduce(tot)
+        if rank == 0:
+            frame, offsets = res
+            assert int(offsets[-1].item()) == int(tot.item()) == frame.numel(), "gatherv size"
+
     if rank == 0:
-        n_all = shard * world * args.steps
-        value = n_all / elapsed / 2 ** 30
-        enc = float(np.mean(enc_ms))
-        # dominant kernel: k_encode; algorithmic bytes per launch = N (read) + C (written)
-        alg = shard + total_c
-        achieved = alg / (enc * 1e-3) / 1e9
-        workload = ("T: float32 ts=4 SHUFFLE+BloscLZ clevel 5, 256 KiB blocks, "
-                    f"{args.chunk_mib} MiB chunks x {nch} per GPU")
-        traffic, traffic_src = pmc_traffic("k_encode", workload)
+        n_all = shard * world if args.workload == "T" else nch_total * chunk
+        value = n_all * args.steps / elapsed / 2 ** 30
+        enc, dec = float(np.mean(enc_ms)), float(np.mean(dec_ms))
+        N, Cb = shard, total_c
+        dominant = "k_encode" if enc >= dec else "k_decode"
+        kms = enc if dominant == "k_encode" else dec
+        achieved = (N + Cb) / (kms * 1e-3) / 1e9     # algorithmic bytes of one launch: N + C
+        traffic, traffic_src, traffic_corr = pmc_traffic(dominant, workload)
+        peak_copy = copy_peak_gbps(dev)
+        step_gbps = 2 * (N + Cb) / ((t_c + t_d) * 1e-3) / 1e9
         res = {
-            "metric": "device-resident GiB/s compress+decompress, f32 shuffle+blosclz, 1/2/4/8 GPU",
+            "metric": METRIC,
             "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic gen_f32 (SURVEY §8d), generated on device",
-            "config": {"workload": workload,
-                       "chunks_per_gpu": nch, "chunk_bytes": chunk, "clevel": args.clevel,
-                       "parallelism": f"chunk-sharded x{world}",
-                       "cratio": round(shard / total_c, 4)},
-            "roofline": {"bound": "hbm", "kernel": "k_encode", "achieved": round(achieved, 2),
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u8",
+            "data": ("synthetic gen_f32 (SURVEY §8d), generated on device" if args.workload == "T"
+                     else "synthetic int64 ramp (value = global element index), generated on device"),
+            "config": {"workload": workload, "chunks_per_gpu": nch, "chunk_bytes": chunk, "clevel": args.clevel,
+                       "parallelism": f"chunk-sharded x{world}", "cratio": round(N / Cb, 4)},
+            "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": round(traffic) if traffic else None,
-                         "traffic_source": traffic_src,
-                         "algorithmic_bytes": alg,
-                         "encode_ms": round(enc, 3), "decode_ms": round(float(np.mean(dec_ms)), 3)},
+                         "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
+                         "traffic_correction": traffic_corr,
+                         "algorithmic_bytes": N + Cb,
+                         "encode_ms": round(enc, 3), "decode_ms": round(dec, 3),
+                         "step": {"compress_ms": round(t_c, 3), "decompress_ms": round(t_d, 3),
+                                  "achieved": round(step_gbps, 1),
+                                  "frac": round(step_gbps / HBM_PEAK_GBS, 5),
+                                  "read_frac": round(step_gbps / 2 / HBM_PEAK_GBS, 5),
+                                  "copy_peak": round(peak_copy, 1),
+                                  "frac_of_copy_peak": round(step_gbps / peak_copy, 5),
+                                  "definition": "achieved = 2(N+C)/(t_c+t_d) over HIP events around the "
+                                                "whole compress and decompress calls; read_frac = "
+                                                "(N+C)/(t_c+t_d)/peak (SURVEY §8d); copy_peak = measured "
+                                                "D2D copy read+write GB/s"}},
         }
         if scatter_s is not None:
             res["config"]["rccl_scatter_s"] = round(scatter_s, 4)
+        if gather_s is not None:
+            res["config"]["gatherv_s"] = round(gather_s, 4)
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(args.cpu_sample_chunks, chunk, min(16, os.cpu_count() or 1))
+            host = src_u8.cpu().numpy()
+            host_comp = comp.cpu().numpy()
+            host_cb = cbytes.cpu().numpy()
+            ncpu = nch if args.workload == "T" else min(nch, 1000)
+            res["cpu_baseline"] = cpu_baseline(
+                host, chunk, ncpu, kw, lambda i: host_comp[i * stride:i * stride + int(host_cb[i])],
+                reps=5 if args.workload == "T" else 3)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -76,6 +76,9 @@ def _bind(lib):
         "blosc2_get_version_string": ([], C.c_char_p),
         "b2h_compress_batch": ([C.POINTER(CParams), vp, i32, i32, i64, vp, i64, i32, vp, vp], C.c_int),
         "b2h_decompress_batch": ([vp, i64, vp, i32, vp, i64, i32, vp, vp], C.c_int),
+        "b2h_pack_chunks": ([vp, i64, vp, i32, vp, vp, vp], C.c_int),
+        "b2h_unpack_chunks": ([vp, vp, i32, vp, i64, vp, vp], C.c_int),
+        "b2h_device_copy": ([vp, vp, i64, vp], C.c_int),
         "b2h_shuffle": ([i32, i32, vp, vp, C.c_int, vp], i32),
         "b2h_bitshuffle": ([i32, i32, vp, vp, C.c_int, vp], i32),
         "b2h_enable_timing": ([C.c_int], None),
@@ -168,6 +171,28 @@ def decompress_batch(d_src: int, src_stride: int, d_cbytes: int, nchunks: int, d
                                     C.c_void_p(stream))
     if rc < 0:
         raise RuntimeError(f"b2h_decompress_batch: {rc} {lib().b2h_last_error()}")
+
+
+def pack_chunks(d_src: int, src_stride: int, d_sizes: int, n: int, d_dst: int, d_offsets: int, stream: int = 0):
+    """b2h_pack_chunks: chunk i (d_src + i*src_stride, d_sizes[i] bytes) -> d_dst, offsets[n+1]."""
+    rc = lib().b2h_pack_chunks(C.c_void_p(d_src), src_stride, C.c_void_p(d_sizes), n, C.c_void_p(d_dst),
+                               C.c_void_p(d_offsets), C.c_void_p(stream))
+    if rc < 0:
+        raise RuntimeError(f"b2h_pack_chunks: {rc} {lib().b2h_last_error()}")
+
+
+def unpack_chunks(d_src: int, d_offsets: int, n: int, d_dst: int, dst_stride: int, d_sizes: int, stream: int = 0):
+    """b2h_unpack_chunks: d_src[offsets[i], offsets[i+1]) -> d_dst + i*dst_stride (+ sizes)."""
+    rc = lib().b2h_unpack_chunks(C.c_void_p(d_src), C.c_void_p(d_offsets), n, C.c_void_p(d_dst), dst_stride,
+                                 C.c_void_p(d_sizes), C.c_void_p(stream))
+    if rc < 0:
+        raise RuntimeError(f"b2h_unpack_chunks: {rc} {lib().b2h_last_error()}")
+
+
+def device_copy(d_dst: int, d_src: int, nbytes: int, stream: int = 0):
+    rc = lib().b2h_device_copy(C.c_void_p(d_dst), C.c_void_p(d_src), nbytes, C.c_void_p(stream))
+    if rc < 0:
+        raise RuntimeError(f"b2h_device_copy: {rc} {lib().b2h_last_error()}")
 
 
 def last_times():

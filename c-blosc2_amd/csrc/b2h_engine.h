@@ -7,6 +7,17 @@
 
 namespace b2h {
 
+// Device scratch of one user (the process-wide default of a device, a blosc2 context, a frame).
+// Every batch call is stream-ordered on it: the call waits (hipStreamWaitEvent) for the previous
+// user's last kernel when that ran on another stream, and records an event after its own, so
+// independent contexts on different threads or streams never overwrite each other's plan tables
+// or staging (the reference's contexts are independent, include/blosc2.h:1462-1466).  Scratch is
+// freed by workspace_destroy (blosc2_free_ctx) or release_device_workspaces (blosc2_destroy).
+struct Workspace;
+Workspace* workspace_create();
+void workspace_destroy(Workspace* ws);
+void release_device_workspaces();
+
 // Uniform compression batch: every chunk has `nbytes` bytes and the same cparams, which is what
 // a super-chunk's shared cctx produces (blosc/schunk.c:1459-1477).
 struct CompressPlan {
@@ -37,21 +48,40 @@ int make_compress_plan(CompressPlan* p, int32_t nbytes, int32_t destsize, int cl
 // d_dst + i*dst_stride (capacity plan.destsize), its cbytes (>0, 0 = does not fit) to d_cbytes[i].
 // Asynchronous on `stream`.
 int compress_batch(const CompressPlan& plan, const uint8_t* d_src, int64_t src_stride, int32_t nchunks,
-                   uint8_t* d_dst, int64_t dst_stride, int32_t* d_cbytes, hipStream_t stream);
+                   uint8_t* d_dst, int64_t dst_stride, int32_t* d_cbytes, hipStream_t stream,
+                   Workspace* ws = nullptr);
 
 // Decompress `n` arbitrary chunks (device pointer arrays).  d_status[i] = nbytes or BLOSC2_ERROR_*.
 // `dst_bound` is an upper bound of the sum of decompressed sizes (sizes the staging scratch).
 // d_maskout (optional, only with n == 1): one byte per block, nonzero = skip (blosc2_set_maskout).
-// Synchronises `stream` once (to size the stream table).
+// `src_bound` >= 0: an upper bound of the sum of the chunks' compressed sizes; the block and stream
+// tables are then sized from it (every block has a 4-byte bstart, every stream a 4-byte csize word)
+// and the call never waits on the host (a batch that exceeds the bounds fails per chunk with
+// BLOSC2_ERROR_MEMORY_ALLOC).  src_bound < 0: the tables are sized exactly, which costs one
+// synchronisation of `stream`.
 int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint8_t* const* d_dst,
                      const int32_t* d_dstsize, int32_t n, int64_t dst_bound, int32_t* d_status,
-                     const uint8_t* d_maskout, hipStream_t stream);
+                     const uint8_t* d_maskout, hipStream_t stream, Workspace* ws = nullptr,
+                     int64_t src_bound = -1);
 
 // Strided convenience form: chunk i at d_src + i*src_stride with cbytes d_cbytes[i], output at
 // d_dst + i*dst_stride with capacity dst_cap.
+// with d_cbytes[i] <= src_stride (chunks do not overlap), so this form never synchronises.
 int decompress_batch_strided(const uint8_t* d_src, int64_t src_stride, const int32_t* d_cbytes, int32_t n,
                              uint8_t* d_dst, int64_t dst_stride, int32_t dst_cap, int32_t* d_status,
-                             hipStream_t stream);
+                             hipStream_t stream, Workspace* ws = nullptr);
+
+// Concatenate chunk i (d_src + i*src_stride, d_sizes[i] bytes) into d_dst in chunk order;
+// d_offsets[0..n] = exclusive prefix sum of the sizes (d_offsets[n] = total).  And the inverse:
+// chunk i = d_src[d_offsets[i], d_offsets[i+1]) to d_dst + i*dst_stride, d_sizes[i] = its size.
+// Asynchronous on `stream` (the multi-GPU scheduler's gatherv staging).
+int pack_chunks(const uint8_t* d_src, int64_t src_stride, const int32_t* d_sizes, int32_t n, uint8_t* d_dst,
+                int64_t* d_offsets, hipStream_t stream);
+int unpack_chunks(const uint8_t* d_src, const int64_t* d_offsets, int32_t n, uint8_t* d_dst, int64_t dst_stride,
+                  int32_t* d_sizes, hipStream_t stream);
+
+// Streaming D2D copy (bench.py's measured copy peak).
+int device_copy(uint8_t* d_dst, const uint8_t* d_src, int64_t nbytes, hipStream_t stream);
 
 // Raw filters on device buffers (blosc2_shuffle & co. use these on staged copies).
 int shuffle_dev(int32_t typesize, int32_t nbytes, const uint8_t* d_src, uint8_t* d_dst, bool inverse, hipStream_t s);

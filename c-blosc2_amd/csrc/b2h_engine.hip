@@ -49,8 +49,9 @@ const char* last_error() { return g_err; }
   } while (0)
 
 // ------------------------------------------------------------------------------ workspace ----
-// Grow-only per-device scratch.  Never freed while the process runs; buffers carry 256 B of
-// slack because the LZ kernels read a few bytes past a stream's end (ldu32).
+// Grow-only scratch of one Workspace (see b2h_engine.h), freed with it; buffers carry 256 B of
+// slack because the LZ kernels read a few bytes past a stream's end (ldu32).  A regrow frees the
+// old buffer with hipFree, which waits for the device work still using it.
 struct Scratch {
   void* p = nullptr;
   size_t cap = 0;
@@ -66,6 +67,11 @@ struct Scratch {
     if (poison) (void)hipMemset(p, 0xA5, n);
     return 0;
   }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
   template <typename T> T* as() const { return static_cast<T*>(p); }
 };
 
@@ -74,17 +80,80 @@ struct Workspace {
   bool porder_init = false;
   Scratch dchunks, dstreams, dblocks, dtotals, stage, stage2, ptrs, dqctr, ddbg;  // decompress
   std::mutex mu;
+  hipEvent_t done = nullptr;       // recorded after the last kernel of the latest call
+  hipStream_t last = nullptr;      // the stream that call ran on
+  bool used = false;
+  // Order this call after the previous user's kernels (same stream: already ordered).
+  int acquire(hipStream_t st) {
+    if (used && last != st && done) HIPCHK(hipStreamWaitEvent(st, done, 0));
+    return 0;
+  }
+  void release(hipStream_t st) {
+    if (!done && hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) done = nullptr;
+    if (done) (void)hipEventRecord(done, st);
+    last = st;
+    used = true;
+  }
+  void free_all() {
+    if (used && done) (void)hipEventSynchronize(done);
+    for (Scratch* s : {&t1, &t2, &work, &sbuf, &res, &place, &mode, &qctr, &gtab, &porder, &dchunks, &dstreams,
+                       &dblocks, &dtotals, &stage, &stage2, &ptrs, &dqctr, &ddbg})
+      s->release();
+    if (done) (void)hipEventDestroy(done);
+    done = nullptr;
+    used = false;
+    porder_init = false;
+  }
 };
 
+// The lock + stream ordering of one batch call; the event is recorded on every exit path.
+struct WsUse {
+  Workspace* ws;
+  hipStream_t st;
+  std::lock_guard<std::mutex> lock;
+  int rc;
+  WsUse(Workspace* w, hipStream_t s) : ws(w), st(s), lock(w->mu), rc(w->acquire(s)) {}
+  ~WsUse() { ws->release(st); }
+};
+
+static std::mutex g_ws_mu;
+static std::vector<Workspace*> g_ws_dev;   // process-wide default workspace per device
+
 static Workspace* ws_for_current_device() {
-  static std::mutex m;
-  static std::vector<Workspace*> all;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-  std::lock_guard<std::mutex> g(m);
-  if ((int)all.size() <= dev) all.resize(dev + 1, nullptr);
-  if (!all[dev]) all[dev] = new Workspace();
-  return all[dev];
+  std::lock_guard<std::mutex> g(g_ws_mu);
+  if ((int)g_ws_dev.size() <= dev) g_ws_dev.resize(dev + 1, nullptr);
+  if (!g_ws_dev[dev]) g_ws_dev[dev] = new Workspace();
+  return g_ws_dev[dev];
+}
+
+Workspace* workspace_create() { return new Workspace(); }
+
+void workspace_destroy(Workspace* ws) {
+  if (!ws) return;
+  {
+    std::lock_guard<std::mutex> g(ws->mu);
+    ws->free_all();
+  }
+  delete ws;
+}
+
+void release_device_workspaces() {
+  std::lock_guard<std::mutex> g(g_ws_mu);
+  int cur = 0;
+  if (hipGetDevice(&cur) != hipSuccess) cur = 0;
+  for (size_t d = 0; d < g_ws_dev.size(); d++) {
+    if (!g_ws_dev[d]) continue;
+    (void)hipSetDevice((int)d);
+    {
+      std::lock_guard<std::mutex> l(g_ws_dev[d]->mu);
+      g_ws_dev[d]->free_all();
+    }
+    delete g_ws_dev[d];
+    g_ws_dev[d] = nullptr;
+  }
+  (void)hipSetDevice(cur);
 }
 
 int device_count() {
@@ -103,6 +172,7 @@ int debug_stream_results(void* host, int32_t n) {
   Workspace* ws = ws_for_current_device();
   std::lock_guard<std::mutex> lock(ws->mu);
   if (!ws->res.p || (size_t)n * sizeof(StreamResult) > ws->res.cap) return E_PARAM;
+  if (ws->used && ws->done) HIPCHK(hipEventSynchronize(ws->done));
   HIPCHK(hipMemcpy(host, ws->res.p, (size_t)n * sizeof(StreamResult), hipMemcpyDeviceToHost));
   return n;
 }
@@ -114,6 +184,7 @@ int debug_decode_cycles(void* host, int32_t n) {
   Workspace* ws = ws_for_current_device();
   std::lock_guard<std::mutex> lock(ws->mu);
   if (!g_ddebug || !ws->ddbg.p || (size_t)n * 2 * sizeof(int64_t) > ws->ddbg.cap) return E_PARAM;
+  if (ws->used && ws->done) HIPCHK(hipEventSynchronize(ws->done));
   HIPCHK(hipMemcpy(host, ws->ddbg.p, (size_t)n * 2 * sizeof(int64_t), hipMemcpyDeviceToHost));
   return n;
 }
@@ -955,10 +1026,11 @@ static int launch_encode(Workspace* ws, const CGeom& g, int hashlog, const uint8
 }
 
 int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stride, int32_t nchunks, uint8_t* d_dst,
-                   int64_t dst_stride, int32_t* d_cbytes, hipStream_t st) {
+                   int64_t dst_stride, int32_t* d_cbytes, hipStream_t st, Workspace* wsx) {
   if (nchunks <= 0) return 0;
-  Workspace* ws = ws_for_current_device();
-  std::lock_guard<std::mutex> lock(ws->mu);
+  Workspace* ws = wsx ? wsx : ws_for_current_device();
+  WsUse use(ws, st);
+  if (use.rc) return use.rc;
   const int32_t n = P.nbytes;
   // header template in device memory (tiny; kept in the mode scratch tail)
   CGeom g{};
@@ -1169,6 +1241,15 @@ __global__ void k_dplan_chunks(const uint8_t* const* __restrict__ srcs, const in
     if (d.flags & kFlagDelta) d.filters[4] = kDelta;
     d.overhead = kHdrMin;
   }
+  // special-chunk header checks of read_chunk_header (blosc/blosc2.c:796-825)
+  if (d.special == kSpecialValue) {
+    const int32_t vts = cb - kHdrExt;
+    if (vts <= 0 || vts > 536866816 || vts > d.nbytes || d.nbytes % vts != 0) return fail(E_HEADER);
+  } else if (d.special != 0 && d.special != kSpecialZero && d.nbytes % d.typesize != 0) {
+    return fail(E_HEADER);
+  }
+  // set_nans handles float32 / float64 only (blosc/blosc2.c:1612-1636)
+  if (d.special == kSpecialNan && d.nbytes > 0 && d.typesize != 4 && d.typesize != 8) return fail(E_DATA);
   if (d.nbytes > 0 && d.blocksize > d.nbytes) d.blocksize = d.nbytes;
   if (cb > ss) return fail(E_HEADER);
   if (d.nbytes > dstsize[c]) return fail(E_WRITE);
@@ -1210,12 +1291,17 @@ struct DTotals {
   int32_t any_delta, max_filters;
   int32_t slot_mask;   // filter slots with a backward filter in any chunk (bit i = slot i)
   int32_t any_special; // some chunk is memcpyed / special (k_dspecial has work)
+  int32_t overflow;    // the batch exceeds the table capacities of the sync-free path
 };
 
-// Single-workgroup exclusive scans (block_base, stream_base, stage_off) + totals.
-__global__ __launch_bounds__(1024) void k_dscan(DChunk* __restrict__ ch, int32_t n, DTotals* __restrict__ tot) {
+// Single-workgroup exclusive scans (block_base, stream_base, stage_off) + totals.  With
+// capacities (cap_blocks >= 0, the sync-free path) a batch whose tables would not fit fails every
+// chunk with E_MEMORY and leaves nothing for the later kernels to do.
+__global__ __launch_bounds__(1024) void k_dscan(DChunk* __restrict__ ch, int32_t n, DTotals* __restrict__ tot,
+                                                int64_t cap_blocks, int64_t cap_streams, int64_t cap_stage) {
   __shared__ int64_t sb[1024];
   __shared__ int32_t sbk[1024], sst[1024], sdl[1024], smf[1024];
+  __shared__ int32_t s_over;
   const int32_t per = (n + blockDim.x - 1) / blockDim.x;
   const int32_t lo = min(n, (int32_t)threadIdx.x * per), hi = min(n, lo + per);
   int64_t a = 0;
@@ -1234,20 +1320,33 @@ __global__ __launch_bounds__(1024) void k_dscan(DChunk* __restrict__ ch, int32_t
   sb[threadIdx.x] = a; sbk[threadIdx.x] = bk; sst[threadIdx.x] = st; sdl[threadIdx.x] = dl; smf[threadIdx.x] = mf;
   __syncthreads();
   if (threadIdx.x == 0) {
-    int64_t ra = 0;
-    int32_t rb = 0, rs = 0, rd = 0, rm = 0;
+    int64_t ra = 0, rb = 0, rs = 0;
+    int32_t rd = 0, rm = 0;
     for (int t = 0; t < (int)blockDim.x; t++) {
       int64_t va = sb[t]; int32_t vb = sbk[t], vs = sst[t];
-      sb[t] = ra; sbk[t] = rb; sst[t] = rs;
+      sb[t] = ra; sbk[t] = (int32_t)rb; sst[t] = (int32_t)rs;
       ra += va; rb += vb; rs += vs; rd |= sdl[t]; rm = max(rm, smf[t]);
     }
-    tot->stage_bytes = ra; tot->nblocks = rb; tot->nstreams = rs; tot->any_delta = (rd >> 8) & 1; tot->slot_mask = rd & 0x3f; tot->max_filters = rm;
-    tot->any_special = (rd >> 9) & 1;
+    const bool over = cap_blocks >= 0 && (rb > cap_blocks || rs > cap_streams || ra > cap_stage);
+    s_over = over;
+    tot->overflow = over;
+    tot->stage_bytes = over ? 0 : ra;
+    tot->nblocks = over ? 0 : (int32_t)rb;
+    tot->nstreams = over ? 0 : (int32_t)rs;
+    tot->any_delta = (rd >> 8) & 1; tot->slot_mask = over ? 0 : rd & 0x3f; tot->max_filters = rm;
+    tot->any_special = over ? 0 : (rd >> 9) & 1;
   }
   __syncthreads();
+  const bool over = s_over;
   int64_t ra = sb[threadIdx.x];
   int32_t rb = sbk[threadIdx.x], rs = sst[threadIdx.x];
   for (int32_t i = lo; i < hi; i++) {
+    if (over) {
+      if (ch[i].status >= 0) ch[i].status = E_MEMORY;
+      ch[i].nblocks = 0;
+      ch[i].nstreams = 0;
+      continue;
+    }
     ch[i].stage_off = ra;
     ch[i].block_base = rb;
     ch[i].stream_base = rs;
@@ -1272,12 +1371,9 @@ __device__ int32_t find_chunk(const DChunk* ch, int32_t n, int32_t idx) {
   return lo;
 }
 
-// Per block: read bstarts, walk the csize words of its streams (blosc/blosc2.c:1987-2025).
-__global__ void k_dplan_blocks(const uint8_t* const* __restrict__ srcs, const int32_t* __restrict__ srcsize,
-                               DChunk* __restrict__ ch, int32_t n, DBlock* __restrict__ blocks,
-                               DStream* __restrict__ streams, int32_t nblocks_total) {
-  const int32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= nblocks_total) return;
+__device__ void dplan_block(const uint8_t* const* __restrict__ srcs, const int32_t* __restrict__ srcsize,
+                            DChunk* __restrict__ ch, int32_t n, DBlock* __restrict__ blocks,
+                            DStream* __restrict__ streams, int32_t idx) {
   const int32_t c = find_chunk(ch, n, idx);
   const DChunk d = ch[c];
   const int32_t b = idx - d.block_base;
@@ -1317,6 +1413,14 @@ __global__ void k_dplan_blocks(const uint8_t* const* __restrict__ srcs, const in
     streams[sbase + j] = st;
   }
   if (err) atomicMin(&ch[c].status, err);
+}
+
+__global__ void k_dplan_blocks(const uint8_t* const* __restrict__ srcs, const int32_t* __restrict__ srcsize,
+                               DChunk* __restrict__ ch, int32_t n, DBlock* __restrict__ blocks,
+                               DStream* __restrict__ streams, const DTotals* __restrict__ tot) {
+  const int32_t nb = tot->nblocks;
+  for (int32_t idx = blockIdx.x * blockDim.x + threadIdx.x; idx < nb; idx += gridDim.x * blockDim.x)
+    dplan_block(srcs, srcsize, ch, n, blocks, streams, idx);
 }
 
 // Decoder: one wave per stream, persistent (as many single-wave workgroups as the LDS ring
@@ -1370,11 +1474,12 @@ __device__ __forceinline__ void decode_stream(const uint8_t* const* __restrict__
 template <int RLOG>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RLOG == 12 ? 8 : 1, 8))) void k_decode(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
                                                DChunk* __restrict__ ch, const DStream* __restrict__ streams,
-                                               uint8_t* __restrict__ stage, int32_t nstreams_total,
+                                               uint8_t* __restrict__ stage, const DTotals* __restrict__ tot,
                                                const uint8_t* __restrict__ maskout, int32_t* __restrict__ next,
                                                int64_t* __restrict__ dbg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   B2H_LDS uint8_t* ring = (B2H_LDS uint8_t*)smem;
+  const int32_t nstreams_total = __builtin_amdgcn_readfirstlane(tot->nstreams);
   for (;;) {
     // branch-free grab (see k_encode)
     const int32_t s = __builtin_amdgcn_readfirstlane(atomicAdd(next, lane_id() == 0 ? 1 : 0));
@@ -1400,13 +1505,12 @@ __device__ __forceinline__ bool fused_delta_shuffle(const DChunk& d, int32_t bsi
   return bsize % (4 * ts) == 0;
 }
 
-// Backward filter for filter slot `slot`; pass 0: all blocks, 1: block 0 only, 2: blocks >= 1.
-__global__ __launch_bounds__(kBlockThreads) void k_dfilter(DChunk* __restrict__ ch, const DBlock* __restrict__ blocks,
-                                                           uint8_t* const* __restrict__ dsts, uint8_t* __restrict__ stage,
-                                                           uint8_t* __restrict__ stage2, int slot, int pass,
-                                                           int32_t nblocks_total, const uint8_t* __restrict__ maskout) {
-  const int32_t idx = blockIdx.x;
-  if (idx >= nblocks_total) return;
+// Backward filter for filter slot `slot` on one block; pass 0: all blocks, 1: block 0 only,
+// 2: blocks >= 1.  Every early return is uniform over the workgroup.
+__device__ __forceinline__ void dfilter_block(DChunk* __restrict__ ch, const DBlock* __restrict__ blocks,
+                                              uint8_t* const* __restrict__ dsts, uint8_t* __restrict__ stage,
+                                              uint8_t* __restrict__ stage2, int slot, int pass, int32_t idx,
+                                              const uint8_t* __restrict__ maskout) {
   const DBlock bk = blocks[idx];
   if (pass == 1 && bk.block != 0) return;
   if (pass == 2 && bk.block == 0) return;
@@ -1450,10 +1554,28 @@ __global__ __launch_bounds__(kBlockThreads) void k_dfilter(DChunk* __restrict__ 
   }
 }
 
-// memcpyed / special chunks (blosc/blosc2.c:1865-1935): grid (pieces, n).
-__global__ void k_dspecial(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
-                           const DChunk* __restrict__ ch, const int32_t* __restrict__ srcsize) {
-  const int32_t c = blockIdx.y;
+// Grid-stride over the batch's blocks (count and active slots from the device totals, so the
+// sync-free path can launch every slot and pass: the ones with nothing to do exit at once).
+// pass 1 / 2 are the block-0-first halves of a delta pipeline; without any delta chunk pass 1
+// runs every block and pass 2 nothing.
+__global__ __launch_bounds__(kBlockThreads) void k_dfilter(DChunk* __restrict__ ch, const DBlock* __restrict__ blocks,
+                                                           uint8_t* const* __restrict__ dsts, uint8_t* __restrict__ stage,
+                                                           uint8_t* __restrict__ stage2, int slot, int pass,
+                                                           const DTotals* __restrict__ tot,
+                                                           const uint8_t* __restrict__ maskout) {
+  if (!((tot->slot_mask >> slot) & 1)) return;
+  if (!tot->any_delta) {
+    if (pass == 2) return;
+    pass = 0;
+  }
+  const int32_t nb = tot->nblocks;
+  for (int32_t idx = blockIdx.x; idx < nb; idx += gridDim.x)
+    dfilter_block(ch, blocks, dsts, stage, stage2, slot, pass, idx, maskout);
+}
+
+// memcpyed / special chunks (blosc/blosc2.c:1865-1935): grid (pieces, chunks), chunks strided.
+__device__ __forceinline__ void dspecial_chunk(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
+                                               const DChunk* __restrict__ ch, int32_t c) {
   const DChunk d = ch[c];
   if (d.status < 0 || d.nstreams != 0 || d.nbytes == 0) return;
   const bool memcpyed = d.flags & kFlagMemcpy;
@@ -1476,6 +1598,12 @@ __global__ void k_dspecial(const uint8_t* const* __restrict__ srcs, uint8_t* con
   }
 }
 
+__global__ void k_dspecial(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
+                           const DChunk* __restrict__ ch, int32_t n, const DTotals* __restrict__ tot) {
+  if (!tot->any_special) return;
+  for (int32_t c = blockIdx.y; c < n; c += gridDim.y) dspecial_chunk(srcs, dsts, ch, c);
+}
+
 __global__ void k_dstatus(const DChunk* __restrict__ ch, int32_t* __restrict__ status, int32_t n) {
   const int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c < n) status[c] = ch[c].status;
@@ -1492,30 +1620,44 @@ static int dec_ring_log() {
 
 template <int RLOG>
 static void launch_decode(const uint8_t* const* d_src, uint8_t* const* d_dst, DChunk* ch, const DStream* streams,
-                          uint8_t* stage, int32_t nstreams, const uint8_t* d_maskout, int32_t* next, int64_t* dbg,
-                          hipStream_t st) {
+                          uint8_t* stage, const DTotals* tot, int64_t nstreams_bound, const uint8_t* d_maskout,
+                          int32_t* next, int64_t* dbg, hipStream_t st) {
   const size_t lds = size_t(1) << RLOG;
   const int slots = resident_slots(reinterpret_cast<const void*>(&k_decode<RLOG>), lds);
-  const uint32_t grid = (uint32_t)std::min<int64_t>(nstreams, slots);
-  k_decode<RLOG><<<grid, 64, lds, st>>>(d_src, d_dst, ch, streams, stage, nstreams, d_maskout, next, dbg);
+  const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(nstreams_bound, slots));
+  k_decode<RLOG><<<grid, 64, lds, st>>>(d_src, d_dst, ch, streams, stage, tot, d_maskout, next, dbg);
 }
 
-int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint8_t* const* d_dst,
-                     const int32_t* d_dstsize, int32_t n, int64_t dst_bound, int32_t* d_status,
-                     const uint8_t* d_maskout, hipStream_t st) {
-  if (n <= 0) return 0;
-  Workspace* ws = ws_for_current_device();
-  std::lock_guard<std::mutex> lock(ws->mu);
+static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const int32_t* d_srcsize,
+                             uint8_t* const* d_dst, const int32_t* d_dstsize, int32_t n, int64_t dst_bound,
+                             int32_t* d_status, const uint8_t* d_maskout, hipStream_t st, int64_t src_bound) {
   if (ws->dchunks.ensure(sizeof(DChunk) * (size_t)n) < 0 || ws->dtotals.ensure(sizeof(DTotals)) < 0) return E_MEMORY;
   DChunk* ch = ws->dchunks.as<DChunk>();
   DTotals* tot = ws->dtotals.as<DTotals>();
+  const bool bounded = src_bound >= 0;
+  // table capacities: exact (one host sync) or from the bounds (every block owns a 4-byte bstart
+  // and every stream a 4-byte csize word inside its chunk)
+  int64_t cap_blocks = -1, cap_streams = -1, cap_stage = -1;
+  if (bounded) {
+    cap_blocks = cap_streams = src_bound / 4 + 1;
+    cap_stage = std::max<int64_t>(dst_bound, 0);
+  }
   k_dplan_chunks<<<(n + 255) / 256, 256, 0, st>>>(d_src, d_srcsize, d_dstsize, ch, n);
-  k_dscan<<<1, 1024, 0, st>>>(ch, n, tot);
+  k_dscan<<<1, 1024, 0, st>>>(ch, n, tot, cap_blocks, cap_streams, cap_stage);
   HIPCHK(hipGetLastError());
   DTotals h{};
-  HIPCHK(hipMemcpyAsync(&h, tot, sizeof h, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  (void)dst_bound;
+  if (bounded) {
+    h.nblocks = (int32_t)std::min<int64_t>(cap_blocks, 0x7fffffff);
+    h.nstreams = (int32_t)std::min<int64_t>(cap_streams, 0x7fffffff);
+    h.stage_bytes = cap_stage;
+    h.max_filters = 2;      // unknown here: stage and stage2 both available
+    h.slot_mask = 0x3f;     // every slot launched; the kernels read the real mask
+    h.any_delta = 1;
+    h.any_special = 1;
+  } else {
+    HIPCHK(hipMemcpyAsync(&h, tot, sizeof h, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
   int rc = 0;
   if (h.nblocks > 0) {
     rc |= ws->dblocks.ensure(sizeof(DBlock) * (size_t)h.nblocks);
@@ -1525,7 +1667,8 @@ int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint
     if (rc) return E_MEMORY;
     DBlock* blocks = ws->dblocks.as<DBlock>();
     DStream* streams = ws->dstreams.as<DStream>();
-    k_dplan_blocks<<<(h.nblocks + 255) / 256, 256, 0, st>>>(d_src, d_srcsize, ch, n, blocks, streams, h.nblocks);
+    const int64_t pb_grid = std::max<int64_t>(1, std::min<int64_t>((h.nblocks + 255) / 256, 4096));
+    k_dplan_blocks<<<(uint32_t)pb_grid, 256, 0, st>>>(d_src, d_srcsize, ch, n, blocks, streams, tot);
     if (ws->dqctr.ensure(16)) return E_MEMORY;
     int32_t* next = ws->dqctr.as<int32_t>();
     ev_decode.start(st);
@@ -1537,28 +1680,31 @@ int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint
         dbg = ws->ddbg.as<int64_t>();
       }
       const int rlog = dec_ring_log();
-      if (rlog == 12) launch_decode<12>(d_src, d_dst, ch, streams, ws->stage.as<uint8_t>(), h.nstreams, d_maskout, next, dbg, st);
-      else if (rlog == 13) launch_decode<13>(d_src, d_dst, ch, streams, ws->stage.as<uint8_t>(), h.nstreams, d_maskout, next, dbg, st);
-      else if (rlog == 14) launch_decode<14>(d_src, d_dst, ch, streams, ws->stage.as<uint8_t>(), h.nstreams, d_maskout, next, dbg, st);
-      else launch_decode<15>(d_src, d_dst, ch, streams, ws->stage.as<uint8_t>(), h.nstreams, d_maskout, next, dbg, st);
+      uint8_t* stage = ws->stage.as<uint8_t>();
+      if (rlog == 12) launch_decode<12>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, next, dbg, st);
+      else if (rlog == 13) launch_decode<13>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, next, dbg, st);
+      else if (rlog == 14) launch_decode<14>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, next, dbg, st);
+      else launch_decode<15>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, next, dbg, st);
     }
     ev_decode.stop(st);
     ev_unfilter.start(st);
     if (h.max_filters > 0) {
+      // exact path: one workgroup per block; bounded path: a resident grid striding the blocks
+      const uint32_t grid = (uint32_t)(bounded ? std::min<int64_t>(h.nblocks, 4096) : h.nblocks);
       const int passes = h.any_delta ? 2 : 1;
       for (int ps = 0; ps < passes; ps++) {
         const int pass = h.any_delta ? ps + 1 : 0;
         for (int slot = 5; slot >= 0; slot--)
           if ((h.slot_mask >> slot) & 1)
-            k_dfilter<<<h.nblocks, kBlockThreads, 0, st>>>(ch, blocks, d_dst, ws->stage.as<uint8_t>(),
-                                                         ws->stage2.as<uint8_t>(), slot, pass, h.nblocks, d_maskout);
+            k_dfilter<<<grid, kBlockThreads, 0, st>>>(ch, blocks, d_dst, ws->stage.as<uint8_t>(),
+                                                     ws->stage2.as<uint8_t>(), slot, pass, tot, d_maskout);
       }
     }
     ev_unfilter.stop(st);
   }
   if (h.any_special) {
-    dim3 grid(64, n);
-    k_dspecial<<<grid, 256, 0, st>>>(d_src, d_dst, ch, d_srcsize);
+    dim3 grid(bounded ? 16 : 64, (uint32_t)std::min<int32_t>(n, 4096));
+    k_dspecial<<<grid, 256, 0, st>>>(d_src, d_dst, ch, n, tot);
   }
   k_dstatus<<<(n + 255) / 256, 256, 0, st>>>(ch, d_status, n);
   HIPCHK(hipGetLastError());
@@ -1569,25 +1715,35 @@ int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint
   return 0;
 }
 
+int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint8_t* const* d_dst,
+                     const int32_t* d_dstsize, int32_t n, int64_t dst_bound, int32_t* d_status,
+                     const uint8_t* d_maskout, hipStream_t st, Workspace* wsx, int64_t src_bound) {
+  if (n <= 0) return 0;
+  Workspace* ws = wsx ? wsx : ws_for_current_device();
+  WsUse use(ws, st);
+  if (use.rc) return use.rc;
+  return decompress_locked(ws, d_src, d_srcsize, d_dst, d_dstsize, n, dst_bound, d_status, d_maskout, st, src_bound);
+}
+
 __global__ void k_fill_ptrs(const uint8_t* src, int64_t src_stride, const int32_t* cbytes, uint8_t* dst, int64_t dst_stride,
                             int32_t dst_cap, const uint8_t** sp, int32_t* ss, uint8_t** dp, int32_t* ds, int32_t n) {
   const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   sp[i] = src + (int64_t)i * src_stride;
-  ss[i] = cbytes[i];
+  // a chunk may not reach into the next one (the bound of the sync-free tables relies on it)
+  ss[i] = src_stride > 0 ? (int32_t)min<int64_t>(cbytes[i], src_stride) : cbytes[i];
   dp[i] = dst + (int64_t)i * dst_stride;
   ds[i] = dst_cap;
 }
 
 int decompress_batch_strided(const uint8_t* d_src, int64_t src_stride, const int32_t* d_cbytes, int32_t n, uint8_t* d_dst,
-                             int64_t dst_stride, int32_t dst_cap, int32_t* d_status, hipStream_t st) {
+                             int64_t dst_stride, int32_t dst_cap, int32_t* d_status, hipStream_t st, Workspace* wsx) {
   if (n <= 0) return 0;
-  Workspace* ws = ws_for_current_device();
+  Workspace* ws = wsx ? wsx : ws_for_current_device();
+  WsUse use(ws, st);
+  if (use.rc) return use.rc;
   const size_t need = (size_t)n * (2 * sizeof(void*) + 2 * sizeof(int32_t)) + 64;
-  {
-    std::lock_guard<std::mutex> lock(ws->mu);
-    if (ws->ptrs.ensure(need) < 0) return E_MEMORY;
-  }
+  if (ws->ptrs.ensure(need) < 0) return E_MEMORY;
   uint8_t* base = ws->ptrs.as<uint8_t>();
   const uint8_t** sp = reinterpret_cast<const uint8_t**>(base);
   uint8_t** dp = reinterpret_cast<uint8_t**>(base + sizeof(void*) * (size_t)n);
@@ -1595,7 +1751,107 @@ int decompress_batch_strided(const uint8_t* d_src, int64_t src_stride, const int
   int32_t* ds = ss + n;
   k_fill_ptrs<<<(n + 255) / 256, 256, 0, st>>>(d_src, src_stride, d_cbytes, d_dst, dst_stride, dst_cap, sp, ss, dp, ds, n);
   HIPCHK(hipGetLastError());
-  return decompress_batch(sp, ss, dp, ds, n, (int64_t)n * dst_cap, d_status, nullptr, st);
+  // src_stride == 0 (every chunk the same source) gives no bound: exact tables
+  const int64_t src_bound = src_stride > 0 ? (int64_t)n * src_stride : -1;
+  return decompress_locked(ws, sp, ss, dp, ds, n, (int64_t)n * dst_cap, d_status, nullptr, st, src_bound);
+}
+
+// ================================================================ chunk packing (gatherv) ====
+// Exclusive prefix sum of n int32 sizes into int64 offsets[0..n] (one workgroup, tiles of 1024).
+__global__ __launch_bounds__(1024) void k_scan_sizes(const int32_t* __restrict__ sizes, int32_t n,
+                                                     int64_t* __restrict__ off) {
+  __shared__ int64_t part[1024 / 64];
+  __shared__ int64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int32_t base = 0; base < n; base += 1024) {
+    const int32_t i = base + threadIdx.x;
+    const int64_t v = i < n ? (int64_t)max(sizes[i], 0) : 0;
+    int64_t incl = v;   // wave inclusive scan (64-bit, shuffles)
+    for (int d = 1; d < 64; d <<= 1) {
+      const int64_t o = __shfl_up(incl, d);
+      if (lane >= d) incl += o;
+    }
+    if (lane == 63) part[w] = incl;
+    __syncthreads();
+    int64_t before = carry;
+    for (int k = 0; k < w; k++) before += part[k];
+    if (i < n) off[i] = before + incl - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = before + incl;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) off[n] = carry;
+}
+
+// grid (pieces, chunks): piece p of chunk c copies its 1/gridDim.x share, one wave per sub-share
+__global__ __launch_bounds__(256) void k_pack(const uint8_t* __restrict__ src, int64_t src_stride,
+                                              const int64_t* __restrict__ off, int32_t n, uint8_t* __restrict__ dst,
+                                              int unpack) {
+  for (int32_t c = blockIdx.y; c < n; c += gridDim.y) {
+    const int64_t o = off[c];
+    const int32_t len = (int32_t)(off[c + 1] - o);
+    if (len <= 0) continue;
+    const int32_t parts = gridDim.x * (blockDim.x / 64);
+    const int32_t per = ((len + parts - 1) / parts + 15) & ~15;
+    const int32_t k = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int32_t a = min(len, k * per), b = min(len, a + per);
+    if (b <= a) continue;
+    if (!unpack) wave_copy((gout_t)(dst + o + a), (gin_t)(src + (int64_t)c * src_stride + a), b - a);
+    else wave_copy((gout_t)(dst + (int64_t)c * src_stride + a), (gin_t)(src + o + a), b - a);
+  }
+}
+
+// Streaming device copy (the measured copy peak of bench.py): 16 B per lane, 4 loads in flight.
+__global__ __launch_bounds__(256) void k_copy16(uint4* __restrict__ d, const uint4* __restrict__ s, int64_t n16) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const uint4 a = s[i], b = s[i + stride], c = s[i + 2 * stride], e = s[i + 3 * stride];
+    d[i] = a; d[i + stride] = b; d[i + 2 * stride] = c; d[i + 3 * stride] = e;
+  }
+  for (; i < n16; i += stride) d[i] = s[i];
+}
+
+int device_copy(uint8_t* d_dst, const uint8_t* d_src, int64_t nbytes, hipStream_t st) {
+  if (nbytes <= 0) return 0;
+  if (((reinterpret_cast<uintptr_t>(d_dst) | reinterpret_cast<uintptr_t>(d_src)) & 15) != 0 || (nbytes & 15) != 0) {
+    HIPCHK(hipMemcpyAsync(d_dst, d_src, (size_t)nbytes, hipMemcpyDeviceToDevice, st));
+    return 0;
+  }
+  const int64_t n16 = nbytes / 16;
+  const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>((n16 + 1023) / 1024, 256 * 16));
+  k_copy16<<<grid, 256, 0, st>>>(reinterpret_cast<uint4*>(d_dst), reinterpret_cast<const uint4*>(d_src), n16);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+__global__ void k_sizes_from_offsets(const int64_t* __restrict__ off, int32_t n, int32_t* __restrict__ sizes) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) sizes[i] = (int32_t)(off[i + 1] - off[i]);
+}
+
+int pack_chunks(const uint8_t* d_src, int64_t src_stride, const int32_t* d_sizes, int32_t n, uint8_t* d_dst,
+                int64_t* d_offsets, hipStream_t st) {
+  if (n < 0) return E_PARAM;
+  k_scan_sizes<<<1, 1024, 0, st>>>(d_sizes, n, d_offsets);
+  if (n > 0) {
+    dim3 grid(16, (uint32_t)std::min<int32_t>(n, 8192));
+    k_pack<<<grid, 256, 0, st>>>(d_src, src_stride, d_offsets, n, d_dst, 0);
+  }
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int unpack_chunks(const uint8_t* d_src, const int64_t* d_offsets, int32_t n, uint8_t* d_dst, int64_t dst_stride,
+                  int32_t* d_sizes, hipStream_t st) {
+  if (n <= 0) return n < 0 ? E_PARAM : 0;
+  dim3 grid(16, (uint32_t)std::min<int32_t>(n, 8192));
+  k_pack<<<grid, 256, 0, st>>>(d_src, dst_stride, d_offsets, n, d_dst, 1);
+  if (d_sizes) k_sizes_from_offsets<<<(n + 255) / 256, 256, 0, st>>>(d_offsets, n, d_sizes);
+  HIPCHK(hipGetLastError());
+  return 0;
 }
 
 // ============================================================================ raw filters ====

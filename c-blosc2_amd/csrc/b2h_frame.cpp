@@ -57,12 +57,15 @@ struct b2h_frame {
   uint8_t filters[6] = {0}, filters_meta[6] = {0};
   std::vector<int64_t> offsets;  // per chunk: >= 0 offset from the header start, < 0 special
   hipStream_t stream = nullptr;
+  b2h::Workspace* ws = nullptr;  // the frame's own engine scratch (stream-ordered on `stream`)
 };
 
 namespace {
 
 void frame_release(b2h_frame* f) {
   if (!f) return;
+  if (f->stream) (void)hipStreamSynchronize(f->stream);
+  b2h::workspace_destroy(f->ws);
   if (f->host) (void)hipHostFree(f->host);
   if (f->dev) (void)hipFree(f->dev);
   if (f->stream) (void)hipStreamDestroy(f->stream);
@@ -113,7 +116,10 @@ int decode_chunks(b2h_frame* f, const std::vector<int64_t>& idx, const std::vect
       hipMemcpyAsync(d_caps, caps.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, f->stream) != hipSuccess) {
     rc = BLOSC2_ERROR_FAILURE;
   }
-  if (!rc) rc = b2h::decompress_batch(d_srcs, d_sizes, d_dsts, d_caps, n, bound, d_status, nullptr, f->stream);
+  int64_t src_bound = 0;
+  for (int32_t k = 0; k < n; k++) src_bound += sizes[k];
+  if (!rc) rc = b2h::decompress_batch(d_srcs, d_sizes, d_dsts, d_caps, n, bound, d_status, nullptr, f->stream, f->ws,
+                                      src_bound);
   status->assign(n, 0);
   if (!rc && hipMemcpyAsync(status->data(), d_status, n * sizeof(int32_t), hipMemcpyDeviceToHost, f->stream) != hipSuccess)
     rc = BLOSC2_ERROR_FAILURE;
@@ -189,6 +195,7 @@ b2h_frame* open_pinned(uint8_t* host, int64_t len, int* err) {
   f->host = host;
   f->len = len;
   int rc = hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking) == hipSuccess ? 0 : BLOSC2_ERROR_FAILURE;
+  if (!rc) f->ws = b2h::workspace_create();
   if (!rc) rc = parse(f);
   if (rc) { frame_release(f); f = nullptr; }
   if (err) *err = rc;
@@ -268,18 +275,21 @@ int64_t b2h_frame_decompress(b2h_frame* f, void* d_dst, int64_t dst_capacity) {
   std::vector<int64_t> idx;
   std::vector<uint8_t*> outs;
   std::vector<int32_t> caps, st;
-  for (int64_t i = 0; i < f->nchunks; i++) {
+  int rc = 0;
+  for (int64_t i = 0; i < f->nchunks && !rc; i++) {
     uint8_t* o = out + i * (int64_t)f->chunksize;
     if (f->offsets[i] < 0) {
-      const int rc = fill_special(f, f->offsets[i], o, chunk_nbytes(f, i));
-      if (rc) return rc;
+      rc = fill_special(f, f->offsets[i], o, chunk_nbytes(f, i));
       continue;
     }
     idx.push_back(i);
     outs.push_back(o);
     caps.push_back(chunk_nbytes(f, i));
   }
-  int rc = decode_chunks(f, idx, outs, caps, &st);
+  if (!rc) rc = decode_chunks(f, idx, outs, caps, &st);
+  // the fills are queued on the frame's stream too: drained before returning on every path
+  // (decode_chunks has nothing to wait for when every chunk is special)
+  if (hipStreamSynchronize(f->stream) != hipSuccess && !rc) rc = BLOSC2_ERROR_FAILURE;
   if (rc) return rc;
   for (size_t k = 0; k < idx.size(); k++)
     if (st[k] != caps[k]) return st[k] < 0 ? st[k] : BLOSC2_ERROR_DATA;

@@ -63,10 +63,14 @@ struct DevBuf {
   uint8_t* u8() const { return static_cast<uint8_t*>(p); }
 };
 
+// Per-context device state: its own stream, staging buffers and engine workspace, so distinct
+// contexts run concurrently (include/blosc2.h:1462-1466); all of it is freed by blosc2_free_ctx
+// (the reference frees its context scratch there, blosc/blosc2.c:6290).
 struct Device {
   int dev = -1;
   hipStream_t stream = nullptr;
   DevBuf in, out, small;
+  b2h::Workspace* ws = nullptr;
   bool init() {
     if (stream) return true;
     int n = 0;
@@ -76,9 +80,13 @@ struct Device {
     }
     if (hipGetDevice(&dev) != hipSuccess) return false;
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return false;
+    ws = b2h::workspace_create();
     return true;
   }
   void release() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    b2h::workspace_destroy(ws);
+    ws = nullptr;
     in.release();
     out.release();
     small.release();
@@ -100,6 +108,8 @@ int g_compressor = BLOSC_BLOSCLZ;
 int g_delta = 0;
 int32_t g_force_blocksize = 0;
 int32_t g_splitmode = BLOSC_FORWARD_COMPAT_SPLIT;
+blosc_threads_callback g_threads_cb = nullptr;
+void* g_threads_cb_data = nullptr;
 
 }  // namespace
 
@@ -212,7 +222,7 @@ int compress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void* d
   if (srcsize && hipMemcpyAsync(d.in.p, src, (size_t)srcsize, hipMemcpyHostToDevice, d.stream) != hipSuccess)
     return BLOSC2_ERROR_FAILURE;
   int32_t* d_cb = reinterpret_cast<int32_t*>(d.small.p);
-  rc = b2h::compress_batch(plan, d.in.u8(), 0, 1, d.out.u8(), 0, d_cb, d.stream);
+  rc = b2h::compress_batch(plan, d.in.u8(), 0, 1, d.out.u8(), 0, d_cb, d.stream, d.ws);
   if (rc < 0) {
     TRACE_ERROR("device compression failed: %s", b2h::last_error());
     return rc;
@@ -276,7 +286,7 @@ int decompress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void*
   Ptrs* dp = reinterpret_cast<Ptrs*>(sm);
   rc = b2h::decompress_batch(reinterpret_cast<const uint8_t* const*>(&dp->s), &dp->ss,
                              reinterpret_cast<uint8_t* const*>(&dp->o), &dp->ds, 1, nbytes, &dp->status, d_mask,
-                             d.stream);
+                             d.stream, d.ws, cbytes);
   if (rc < 0) {
     TRACE_ERROR("device decompression failed: %s", b2h::last_error());
     return rc;
@@ -312,10 +322,12 @@ void blosc2_init(void) {
   g_initlib = true;
 }
 
+// blosc/blosc2.c:6009-6036: the global contexts and every device's default workspace go
 void blosc2_destroy(void) {
   std::lock_guard<std::mutex> g(g_global_mu);
   if (g_global_cctx) { g_global_cctx->dev.release(); delete g_global_cctx; g_global_cctx = nullptr; }
   if (g_global_dctx) { g_global_dctx->dev.release(); delete g_global_dctx; g_global_dctx = nullptr; }
+  b2h::release_device_workspaces();
   g_initlib = false;
 }
 
@@ -580,6 +592,12 @@ int blosc1_decompress(const void* src, void* dest, size_t destsize) {
 }
 
 int16_t blosc2_get_nthreads(void) { return g_nthreads; }
+
+// blosc/blosc2.c:181-185: not thread-safe by contract, affects every context
+void blosc2_set_threads_callback(blosc_threads_callback callback, void* callback_data) {
+  g_threads_cb = callback;
+  g_threads_cb_data = callback_data;
+}
 int16_t blosc2_set_nthreads(int16_t nthreads) {
   const int16_t old = g_nthreads;
   if (nthreads <= 0) return BLOSC2_ERROR_INVALID_PARAM;
@@ -748,6 +766,58 @@ int blosc2_register_filter(blosc2_filter* filter) {
   return 0;
 }
 
+// ------------------------------------------------------------------ special chunks ----
+// blosc2_chunk_zeros / _nans / _uninit / _repeatval (blosc/blosc2.c:6452-6637): a 32-byte header
+// (plus the value) whose blosc2_flags carry the special kind; the blocksize is the one
+// initialize_context_compression computes for these cparams.  Host-only: no data moves.
+static int special_chunk(const blosc2_cparams& cp, int32_t nbytes, void* dest, int32_t destsize, int kind,
+                         const void* value) {
+  const int32_t need = BLOSC_EXTENDED_HEADER_LENGTH + (kind == BLOSC2_SPECIAL_VALUE ? cp.typesize : 0);
+  if (destsize < need) {
+    TRACE_ERROR("dest buffer is not long enough");
+    return BLOSC2_ERROR_DATA;
+  }
+  if (cp.typesize <= 0) return BLOSC2_ERROR_INVALID_PARAM;
+  if ((kind != BLOSC2_SPECIAL_ZERO || nbytes > 0) && nbytes % cp.typesize) {
+    TRACE_ERROR("nbytes must be a multiple of typesize");
+    return BLOSC2_ERROR_DATA;
+  }
+  b2h::CompressPlan plan;
+  int32_t bs = 0;
+  const int rc = b2h::make_compress_plan(&plan, nbytes, destsize, cp.clevel, cp.typesize, cp.blocksize, cp.splitmode,
+                                         cp.filters, cp.filters_meta, &bs, true, cp.compcode);
+  if (rc < 0) return rc;
+  uint8_t h[BLOSC_EXTENDED_HEADER_LENGTH];
+  memset(h, 0, sizeof h);
+  h[0] = BLOSC2_VERSION_FORMAT_STABLE;
+  h[1] = BLOSC_BLOSCLZ_VERSION_FORMAT;
+  h[2] = BLOSC_DOSHUFFLE | BLOSC_DOBITSHUFFLE;   // extended header
+  h[3] = (uint8_t)(cp.typesize > 255 ? 1 : cp.typesize);
+  const int32_t cb = need;
+  memcpy(h + 4, &nbytes, 4);
+  memcpy(h + 8, &bs, 4);
+  memcpy(h + 12, &cb, 4);
+  h[31] = (uint8_t)(kind << 4);
+  memcpy(dest, h, sizeof h);
+  if (kind == BLOSC2_SPECIAL_VALUE) memcpy(static_cast<uint8_t*>(dest) + sizeof h, value, (size_t)cp.typesize);
+  return cb;
+}
+
+int blosc2_chunk_zeros(blosc2_cparams cparams, const int32_t nbytes, void* dest, int32_t destsize) {
+  return special_chunk(cparams, nbytes, dest, destsize, BLOSC2_SPECIAL_ZERO, nullptr);
+}
+int blosc2_chunk_uninit(blosc2_cparams cparams, const int32_t nbytes, void* dest, int32_t destsize) {
+  return special_chunk(cparams, nbytes, dest, destsize, BLOSC2_SPECIAL_UNINIT, nullptr);
+}
+int blosc2_chunk_nans(blosc2_cparams cparams, const int32_t nbytes, void* dest, int32_t destsize) {
+  return special_chunk(cparams, nbytes, dest, destsize, BLOSC2_SPECIAL_NAN, nullptr);
+}
+int blosc2_chunk_repeatval(blosc2_cparams cparams, const int32_t nbytes, void* dest, int32_t destsize,
+                           const void* repeatval) {
+  if (!repeatval) return BLOSC2_ERROR_NULL_POINTER;
+  return special_chunk(cparams, nbytes, dest, destsize, BLOSC2_SPECIAL_VALUE, repeatval);
+}
+
 // ------------------------------------------------------------------- raw filter API ----
 static int32_t raw_filter(int kind, int32_t typesize, int32_t blocksize, const void* src, void* dest) {
   if (typesize < 1 || typesize > 256 || blocksize < 0) return BLOSC2_ERROR_INVALID_PARAM;
@@ -823,6 +893,26 @@ int b2h_decompress_ptrs(const void* const* d_srcs, const int32_t* d_srcsizes, vo
   return b2h::decompress_batch(reinterpret_cast<const uint8_t* const*>(d_srcs), d_srcsizes,
                                reinterpret_cast<uint8_t* const*>(d_dsts), d_dstsizes, n, dst_bound, d_status, nullptr,
                                static_cast<hipStream_t>(stream));
+}
+
+int b2h_pack_chunks(const void* d_src, int64_t src_stride, const int32_t* d_sizes, int32_t n, void* d_dst,
+                    int64_t* d_offsets, void* stream) {
+  if (n < 0 || !d_offsets || (n > 0 && (!d_src || !d_sizes || !d_dst))) return BLOSC2_ERROR_INVALID_PARAM;
+  return b2h::pack_chunks(static_cast<const uint8_t*>(d_src), src_stride, d_sizes, n, static_cast<uint8_t*>(d_dst),
+                          d_offsets, static_cast<hipStream_t>(stream));
+}
+
+int b2h_unpack_chunks(const void* d_src, const int64_t* d_offsets, int32_t n, void* d_dst, int64_t dst_stride,
+                      int32_t* d_sizes, void* stream) {
+  if (n < 0 || (n > 0 && (!d_src || !d_offsets || !d_dst))) return BLOSC2_ERROR_INVALID_PARAM;
+  return b2h::unpack_chunks(static_cast<const uint8_t*>(d_src), d_offsets, n, static_cast<uint8_t*>(d_dst), dst_stride,
+                            d_sizes, static_cast<hipStream_t>(stream));
+}
+
+int b2h_device_copy(void* d_dst, const void* d_src, int64_t nbytes, void* stream) {
+  if (nbytes < 0 || (nbytes > 0 && (!d_dst || !d_src))) return BLOSC2_ERROR_INVALID_PARAM;
+  return b2h::device_copy(static_cast<uint8_t*>(d_dst), static_cast<const uint8_t*>(d_src), nbytes,
+                          static_cast<hipStream_t>(stream));
 }
 
 int32_t b2h_shuffle(int32_t typesize, int32_t nbytes, const void* d_src, void* d_dst, int inverse, void* stream) {

@@ -4,19 +4,24 @@ The reference appends / decompresses a super-chunk one chunk at a time through o
 context (blosc/schunk.c:1459-1477 blosc2_schunk_append_buffer, 1481-1530
 blosc2_schunk_decompress_chunk).  Chunks are independent (each carries its own header and
 bstarts; delta only references block 0 of the same chunk), so here a super-chunk is partitioned
-into contiguous chunk ranges, one per rank (one process per GPU), and each rank runs the batch
-engine on its range.  The only exchanges are distribution and collection:
+into contiguous chunk ranges, one per rank (one process per GPU), and each rank runs ONE batch
+launch of the engine over its range.  The only exchanges are distribution and collection:
 
-  scatter_chunks     root -> ranks, equal-size raw shards (RCCL scatter over xGMI)
-  gather_compressed  ranks -> root, variable-size compressed chunks + the per-chunk sizes,
-                     assembled on the root into chunk order with an offsets index (the
-                     information a frame's chunk-offsets index holds, frame.c:1993)
-  scatter_compressed root -> ranks, the inverse for decompression
+  scatter_chunks     root -> ranks, raw shards (one RCCL scatter over xGMI)
+  gather_compressed  ranks -> root, "gatherv": every rank packs its variable-size chunks into one
+                     contiguous buffer on the device (b2h_pack_chunks), the per-chunk sizes are
+                     all-gathered, and the root receives each rank's bytes straight into its slot
+                     of the chunk-ordered result with grouped point-to-point receives (no padding,
+                     the root receives exactly the compressed bytes).  The result carries the
+                     offsets index a frame keeps (frame.c:1993).
+  scatter_compressed root -> ranks, the inverse: grouped sends of each rank's contiguous span,
+                     unpacked on the device into the batch layout (b2h_unpack_chunks)
   gather_chunks      ranks -> root, decompressed shards
 
-There is no reduction anywhere, so no ring collective is involved.  Every function takes the
-process group's backend as given ("nccl" = RCCL on ROCm for device tensors, "gloo" for the CPU
-tests) and works on whatever device the tensors live on.
+There is no reduction anywhere, so no ring collective is involved.  Device tensors go over the
+process group's backend ("nccl" = RCCL on ROCm); with the "gloo" backend (the CPU tests, or
+several ranks sharing one GPU in a test) device tensors are staged through host memory.  The
+per-chunk work never loops in Python: packing is one kernel (or one vectorised gather on CPU).
 """
 import torch
 import torch.distributed as dist
@@ -31,68 +36,153 @@ def _max_shard(nchunks, world):
     return max(hi - lo for lo, hi in (shard_range(nchunks, world, r) for r in range(world)))
 
 
-def scatter_chunks(full, chunk_nbytes, nchunks, device, root=0, group=None):
-    """Distribute the raw super-chunk `full` (uint8, nchunks*chunk_nbytes, significant on root
-    only) so that each rank receives its shard_range.  Returns the local uint8 shard."""
-    world, rank = dist.get_world_size(group), dist.get_rank(group)
-    lo, hi = shard_range(nchunks, world, rank)
-    cap = _max_shard(nchunks, world) * chunk_nbytes
-    recv = torch.empty(cap, dtype=torch.uint8, device=device)
-    parts = None
-    if rank == root:
-        parts = []
-        for r in range(world):
-            a, b = shard_range(nchunks, world, r)
-            p = full[a * chunk_nbytes:b * chunk_nbytes]
-            if p.numel() < cap:                      # equal-size scatter: pad the short shards
-                p = torch.cat([p, torch.zeros(cap - p.numel(), dtype=torch.uint8, device=device)])
-            parts.append(p.contiguous())
-    dist.scatter(recv, parts, src=root, group=group)
-    return recv[:(hi - lo) * chunk_nbytes]
+# ----------------------------------------------------------------- transport helpers ----
+def _staged(group):
+    """gloo moves host tensors only: device tensors are staged through host memory."""
+    return dist.get_backend(group) == "gloo"
+
+
+def _to_comm(t, group):
+    return t.cpu() if (t.is_cuda and _staged(group)) else t
+
+
+def _all_gather(t, group):
+    world = dist.get_world_size(group)
+    tc = _to_comm(t, group)
+    outs = [torch.empty_like(tc) for _ in range(world)]
+    dist.all_gather(outs, tc, group=group)
+    return [o.to(t.device) for o in outs]
+
+
+def _p2p(sends, recvs, group):
+    """Grouped point-to-point exchange: sends = [(tensor, dst)], recvs = [(tensor, src)].  Empty
+    tensors are skipped (both sides know every size).  Receives land in the given tensors."""
+    ops, back = [], []
+    for t, peer in sends:
+        if t.numel():
+            ops.append(dist.P2POp(dist.isend, _to_comm(t, group).contiguous(), dist.get_global_rank(group, peer)
+                                  if group is not None else peer, group))
+    for t, peer in recvs:
+        if t.numel():
+            tc = torch.empty(t.shape, dtype=t.dtype) if (t.is_cuda and _staged(group)) else t
+            ops.append(dist.P2POp(dist.irecv, tc, dist.get_global_rank(group, peer)
+                                  if group is not None else peer, group))
+            back.append((tc, t))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    for tc, t in back:
+        if tc is not t:
+            t.copy_(tc)
+
+
+# ------------------------------------------------------------------ pack / unpack ----
+def _index(sizes, stride):
+    """(source index of every packed byte in the strided layout, offsets[n+1]) -- CPU only."""
+    n = sizes.numel()
+    offs = torch.zeros(n + 1, dtype=torch.int64)
+    offs[1:] = torch.cumsum(sizes, 0)
+    total = int(offs[-1])
+    cid = torch.repeat_interleave(torch.arange(n, dtype=torch.int64), sizes)
+    pos = torch.arange(total, dtype=torch.int64) - offs[cid]
+    return cid * stride + pos, offs
 
 
 def pack_chunks(comp, stride, cbytes):
     """Concatenate the compressed chunks of a batch (chunk i at comp[i*stride:], cbytes[i] bytes)
-    into one contiguous buffer.  Returns (packed uint8, sizes int64 on the same device)."""
+    into one contiguous buffer.  Returns (packed uint8, offsets int64[n+1]) on comp's device."""
     sizes = cbytes.to(torch.int64)
-    host = sizes.cpu().tolist()
-    total = int(sum(host))
-    out = torch.empty(total, dtype=torch.uint8, device=comp.device)
-    o = 0
-    for i, n in enumerate(host):
-        out[o:o + n] = comp[i * stride:i * stride + n]
-        o += n
-    return out, sizes
+    n = sizes.numel()
+    if comp.is_cuda:
+        import blosc2_amd as B
+        total = int(sizes.sum().item())
+        out = torch.empty(max(total, 1), dtype=torch.uint8, device=comp.device)
+        offs = torch.empty(n + 1, dtype=torch.int64, device=comp.device)
+        c32 = cbytes.to(torch.int32).contiguous()
+        B.pack_chunks(comp.data_ptr(), stride, c32.data_ptr(), n, out.data_ptr(), offs.data_ptr(),
+                      torch.cuda.current_stream().cuda_stream)
+        return out[:total], offs
+    idx, offs = _index(sizes.cpu(), stride)
+    return comp[idx], offs
+
+
+def unpack_chunks(packed, offsets, stride, device):
+    """Inverse of pack_chunks: chunk i = packed[offsets[i]:offsets[i+1]] at out[i*stride:].
+    Returns (out uint8 [n*stride], sizes int32[n])."""
+    n = offsets.numel() - 1
+    out = torch.zeros(max(1, n) * stride, dtype=torch.uint8, device=device)
+    sizes = torch.empty(max(1, n), dtype=torch.int32, device=device)
+    if n == 0:
+        return out, sizes[:0]
+    if out.is_cuda:
+        import blosc2_amd as B
+        offs = offsets.to(device=device, dtype=torch.int64).contiguous()
+        src = packed.to(device)
+        B.unpack_chunks(src.data_ptr(), offs.data_ptr(), n, out.data_ptr(), stride, sizes.data_ptr(),
+                        torch.cuda.current_stream().cuda_stream)
+        return out, sizes[:n]
+    offs = offsets.cpu().to(torch.int64)
+    d = offs[1:] - offs[:-1]
+    idx, _ = _index(d, stride)
+    out[idx] = packed.to(device)
+    return out, d.to(torch.int32)
+
+
+# ------------------------------------------------------------------- collectives ----
+def scatter_chunks(full, chunk_nbytes, nchunks, device, root=0, group=None):
+    """Distribute the raw super-chunk `full` (uint8, nchunks*chunk_nbytes, significant on root
+    only) so that each rank receives its shard_range.  Returns the local uint8 shard.  Equal
+    shards go in one scatter; uneven ones (nchunks % world != 0) by grouped sends."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    lo, hi = shard_range(nchunks, world, rank)
+    spans = [shard_range(nchunks, world, r) for r in range(world)]
+    if len({b - a for a, b in spans}) == 1:
+        recv = torch.empty((hi - lo) * chunk_nbytes, dtype=torch.uint8, device=device)
+        parts = [full[a * chunk_nbytes:b * chunk_nbytes] for a, b in spans] if rank == root else None
+        if _staged(group):
+            rc = _to_comm(recv, group)
+            dist.scatter(rc, [_to_comm(p, group).contiguous() for p in parts] if parts else None, src=root, group=group)
+            recv.copy_(rc)
+        else:
+            dist.scatter(recv, parts, src=root, group=group)
+        return recv
+    recv = torch.empty((hi - lo) * chunk_nbytes, dtype=torch.uint8, device=device)
+    if rank == root:
+        recv.copy_(full[lo * chunk_nbytes:hi * chunk_nbytes])
+        _p2p([(full[a * chunk_nbytes:b * chunk_nbytes], r) for r, (a, b) in enumerate(spans) if r != root], [], group)
+    else:
+        _p2p([], [(recv, root)], group)
+    return recv
 
 
 def gather_compressed(comp, stride, cbytes, nchunks, root=0, group=None):
-    """Collect every rank's compressed chunks on the root, in chunk order.
+    """Collect every rank's compressed chunks on the root, in chunk order ("gatherv").
     Returns on the root (frame_bytes uint8, offsets int64[nchunks+1]); None elsewhere."""
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     dev = comp.device
-    packed, sizes = pack_chunks(comp, stride, cbytes)
+    packed, _ = pack_chunks(comp, stride, cbytes)
     mx = _max_shard(nchunks, world)
-    # per-chunk sizes of every rank (fixed count: pad to the largest shard)
     sz = torch.zeros(mx, dtype=torch.int64, device=dev)
-    sz[:sizes.numel()] = sizes
-    all_sz = [torch.zeros(mx, dtype=torch.int64, device=dev) for _ in range(world)]
-    dist.all_gather(all_sz, sz, group=group)
-    totals = [int(t.sum().item()) for t in all_sz]
-    cap = max(totals) if totals else 0
-    buf = torch.zeros(cap, dtype=torch.uint8, device=dev)
-    buf[:packed.numel()] = packed
-    bufs = [torch.empty(cap, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == root else None
-    dist.gather(buf, bufs, dst=root, group=group)
-    if rank != root:
-        return None
-    pieces, lens = [], []
-    for r in range(world):
-        lo, hi = shard_range(nchunks, world, r)
-        pieces.append(bufs[r][:totals[r]])
-        lens.append(all_sz[r][:hi - lo])
-    frame = torch.cat(pieces)
+    sz[:cbytes.numel()] = cbytes.to(torch.int64)
+    all_sz = _all_gather(sz, group)                     # per-chunk sizes of every rank (fixed count)
+    lens = torch.cat([all_sz[r][:b - a] for r, (a, b) in
+                      enumerate(shard_range(nchunks, world, q) for q in range(world))])
     offsets = torch.zeros(nchunks + 1, dtype=torch.int64, device=dev)
-    offsets[1:] = torch.cumsum(torch.cat(lens), 0)
+    offsets[1:] = torch.cumsum(lens, 0)
+    if rank != root:
+        _p2p([(packed, root)], [], group)
+        return None
+    host_off = offsets.cpu().tolist()
+    frame = torch.empty(int(host_off[-1]), dtype=torch.uint8, device=dev)
+    recvs = []
+    for r in range(world):
+        a, b = shard_range(nchunks, world, r)
+        piece = frame[int(host_off[a]):int(host_off[b])]
+        if r == root:
+            piece.copy_(packed)
+        else:
+            recvs.append((piece, r))
+    _p2p([], recvs, group)
     return frame, offsets
 
 
@@ -101,63 +191,66 @@ def scatter_compressed(frame, offsets, nchunks, stride, device, root=0, group=No
     (ready for b2h_decompress_batch) plus the per-chunk sizes (int32)."""
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     lo, hi = shard_range(nchunks, world, rank)
-    mx = _max_shard(nchunks, world)
-    # sizes first (fixed count), then each shard's packed bytes padded to the largest
-    sizes = torch.zeros(mx, dtype=torch.int64, device=device)
-    parts_sz, spans = None, None
+    # every rank learns the offsets index (nchunks + 1 int64, a broadcast of a few KiB)
+    off = offsets.to(device=device, dtype=torch.int64) if rank == root else \
+        torch.empty(nchunks + 1, dtype=torch.int64, device=device)
+    oc = _to_comm(off, group)
+    dist.broadcast(oc, src=root, group=group)
+    if oc is not off:
+        off.copy_(oc)
+    host_off = off.cpu().tolist()
+    span = torch.empty(int(host_off[hi] - host_off[lo]), dtype=torch.uint8, device=device)
     if rank == root:
-        off = offsets.to(device)
-        d = off[1:] - off[:-1]
-        parts_sz, spans = [], []
+        span.copy_(frame[int(host_off[lo]):int(host_off[hi])].to(device))
+        sends = []
         for r in range(world):
             a, b = shard_range(nchunks, world, r)
-            p = torch.zeros(mx, dtype=torch.int64, device=device)
-            p[:b - a] = d[a:b]
-            parts_sz.append(p)
-            spans.append(int(off[b] - off[a]))
-        span_t = torch.tensor([max(spans)], dtype=torch.int64, device=device)
+            if r != root:
+                sends.append((frame[int(host_off[a]):int(host_off[b])].to(device), r))
+        _p2p(sends, [], group)
     else:
-        span_t = torch.zeros(1, dtype=torch.int64, device=device)
-    dist.scatter(sizes, parts_sz, src=root, group=group)
-    dist.broadcast(span_t, src=root, group=group)
-    cap = int(span_t.item())
-    recv = torch.empty(cap, dtype=torch.uint8, device=device)
-    parts = None
-    if rank == root:
-        parts = []
-        for r in range(world):
-            a, b = shard_range(nchunks, world, r)
-            p = frame[int(offsets[a]):int(offsets[b])].to(device)
-            if p.numel() < cap:
-                p = torch.cat([p, torch.zeros(cap - p.numel(), dtype=torch.uint8, device=device)])
-            parts.append(p.contiguous())
-    dist.scatter(recv, parts, src=root, group=group)
-    n = hi - lo
-    host = sizes[:n].cpu().tolist()
-    comp = torch.zeros(n * stride, dtype=torch.uint8, device=device)
-    o = 0
-    for i, c in enumerate(host):
-        comp[i * stride:i * stride + c] = recv[o:o + c]
-        o += c
-    return comp, sizes[:n].to(torch.int32)
+        _p2p([], [(span, root)], group)
+    local_off = off[lo:hi + 1] - off[lo]
+    return unpack_chunks(span, local_off, stride, device)
 
 
 def gather_chunks(local, chunk_nbytes, nchunks, root=0, group=None):
     """Collect the decompressed shards on the root in chunk order (inverse of scatter_chunks)."""
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    cap = _max_shard(nchunks, world) * chunk_nbytes
-    buf = torch.zeros(cap, dtype=torch.uint8, device=local.device)
-    buf[:local.numel()] = local
-    bufs = [torch.empty(cap, dtype=torch.uint8, device=local.device) for _ in range(world)] \
-        if rank == root else None
-    dist.gather(buf, bufs, dst=root, group=group)
     if rank != root:
+        _p2p([(local, root)], [], group)
         return None
-    out = []
+    out = torch.empty(nchunks * chunk_nbytes, dtype=torch.uint8, device=local.device)
+    recvs = []
     for r in range(world):
         a, b = shard_range(nchunks, world, r)
-        out.append(bufs[r][:(b - a) * chunk_nbytes])
-    return torch.cat(out)
+        piece = out[a * chunk_nbytes:b * chunk_nbytes]
+        if r == root:
+            piece.copy_(local)
+        else:
+            recvs.append((piece, r))
+    _p2p([], recvs, group)
+    return out
+
+
+# ------------------------------------------------------------- engine + pipelines ----
+def device_engine(cparams):
+    """(compress_batch, decompress_batch) callables over the MI355X engine on torch's current
+    stream, in the signatures compress_schunk / decompress_schunk take."""
+    import blosc2_amd as B
+    cp = B.cparams(**cparams)
+
+    def comp(_, src, chunk_nbytes, n, out, stride, cap, cbytes):
+        B.compress_batch(cp, src.data_ptr(), chunk_nbytes, n, chunk_nbytes, out.data_ptr(), stride, cap,
+                         cbytes.data_ptr(), torch.cuda.current_stream().cuda_stream)
+
+    def decomp(comp_buf, stride, cbytes, n, out, chunk_nbytes):
+        status = torch.empty(n, dtype=torch.int32, device=out.device)
+        B.decompress_batch(comp_buf.data_ptr(), stride, cbytes.data_ptr(), n, out.data_ptr(), chunk_nbytes,
+                           chunk_nbytes, status.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        return status
+
+    return comp, decomp
 
 
 def compress_schunk(full, chunk_nbytes, nchunks, cparams, device, compress_batch, root=0, group=None):
@@ -175,6 +268,8 @@ def compress_schunk(full, chunk_nbytes, nchunks, cparams, device, compress_batch
     cbytes = torch.zeros(max(1, n), dtype=torch.int32, device=device)
     if n:
         compress_batch(cparams, local, chunk_nbytes, n, comp, stride, cap, cbytes)
+        if not bool((cbytes[:n] > 0).all()):   # 0: did not fit (cannot happen at cap = nbytes + 32)
+            raise RuntimeError(f"rank {rank}: a chunk failed to compress: {cbytes[:n].min().item()}")
     return gather_compressed(comp, stride, cbytes[:n], nchunks, root, group)
 
 
@@ -188,5 +283,7 @@ def decompress_schunk(frame, offsets, chunk_nbytes, nchunks, device, decompress_
     n = hi - lo
     out = torch.empty(max(1, n) * chunk_nbytes, dtype=torch.uint8, device=device)
     if n:
-        decompress_batch(comp, stride, cbytes, n, out, chunk_nbytes)
+        status = decompress_batch(comp, stride, cbytes, n, out, chunk_nbytes)
+        if status is not None and not bool((status == chunk_nbytes).all()):
+            raise RuntimeError(f"rank {rank}: decompression status {status.min().item()}")
     return gather_chunks(out[:n * chunk_nbytes], chunk_nbytes, nchunks, root, group)

@@ -30,17 +30,34 @@ BLOSC_EXPORT int b2h_compress_batch(const blosc2_cparams *cparams, const void *d
                                     int32_t nchunks, int64_t src_stride, void *d_dst, int64_t dst_stride,
                                     int32_t dst_capacity, int32_t *d_cbytes, void *stream);
 
-/* Decompress chunk i = d_src + i*src_stride (d_cbytes[i] bytes) into d_dst + i*dst_stride
- * (capacity dst_capacity).  d_status[i] = decompressed bytes or BLOSC2_ERROR_*.
- * Synchronises `stream` once (plan totals).  Returns 0 or a BLOSC2_ERROR_* code. */
+/* Decompress chunk i = d_src + i*src_stride (d_cbytes[i] bytes, at most src_stride: chunks do not
+ * overlap) into d_dst + i*dst_stride (capacity dst_capacity).  d_status[i] = decompressed bytes or
+ * BLOSC2_ERROR_*.  Stream-ordered: never waits on the host (the plan tables are sized from
+ * nchunks*src_stride).  Returns 0 or a BLOSC2_ERROR_* code. */
 BLOSC_EXPORT int b2h_decompress_batch(const void *d_src, int64_t src_stride, const int32_t *d_cbytes,
                                       int32_t nchunks, void *d_dst, int64_t dst_stride, int32_t dst_capacity,
                                       int32_t *d_status, void *stream);
 
-/* Same with device arrays of chunk pointers/sizes (arbitrary, mixed chunks). */
+/* Same with device arrays of chunk pointers/sizes (arbitrary, mixed chunks).  Synchronises `stream`
+ * once to size the plan tables exactly. */
 BLOSC_EXPORT int b2h_decompress_ptrs(const void *const *d_srcs, const int32_t *d_srcsizes, void *const *d_dsts,
                                      const int32_t *d_dstsizes, int32_t n, int64_t dst_bound, int32_t *d_status,
                                      void *stream);
+
+/* Chunk packing for the multi-GPU super-chunk scheduler (SURVEY.md §8e gatherv staging; replaces
+ * the per-chunk appends of blosc/schunk.c:1459-1477 into a contiguous, chunk-ordered buffer).
+ * pack:   chunk i (d_src + i*src_stride, d_sizes[i] bytes) -> d_dst at d_offsets[i];
+ *         d_offsets[0..n] = exclusive prefix sum of d_sizes (d_offsets[n] = total bytes).
+ * unpack: d_src[d_offsets[i], d_offsets[i+1]) -> d_dst + i*dst_stride; d_sizes[i] (optional) = size.
+ * Both asynchronous on `stream`.  Return 0 or a BLOSC2_ERROR_* code. */
+BLOSC_EXPORT int b2h_pack_chunks(const void *d_src, int64_t src_stride, const int32_t *d_sizes, int32_t n, void *d_dst,
+                                 int64_t *d_offsets, void *stream);
+BLOSC_EXPORT int b2h_unpack_chunks(const void *d_src, const int64_t *d_offsets, int32_t n, void *d_dst,
+                                   int64_t dst_stride, int32_t *d_sizes, void *stream);
+
+/* Plain device-to-device copy with the engine's streaming kernel (the achievable copy bandwidth
+ * bench.py reports next to the HBM spec).  Asynchronous on `stream`. */
+BLOSC_EXPORT int b2h_device_copy(void *d_dst, const void *d_src, int64_t nbytes, void *stream);
 
 /* Raw byte/bit (un)shuffle of a device buffer (blosc2_shuffle semantics). */
 BLOSC_EXPORT int32_t b2h_shuffle(int32_t typesize, int32_t nbytes, const void *d_src, void *d_dst, int inverse,

@@ -338,6 +338,13 @@ BLOSC_EXPORT blosc2_context *blosc2_create_dctx(blosc2_dparams dparams);
 BLOSC_EXPORT void blosc2_free_ctx(blosc2_context *context);
 BLOSC_EXPORT int blosc2_ctx_get_cparams(blosc2_context *ctx, blosc2_cparams *cparams);
 BLOSC_EXPORT int blosc2_ctx_get_dparams(blosc2_context *ctx, blosc2_dparams *dparams);
+/* Special chunks (reference include/blosc2.h:1616-1668, blosc/blosc2.c:6452-6637): header-only chunks
+ * that decompress to zeros / NaNs / uninitialised bytes / one repeated value. */
+BLOSC_EXPORT int blosc2_chunk_zeros(blosc2_cparams cparams, int32_t nbytes, void *dest, int32_t destsize);
+BLOSC_EXPORT int blosc2_chunk_uninit(blosc2_cparams cparams, int32_t nbytes, void *dest, int32_t destsize);
+BLOSC_EXPORT int blosc2_chunk_nans(blosc2_cparams cparams, int32_t nbytes, void *dest, int32_t destsize);
+BLOSC_EXPORT int blosc2_chunk_repeatval(blosc2_cparams cparams, int32_t nbytes, void *dest, int32_t destsize,
+                                        const void *repeatval);
 BLOSC_EXPORT int blosc2_set_maskout(blosc2_context *ctx, bool *maskout, int nblocks);
 
 /* the hot path: include/blosc2.h:1482-1484 and 1538-1539 */
@@ -364,6 +371,13 @@ BLOSC_EXPORT int blosc1_getitem(const void *src, int start, int nitems, void *de
 /* global settings: include/blosc2.h:751-797, 2649-2679 */
 BLOSC_EXPORT int16_t blosc2_get_nthreads(void);
 BLOSC_EXPORT int16_t blosc2_set_nthreads(int16_t nthreads);
+/* Caller-managed threading backend (include/blosc2.h:731-744 of the reference, blosc/blosc2.c:181):
+ * `callback` runs dojob(jobdata + i*jobdata_elsize) for i in [0, numjobs).  The device pipeline has
+ * no host worker pool; the callback dispatches the per-block / per-stream host callbacks of
+ * user-registered filters and codecs when nthreads > 1, as the reference's pool would. */
+typedef void (*blosc_threads_callback)(void *callback_data, void (*dojob)(void *), int numjobs, size_t jobdata_elsize,
+                                       void *jobdata);
+BLOSC_EXPORT void blosc2_set_threads_callback(blosc_threads_callback callback, void *callback_data);
 BLOSC_EXPORT const char *blosc1_get_compressor(void);
 BLOSC_EXPORT int blosc1_set_compressor(const char *compname);
 BLOSC_EXPORT void blosc2_set_delta(int dodelta);

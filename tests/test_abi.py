@@ -94,3 +94,36 @@ def test_no_gpu_fails_loudly():
     out = np.zeros(src.nbytes + 64, np.uint8)
     assert L.blosc2_compress_ctx(ctx, B._p(src), src.nbytes, B._p(out), out.nbytes) < 0
     L.blosc2_free_ctx(ctx)
+
+
+@pytest.mark.parametrize("ts,nbytes,blocksize", [(4, 4 << 20, 0), (8, 1 << 20, 0), (4, 40, 0), (8, 0, 0),
+                                                 (2, 1000, 256), (16, 1 << 16, 0)])
+def test_special_chunk_creators_match_reference(ts, nbytes, blocksize):
+    """blosc2_chunk_zeros/nans/uninit/repeatval are header-only (blosc/blosc2.c:6452-6637): the
+    drop-in writes the same bytes as the reference build (host logic, no GPU involved)."""
+    from oracle_lib import ref
+    from b2ctypes import CParams as RefCParams, cparams as rcp
+    R = ref()
+    if R is None:
+        pytest.skip("reference build absent")
+    L = B.lib()
+    val = np.arange(3, ts + 3, dtype=np.uint8)
+    for lib, ctype, mk in ((L, B.CParams, lambda: B.cparams(typesize=ts, blocksize=blocksize)),
+                           (R, RefCParams, lambda: rcp(typesize=ts, blocksize=blocksize))):
+        for fn in ("blosc2_chunk_zeros", "blosc2_chunk_nans", "blosc2_chunk_uninit"):
+            getattr(lib, fn).argtypes = [ctype, C.c_int32, C.c_void_p, C.c_int32]
+        lib.blosc2_chunk_repeatval.argtypes = [ctype, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p]
+    for fn in ("blosc2_chunk_zeros", "blosc2_chunk_nans", "blosc2_chunk_uninit", "blosc2_chunk_repeatval"):
+        extra = (C.c_void_p(val.ctypes.data),) if fn.endswith("repeatval") else ()
+        a, b = np.zeros(64, np.uint8), np.zeros(64, np.uint8)
+        na = getattr(L, fn)(B.cparams(typesize=ts, blocksize=blocksize), nbytes, C.c_void_p(a.ctypes.data), 64, *extra)
+        nb = getattr(R, fn)(rcp(typesize=ts, blocksize=blocksize), nbytes, C.c_void_p(b.ctypes.data), 64, *extra)
+        assert na == nb, (fn, na, nb)
+        assert np.array_equal(a, b), fn
+    # too-small destination and ragged nbytes are refused the same way
+    for fn in ("blosc2_chunk_nans", "blosc2_chunk_uninit"):
+        a = np.zeros(64, np.uint8)
+        assert getattr(L, fn)(B.cparams(typesize=ts), nbytes + (1 if ts > 1 else 0), C.c_void_p(a.ctypes.data), 64) == \
+            (getattr(R, fn)(rcp(typesize=ts), nbytes + (1 if ts > 1 else 0), C.c_void_p(a.ctypes.data), 64))
+        assert getattr(L, fn)(B.cparams(typesize=ts), nbytes, C.c_void_p(a.ctypes.data), 31) == \
+            getattr(R, fn)(rcp(typesize=ts), nbytes, C.c_void_p(a.ctypes.data), 31)
