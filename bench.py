@@ -258,6 +258,8 @@ def parse(argv=None):
     ap.add_argument("--chunks", type=int, default=None, help="chunks per GPU (T) / in the super-chunk (C5)")
     ap.add_argument("--chunk-mib", type=int, default=None)
     ap.add_argument("--clevel", type=int, default=5)
+    ap.add_argument("--lz-mode", default="exact", choices=["exact", "fast"],
+                    help="BloscLZ encoder: exact (byte-identical to the reference) or fast (b2h_set_blosclz_mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args(argv)
 
@@ -301,6 +303,7 @@ def run(args):
         dist.init_process_group("nccl", device_id=dev)
     import schunk_dist as SD
     L = B.lib()
+    L.b2h_set_blosclz_mode(1 if args.lz_mode == "fast" else 0)
     stream = torch.cuda.current_stream().cuda_stream
 
     if args.workload == "T":

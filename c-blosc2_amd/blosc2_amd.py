@@ -82,6 +82,7 @@ def _bind(lib):
         "b2h_shuffle": ([i32, i32, vp, vp, C.c_int, vp], i32),
         "b2h_bitshuffle": ([i32, i32, vp, vp, C.c_int, vp], i32),
         "b2h_enable_timing": ([C.c_int], None),
+        "b2h_set_blosclz_mode": ([C.c_int], C.c_int),
         "b2h_last_times": ([C.POINTER(C.c_float)], None),
         "b2h_last_error": ([], C.c_char_p),
         "b2h_device_count": ([], C.c_int),

@@ -88,6 +88,9 @@ int shuffle_dev(int32_t typesize, int32_t nbytes, const uint8_t* d_src, uint8_t*
 int bitshuffle_dev(int32_t typesize, int32_t nbytes, const uint8_t* d_src, uint8_t* d_dst, bool inverse,
                    uint8_t format_version, hipStream_t s);
 
+// BloscLZ encoder mode, process-wide: 0 exact (default), 1 fast.  Returns the previous mode.
+int set_blosclz_mode(int mode);
+
 // Kernel timing hook for bench.py (HIP events around the dominant kernels of the last batch).
 struct KernelTimes { float filter_ms, encode_ms, finalize_ms, decode_ms, unfilter_ms; };
 void enable_timing(bool on);

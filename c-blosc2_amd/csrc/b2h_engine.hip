@@ -27,6 +27,7 @@
 #include "b2h_filters.h"
 #include "b2h_format.h"
 #include "b2h_lz.h"
+#include "b2h_lzfast.h"
 
 namespace b2h {
 
@@ -433,6 +434,87 @@ __global__ __launch_bounds__(64 * (NLDS + NGLB)) void k_encode(CGeom g, const ui
     t.t = (B2H_GLB POS*)(gtab + (((size_t)blockIdx.x * NGLB + (w - NLDS)) << hashlog));
     encode_loop(g, t, dbits, oring, filt, sbuf, res, nstreams_total, next, porder);
   }
+}
+
+// ------------------------------------------------------------------ BloscLZ fast mode ----
+// One wave per workgroup (persistent, pulling streams like k_encode), the LDS holding the wave's
+// u32 hash table (2^tablog entries) and its output ring.  b2h_lzfast.h has the algorithm.
+template <typename POS>
+__global__ __launch_bounds__(64) void k_encode_fast(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
+                                                    StreamResult* __restrict__ res, int32_t nstreams_total,
+                                                    int32_t* __restrict__ next, int tablog,
+                                                    const int32_t* __restrict__ porder) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  B2H_LDS uint8_t* tab = (B2H_LDS uint8_t*)smem;
+  B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + (sizeof(POS) << tablog));
+  for (;;) {
+    const int32_t i = __builtin_amdgcn_readfirstlane(atomicAdd(next, lane_id() == 0 ? 1 : 0));
+    if (i >= nstreams_total) return;
+    const int32_t s = __builtin_amdgcn_readfirstlane(pull_to_stream(g, porder, g.front, i, nstreams_total));
+    const int32_t c = s / g.nsc, l = s - c * g.nsc;
+    int32_t off, len, blk;
+    stream_locate(g, l, &off, &len, &blk);
+    gin_t in = (gin_t)(filt + (int64_t)c * g.wstride + off);
+    gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+    StreamResult r = encode_stream_fast<POS>(in, len, g.clevel, out, tab, tablog, oring, g.overhead == kHdrExt);
+    r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
+    r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
+    if (lane_id() == 0) res[s] = r;
+  }
+}
+
+// BloscLZ encoder mode: exact (default, byte-identical to the reference) or fast (round-trip
+// identical, same grammar and decisions, parse-independent candidates).  Process-wide; also
+// B2H_LZ_MODE=fast|exact and B2H_FAST_TABLOG (12..14, default 13) in the environment.
+static int g_lz_mode = -1;
+static int lz_mode() {
+  if (g_lz_mode < 0) {
+    const char* e = getenv("B2H_LZ_MODE");
+    g_lz_mode = (e && !strcmp(e, "fast")) ? 1 : 0;
+  }
+  return g_lz_mode;
+}
+int set_blosclz_mode(int mode) {
+  const int old = lz_mode();
+  if (mode == 0 || mode == 1) g_lz_mode = mode;
+  return old;
+}
+static int fast_tablog() {
+  static int v = 0;
+  if (!v) {
+    const char* e = getenv("B2H_FAST_TABLOG");
+    v = e ? std::max(10, std::min(14, atoi(e))) : 13;
+  }
+  return v;
+}
+
+template <typename POS>
+static int launch_encode_fast_t(Workspace* ws, const CGeom& g, const uint8_t* filt, StreamResult* res, int64_t ntot,
+                                int32_t* next, const int32_t* porder, hipStream_t st) {
+  const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
+  const int tablog = std::min(fast_tablog(), hashlog);
+  const size_t lds = (sizeof(POS) << tablog) + kOutRing;
+  const void* fn = reinterpret_cast<const void*>(&k_encode_fast<POS>);
+  static bool attr_set = false;
+  if (!attr_set) {   // > 64 KiB of dynamic LDS (u32, tablog 14): opt in once
+    HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  const int slots = resident_slots(fn, lds);
+  const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(ntot, slots));
+  k_encode_fast<POS><<<grid, 64, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog, porder);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// u16 positions (half the LDS: twice the waves per CU) while every stream fits 64 KiB
+static int launch_encode_fast(Workspace* ws, const CGeom& g, const uint8_t* filt, StreamResult* res, int64_t ntot,
+                              int32_t* next, const int32_t* porder, hipStream_t st) {
+  if (std::max(g.neblock, g.leftover) <= 65536)
+    return launch_encode_fast_t<uint16_t>(ws, g, filt, res, ntot, next, porder, st);
+  return launch_encode_fast_t<uint32_t>(ws, g, filt, res, ntot, next, porder, st);
 }
 
 // ------------------------------------------------------------------------ LZ4 encoder ----
@@ -1167,8 +1249,9 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
       HIPCHK(hipMemsetAsync(porder, 0, 32 * sizeof(int32_t), st));
       ws->porder_init = true;
     }
-    rc = small ? launch_encode<uint16_t>(ws, g, hashlog, filt, res, ntot, next, porder, st)
-               : launch_encode<uint32_t>(ws, g, hashlog, filt, res, ntot, next, porder, st);
+    if (lz_mode() == 1) rc = launch_encode_fast(ws, g, filt, res, ntot, next, porder, st);
+    else rc = small ? launch_encode<uint16_t>(ws, g, hashlog, filt, res, ntot, next, porder, st)
+                    : launch_encode<uint32_t>(ws, g, hashlog, filt, res, ntot, next, porder, st);
     if (rc) return rc;
     k_plane_cost<<<1, 1024, 0, st>>>(g, res, (int32_t)ntot, porder);
   }

@@ -101,6 +101,15 @@ BLOSC_EXPORT int b2h_frame_decompress_chunk(b2h_frame *frame, int64_t nchunk, vo
  * BLOSC2_ERROR_* code (INVALID_PARAM for a range outside the frame).  Synchronous. */
 BLOSC_EXPORT int b2h_frame_get_slice(b2h_frame *frame, int64_t start, int64_t stop, void *d_dst);
 
+/* BloscLZ encoder mode (process-wide), returns the previous one.
+ *   0 exact (default): byte-identical to blosclz_compress (blosc/blosclz.c:422-619).
+ *   1 fast: same token grammar, greedy rule, limits, entropy-probe thresholds and emission, but the
+ *     hash-table candidates come from positions inserted in 64-position tiles independently of the
+ *     parse (c-blosc2_amd/csrc/b2h_lzfast.h, model tools/fm_model.c); every stream decodes with the
+ *     reference's blosclz_decompress and the chunk format is unchanged.  Also B2H_LZ_MODE=fast.
+ * Any other value only queries. */
+BLOSC_EXPORT int b2h_set_blosclz_mode(int mode);
+
 /* Per-phase HIP-event timings of the last batch on this process (ms): filter, encode, finalize,
  * decode, unfilter.  Enabling adds event records only (no extra synchronisation until read). */
 BLOSC_EXPORT void b2h_enable_timing(int on);
