@@ -11,7 +11,7 @@
 //   * one LDS atomic exchange per lane swaps the lane's position into its bucket and returns the
 //     bucket's previous position -- the most recent earlier position with that hash, earlier lanes
 //     of the same tile included (LDS applies the lanes of one instruction in lane order);
-//   * so a tile's candidates, their 28-byte compares and match lengths are known before the parse
+//   * so a tile's candidates, their 60-byte compares and match lengths are known before the parse
 //     reaches it: the kernel software-pipelines tiles T (compare + parse), T + 1 (table exchange +
 //     candidate loads) and T + 2 (input loads), and the parse itself is the exact-mode window code
 //     (ballot chain walk, DPP prefix-sum emission through the LDS output ring) started at the
@@ -53,25 +53,29 @@ __device__ __forceinline__ uint32_t fast_exchange(uint32_t v, int32_t p, bool va
   return old;
 }
 
-// The candidate's 28 bytes (p itself when the distance is out of range: compares equal, flagged off).
+// Candidate usable: 0 < distance < MAX_FARDISTANCE (blosc/blosclz.c:516-519).  Lanes without one
+// load their own bytes (compares equal, flagged off).
 __device__ __forceinline__ bool fast_cand_ok(int32_t p, uint32_t cand, bool valid) {
   const uint32_t d = (uint32_t)(p - (int32_t)cand);
   return valid && d != 0 && d < kLzFar;
 }
 
-// 28 bytes at p kept as the 8 raw aligned dwords that hold them (+ the byte shift): the loads stay
-// in flight across a whole tile of parsing and are only funnel-shifted when the bytes are used.
-struct Raw28 {
-  uint32_t d[8];
+// kCmpWords words (60 bytes) at p kept as the raw aligned dwords that hold them (+ the byte shift):
+// the loads stay in flight across a whole tile of parsing and are only funnel-shifted when the
+// bytes are used.  60 bytes up front: on T's smooth plane 32 % of the matches are >= 28 bytes but
+// only 8 % >= 60, and every longer one costs a global round trip (or a neighbour-lane lookup).
+constexpr int kCmpWords = 15, kCmpBytes = 4 * kCmpWords, kNbrStride = kCmpBytes - 4;
+struct RawCmp {
+  uint32_t d[kCmpWords + 1];
   uint32_t sh;
 };
-__device__ __forceinline__ void raw28_load(gin_t p, Raw28& r) {
+__device__ __forceinline__ void rawc_load(gin_t p, RawCmp& r) {
   const B2H_GLB uint32_t* q = align4(p);
   r.sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
 #pragma unroll
-  for (int i = 0; i < 8; i++) r.d[i] = q[i];
+  for (int i = 0; i < kCmpWords + 1; i++) r.d[i] = q[i];
 }
-__device__ __forceinline__ uint32_t raw28_word(const Raw28& r, int i) { return funnel(r.d[i], r.d[i + 1], r.sh); }
+__device__ __forceinline__ uint32_t rawc_word(const RawCmp& r, int i) { return funnel(r.d[i], r.d[i + 1], r.sh); }
 
 template <bool PROBE, typename POS>
 __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int probe_hashlog, int tablog, gout_t out,
@@ -115,25 +119,29 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
   bool early = false, sure = false;
   EPROF_DECL;
 
-  // ---- pipeline state: tile T (a, rr, cand), tile T + 1 (a), the loads of tile T + 2 ----
+  // ---- pipeline state: tile T (a, rr, cand), tiles T + 1 and T + 2 (a), the loads of T + 3 ----
+  // Input loads are consumed two tiles after issue (an input line is an HBM miss every other
+  // tile), candidate loads one tile after (recent positions: cache hits); vmcnt is in order, so
+  // consuming tile T + 1's candidates leaves tile T + 3's input loads in flight.
   int32_t T = pos / kFastTile;
-  Raw28 ca, crr, na;
+  RawCmp ca, crr, na, nna;
   uint32_t ccand = 0;
-  auto load_a = [&](int32_t t, Raw28& a) {
+  auto load_a = [&](int32_t t, RawCmp& a) {
     const int32_t p = t * kFastTile + lane;
-    raw28_load(in + (p < loop_end ? p : 0), a);
+    rawc_load(in + (p < loop_end ? p : 0), a);
   };
-  auto exchange_and_load = [&](int32_t t, const Raw28& a, uint32_t& cand, Raw28& rr) {
+  auto exchange_and_load = [&](int32_t t, const RawCmp& a, uint32_t& cand, RawCmp& rr) {
     const int32_t p = t * kFastTile + lane;
     const bool valid = p < loop_end;
-    cand = fast_exchange<POS>(raw28_word(a, 0), p, valid, tablog, tab);
+    cand = fast_exchange<POS>(rawc_word(a, 0), p, valid, tablog, tab);
     const int32_t q = fast_cand_ok(p, cand, valid) ? (int32_t)cand : (valid ? p : 0);
-    raw28_load(in + q, rr);
+    rawc_load(in + q, rr);
   };
   if (pos < loop_end) {
     load_a(T, ca);
     exchange_and_load(T, ca, ccand, crr);
     load_a(T + 1, na);
+    load_a(T + 2, nna);
   }
   while (pos < loop_end) {
     if (PROBE) {
@@ -153,33 +161,33 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
     const int32_t lim = min(kFastTile, loop_end - P);      // lanes below lim are main-loop positions
     // ---- stage B of tile T + 1 (table exchange, candidate loads) and stage A of tile T + 2: issued
     // first, consumed one tile later ----
-    Raw28 nrr, nna;
+    RawCmp nrr, n3a;
     uint32_t ncand = 0;
     exchange_and_load(T + 1, na, ncand, nrr);
-    load_a(T + 2, nna);
+    load_a(T + 3, n3a);
     EPROF_T(t1);
     EPROF_ADD(0, t0f, t1);
     // ---- stage C of tile T: candidate test (exactly as the serial loop decides) ----
-    const uint32_t v = raw28_word(ca, 0);
+    const uint32_t v = rawc_word(ca, 0);
     const uint32_t dist = (uint32_t)(p - (int32_t)ccand);
-    // first mismatching byte of in[p..p+27] vs the candidate's (28: all equal), for every lane
+    // first mismatching byte of in[p..p+59] vs the candidate's (60: all equal), for every lane
     // with a usable candidate (mmd = -1 otherwise): the chain walk extends long matches from the
     // compares of later lanes that sit at the same distance
     const bool cok = fast_cand_ok(p, ccand, valid);
-    int32_t mm = 28;
+    int32_t mm = kCmpBytes;
 #pragma unroll
-    for (int i = 6; i >= 0; i--) {
-      const uint32_t x = raw28_word(ca, i) ^ raw28_word(crr, i);
+    for (int i = kCmpWords - 1; i >= 0; i--) {
+      const uint32_t x = rawc_word(ca, i) ^ rawc_word(crr, i);
       if (x) mm = 4 * i + (__builtin_ctz(x) >> 3);
     }
     const int32_t mmd = cok ? mm : -1;
     bool accept = false;
-    int32_t lenx = 0;   // match length, or -1: the first 28 bytes all match (extend later)
+    int32_t lenx = 0;   // match length, or -1: the first kCmpBytes all match (extend later)
     if (lane >= s0 && cok && mm >= 4) {
-      const int32_t e = min(mm < 28 ? p + mm + 1 : 0x7fffffff, bound);
+      const int32_t e = min(mm < kCmpBytes ? p + mm + 1 : 0x7fffffff, bound);
       const int32_t len = e - 4 - p;
       accept = len >= 4 && (PROBE || !(len <= 5 && (dist - 1) >= kLzNear));
-      lenx = (mm < 28 || p + 29 >= bound) ? len : -1;
+      lenx = (mm < kCmpBytes || p + kCmpBytes + 1 >= bound) ? len : -1;
     }
 
     const uint64_t am = __ballot(accept);
@@ -203,17 +211,17 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
           int32_t lm = rdlane(lenx, m);
           if (lm < 0) {
             EPROF_T(te0);
-            // bytes [p_m, p_m + L) are verified; lane m + 24 k compared the next 28 at the same
+            // bytes [p_m, p_m + L) are verified; lane m + 56 k compared the next 60 at the same
             // distance if its candidate sits there: follow those lanes, go to memory only past them
             const int32_t pm = P + m;
             const uint32_t dm = (uint32_t)rdlane((int32_t)dist, m);
-            int32_t L = 28, e = -1;
-            for (int32_t j = m + 24; j < kFastTile; j += 24) {
+            int32_t L = kCmpBytes, e = -1;
+            for (int32_t j = m + kNbrStride; j < kFastTile; j += kNbrStride) {
               if (pm + L >= bound) { e = bound; break; }
               const int32_t mj = rdlane(mmd, j);
               if (mj < 0 || (uint32_t)rdlane((int32_t)dist, j) != dm) break;
-              if (mj < 28) { e = min(P + j + mj + 1, bound); break; }
-              L = j - m + 28;
+              if (mj < kCmpBytes) { e = min(P + j + mj + 1, bound); break; }
+              L = j - m + kCmpBytes;
             }
             if (e < 0) e = pm + L >= bound ? bound : wave_match_end(in, pm + L, dm, bound);
             lm = e - 4 - pm;
@@ -264,27 +272,25 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
           const int32_t req = lelit ? rdlane(base, le) + 2 : rdlane(ts + tok + 1, le);
           peak = max(peak, req);
           if (req > maxout) { fail = true; break; }
-          const bool nextchain = lane < 63 && ((chain >> (lane + 1)) & 1ull);
-          if (islit) {
-            oring[base & ORM] = (uint8_t)(v & 0xffu);
-            if (rr5 == 31 && !nextchain) oring[(base + 1) & ORM] = (uint8_t)(kLzMaxCopy - 1);
-          }
-          if (ischain) {
+          // Every element writes a fixed 6-byte slot from its start in DESCENDING byte order: a
+          // position's owner always has the lowest byte index among the elements that touch it
+          // (the others start earlier), so the owner's byte lands last and the bytes past an
+          // element's end need no masks: the next element's first byte replaces a literal's
+          // pending run marker or a token's trailing marker exactly as the reference overwrites it.
+          // Token bytes (MATCH_SHORT/LONG/_FAR, blosc/blosclz.c:270-316) + the marker opening the
+          // next literal run, built without branches.
+          if (islit || ischain) {
             const uint32_t fd = bd - kLzNear;
-            uint64_t tb;
-            int32_t nb;
-            if (ulen < 7) {
-              if (near) { tb = (uint64_t)((ulen << 5) + (bd >> 8)) | ((uint64_t)(bd & 255) << 8) | (31ull << 16); nb = 3; }
-              else { tb = (uint64_t)((ulen << 5) + 31) | (255ull << 8) | ((uint64_t)(fd >> 8) << 16) | ((uint64_t)(fd & 255) << 24) | (31ull << 32); nb = 5; }
-            } else {
-              const uint64_t rl = ulen - 7;
-              if (near) { tb = (uint64_t)((7u << 5) + (bd >> 8)) | (rl << 8) | ((uint64_t)(bd & 255) << 16) | (31ull << 24); nb = 4; }
-              else { tb = (uint64_t)((7u << 5) + 31) | (rl << 8) | (255ull << 16) | ((uint64_t)(fd >> 8) << 24) | ((uint64_t)(fd & 255) << 32) | (31ull << 40); nb = 6; }
-            }
-            if (c2v < 64 && ((chain >> c2v) & 1ull)) nb--;   // the next match overwrites the marker
+            const bool lng = ulen >= 7;
+            const uint32_t b0 = (lng ? (7u << 5) : (ulen << 5)) + (near ? (bd >> 8) : 31u);
+            const uint32_t dbytes = near ? (bd & 255u) : (255u | ((fd >> 8) << 8) | ((fd & 255u) << 16));
+            uint64_t rest = (uint64_t)dbytes | (31ull << (near ? 8 : 24));
+            if (lng) rest = (uint64_t)(ulen - 7) | (rest << 8);
+            const uint64_t bytes = islit ? (uint64_t)((v & 0xffu) | ((uint32_t)(kLzMaxCopy - 1) << 8))
+                                         : ((uint64_t)b0 | (rest << 8));
+            const int32_t start = islit ? base : ts;
 #pragma unroll
-            for (int i = 0; i < 6; i++)
-              if (i < nb) oring[(ts + i) & ORM] = (uint8_t)(tb >> (8 * i));
+            for (int i = 5; i >= 0; i--) oring[(start + i) & ORM] = (uint8_t)(bytes >> (8 * i));
           }
           if (ischain && rr5 > 0) oring[(ts - rr5 - 1) & ORM] = (uint8_t)(rr5 - 1);
           const uint64_t z = __ballot(ischain && rr5 > 0 && ts - rr5 - 1 == 0);
@@ -350,6 +356,7 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
       ca = na;
       crr = nrr;
       na = nna;
+      nna = n3a;
       ccand = ncand;
       T = NT;
     } else {   // a match jumped past tile T + 1: restart at its end
@@ -357,6 +364,7 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
       load_a(T, ca);
       exchange_and_load(T, ca, ccand, crr);
       load_a(T + 1, na);
+      load_a(T + 2, nna);
     }
     EPROF_T(t6);
     EPROF_ADD(4, t5, t6);
