@@ -140,11 +140,13 @@ def _ref_roundtrip(R, raw, chunk, nchunks, cparams, threads, reps, keep=False):
     return float(np.median(tc)), float(np.median(td)), (outs if keep else None)
 
 
-def cpu_baseline(host_src, chunk, nchunks, cparams, gpu_chunks, reps=5, single_sample=128):
+def cpu_baseline(host_src, chunk, nchunks, cparams, exact_chunks, fast_chunks, reps=5, single_sample=128):
     """The reference library (oracle/_ref, built from /root/reference sources) on the host cores,
     over the same bytes the GPU compressed: every chunk at nthreads = P, a `single_sample`-chunk
-    sample at nthreads = 1 whose outputs are byte-compared with the GPU's chunks (`gpu_chunks(i)`
-    -> uint8 array).  Without the reference build: the oracle port, 1 thread."""
+    sample at nthreads = 1 whose outputs are byte-compared with the GPU's exact-mode chunks
+    (`exact_chunks`: {chunk index: uint8 array}); the GPU's fast-mode chunks of the same sample
+    (`fast_chunks`) are decoded by the reference's blosc2_decompress_ctx and compared with the input.
+    Without the reference build: the oracle port, 1 thread."""
     import oracle_lib
     R = oracle_lib.ref()
     nbytes = nchunks * chunk
@@ -157,9 +159,10 @@ def cpu_baseline(host_src, chunk, nchunks, cparams, gpu_chunks, reps=5, single_s
         for ch in outs:
             oracle_lib.oracle_decompress(ch, chunk)
         t2 = time.perf_counter()
-        same = sum(int(np.array_equal(outs[i], gpu_chunks(i))) for i in range(nchunks))
+        same = sum(int(np.array_equal(outs[i], c)) for i, c in exact_chunks.items())
         return {"value": round(nbytes / (t2 - t0) / 2 ** 30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
-                "sample": f"oracle port, {nchunks} chunks, 1 thread; {same}/{nchunks} chunks byte-identical to the GPU"}
+                "sample": f"oracle port, {nchunks} chunks, 1 thread; {same}/{len(exact_chunks)} sampled exact-mode "
+                          f"chunks byte-identical to the GPU"}
     tc, td, _ = _ref_roundtrip(R, host_src, chunk, nchunks, cparams, P, reps)
     # nthreads = 1 on an evenly spaced sample; these chunks are also the byte-exactness check (with
     # nthreads > 1 the reference appends blocks in completion order, blosc2.c:5031-5045, so only
@@ -168,7 +171,17 @@ def cpu_baseline(host_src, chunk, nchunks, cparams, gpu_chunks, reps=5, single_s
     pick = np.linspace(0, nchunks - 1, n1).astype(np.int64)
     sample = np.concatenate([host_src[i * chunk:(i + 1) * chunk] for i in pick])
     tc1, td1, outs1 = _ref_roundtrip(R, sample, chunk, n1, cparams, 1, 3, keep=True)
-    same = sum(int(np.array_equal(outs1[k], gpu_chunks(int(i)))) for k, i in enumerate(pick))
+    same = sum(int(int(i) in exact_chunks and np.array_equal(outs1[k], exact_chunks[int(i)]))
+               for k, i in enumerate(pick))
+    # the fast-mode chunks through the reference decoder
+    from b2ctypes import dparams as rdp
+    dctx = R.blosc2_create_dctx(rdp(nthreads=1))
+    dec = np.empty(chunk, np.uint8)
+    fast_ok = 0
+    for i, c in fast_chunks.items():
+        n = R.blosc2_decompress_ctx(dctx, C.c_void_p(c.ctypes.data), c.nbytes, C.c_void_p(dec.ctypes.data), chunk)
+        fast_ok += int(n == chunk and np.array_equal(dec, host_src[i * chunk:(i + 1) * chunk]))
+    R.blosc2_free_ctx(dctx)
     b1 = n1 * chunk
     cpu = ""
     try:
@@ -180,13 +193,16 @@ def cpu_baseline(host_src, chunk, nchunks, cparams, gpu_chunks, reps=5, single_s
         pass
     return {"value": round(nbytes / (tc + td) / 2 ** 30, 4), "unit": "GiB/s", "cores": P, "kind": "reference",
             "nthreads1_value": round(b1 / (tc1 + td1) / 2 ** 30, 4),
-            "byte_identical_chunks": f"{same}/{n1}",
+            "byte_identical_chunks": f"{same}/{len(exact_chunks)}",
+            "fast_chunks_decoded_by_reference": f"{fast_ok}/{len(fast_chunks)}",
             "sample": f"all {nchunks} x {chunk >> 20} MiB chunks of this run's input (host copy of the device "
                       f"bytes, same cparams), median of {reps}: compress {nbytes / tc / 2**30:.3f} GiB/s + "
                       f"decompress {nbytes / td / 2**30:.3f} GiB/s at nthreads={P} ({core_note}); nthreads=1 on "
                       f"{n1} chunks: {b1 / (tc1 + td1) / 2**30:.3f} GiB/s (c {b1 / tc1 / 2**30:.3f}, "
                       f"d {b1 / td1 / 2**30:.3f}); {host_isa()}; host CPU: {cpu}; the reference's serial "
-                      f"(nthreads=1) chunks are byte-identical to the GPU's for {same} of the {n1} sampled"}
+                      f"(nthreads=1) chunks are byte-identical to the GPU's exact-mode chunks for {same} of "
+                      f"{len(exact_chunks)} sampled; the reference decodes {fast_ok} of {len(fast_chunks)} sampled "
+                      f"fast-mode chunks back to the input"}
 
 
 def pmc_traffic(kernel, workload):
@@ -258,8 +274,9 @@ def parse(argv=None):
     ap.add_argument("--chunks", type=int, default=None, help="chunks per GPU (T) / in the super-chunk (C5)")
     ap.add_argument("--chunk-mib", type=int, default=None)
     ap.add_argument("--clevel", type=int, default=5)
-    ap.add_argument("--lz-mode", default="exact", choices=["exact", "fast"],
-                    help="BloscLZ encoder: exact (byte-identical to the reference) or fast (b2h_set_blosclz_mode)")
+    ap.add_argument("--lz-mode", default="both", choices=["exact", "fast", "both"],
+                    help="BloscLZ encoder: exact (byte-identical to the reference), fast (b2h_set_blosclz_mode), "
+                         "or both (exact measured beside the fast headline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args(argv)
 
@@ -303,7 +320,6 @@ def run(args):
         dist.init_process_group("nccl", device_id=dev)
     import schunk_dist as SD
     L = B.lib()
-    L.b2h_set_blosclz_mode(1 if args.lz_mode == "fast" else 0)
     stream = torch.cuda.current_stream().cuda_stream
 
     if args.workload == "T":
@@ -351,6 +367,8 @@ def run(args):
     out = torch.empty(shard, dtype=torch.uint8, device=dev)
     status = torch.zeros(nch, dtype=torch.int32, device=dev)
     cp = B.cparams(**kw)
+    ncpu = nch if args.workload == "T" else min(nch, 1000)
+    pick = np.linspace(0, max(0, ncpu - 1), min(ncpu, 128)).astype(np.int64)   # chunks the CPU leg checks
 
     def compress():
         B.compress_batch(cp, src_u8.data_ptr(), chunk, nch, chunk, comp.data_ptr(), stride, cap,
@@ -360,44 +378,53 @@ def run(args):
         B.decompress_batch(comp.data_ptr(), stride, cbytes.data_ptr(), nch, out.data_ptr(), chunk, chunk,
                            status.data_ptr(), stream)
 
-    for _ in range(max(1, args.warmup)):    # at least one pass: the check below reads its output
-        compress()
-        decompress()
-    torch.cuda.synchronize()
-    # correctness of the measured configuration (outside the timed region)
-    assert torch.equal(out, src_u8), "round trip mismatch"
-    assert bool((status == chunk).all()), "decompress status"
-    total_c = int(cbytes.to(torch.int64).sum().item())
-    out.zero_()
+    def measure(mode):
+        """W untimed + K timed steps with BloscLZ encoder `mode` (0 exact, 1 fast)."""
+        L.b2h_set_blosclz_mode(mode)
+        for _ in range(max(1, args.warmup)):    # at least one pass: the check below reads its output
+            compress()
+            decompress()
+        torch.cuda.synchronize()
+        # correctness of the measured configuration (outside the timed region)
+        assert torch.equal(out, src_u8), "round trip mismatch"
+        assert bool((status == chunk).all()), "decompress status"
+        total_c = int(cbytes.to(torch.int64).sum().item())
+        out.zero_()
+        L.b2h_enable_timing(1)
+        enc_ms, dec_ms = [], []
+        tm = Timer()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            tm.mark()
+            compress()
+            enc_ms.append(B.last_times()["encode_ms"])   # waits on this call's k_encode events only
+            tm.mark()
+            decompress()
+            dec_ms.append(B.last_times()["decode_ms"])
+        tm.mark()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        L.b2h_enable_timing(0)
+        spans = tm.spans()
+        assert torch.equal(out, src_u8), "round trip mismatch (timed steps)"
+        el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        hc = cbytes.cpu().numpy()
+        hcomp = comp.cpu().numpy() if (rank == 0 and world == 1) else None
+        sample = {int(i): hcomp[i * stride:i * stride + int(hc[i])].copy() for i in pick} if hcomp is not None else {}
+        return {"elapsed": float(el.item()), "t_c": float(np.mean(spans[0::2])), "t_d": float(np.mean(spans[1::2])),
+                "enc": float(np.mean(enc_ms)), "dec": float(np.mean(dec_ms)), "total_c": total_c, "sample": sample}
 
-    L.b2h_enable_timing(1)
-    enc_ms, dec_ms = [], []
-    tm = Timer()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        tm.mark()
-        compress()
-        enc_ms.append(B.last_times()["encode_ms"])   # waits on this call's k_encode events only
-        tm.mark()
-        decompress()
-        dec_ms.append(B.last_times()["decode_ms"])
-    tm.mark()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    L.b2h_enable_timing(0)
-    spans = tm.spans()
-    t_c = float(np.mean(spans[0::2]))
-    t_d = float(np.mean(spans[1::2]))
-    assert torch.equal(out, src_u8), "round trip mismatch (timed steps)"
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+    modes = {"exact": [0], "fast": [1], "both": [0, 1]}[args.lz_mode]
+    meas = {m: measure(m) for m in modes}
+    head = meas[modes[-1]]                     # the headline: fast when measured
+    total_c = head["total_c"]
 
     gather_s = None
     if args.workload == "C5" and world > 1:   # chunk-ordered collection on rank 0 (gatherv)
@@ -415,24 +442,37 @@ def run(args):
 
     if rank == 0:
         n_all = shard * world if args.workload == "T" else nch_total * chunk
-        value = n_all * args.steps / elapsed / 2 ** 30
-        enc, dec = float(np.mean(enc_ms)), float(np.mean(dec_ms))
-        N, Cb = shard, total_c
+        N = shard
+
+        def summary(m):
+            Cb = m["total_c"]
+            return {"value": round(n_all * args.steps / m["elapsed"] / 2 ** 30, 3),
+                    "ms_per_step": round(m["elapsed"] / args.steps * 1e3, 3), "cratio": round(N / Cb, 4),
+                    "compress_ms": round(m["t_c"], 3), "decompress_ms": round(m["t_d"], 3),
+                    "encode_ms": round(m["enc"], 3), "decode_ms": round(m["dec"], 3)}
+        enc, dec, Cb = head["enc"], head["dec"], head["total_c"]
+        t_c, t_d = head["t_c"], head["t_d"]
         dominant = "k_encode" if enc >= dec else "k_decode"
         kms = enc if dominant == "k_encode" else dec
         achieved = (N + Cb) / (kms * 1e-3) / 1e9     # algorithmic bytes of one launch: N + C
-        traffic, traffic_src, traffic_corr = pmc_traffic(dominant, workload)
+        lz_name = "fast" if modes[-1] == 1 else "exact"
+        traffic, traffic_src, traffic_corr = pmc_traffic(dominant, workload + f" [{lz_name}]")
         peak_copy = copy_peak_gbps(dev)
         step_gbps = 2 * (N + Cb) / ((t_c + t_d) * 1e-3) / 1e9
         res = {
             "metric": METRIC,
-            "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "value": summary(head)["value"], "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": summary(head)["ms_per_step"],
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u8",
             "data": ("synthetic gen_f32 (SURVEY §8d), generated on device" if args.workload == "T"
                      else "synthetic int64 ramp (value = global element index), generated on device"),
             "config": {"workload": workload, "chunks_per_gpu": nch, "chunk_bytes": chunk, "clevel": args.clevel,
-                       "parallelism": f"chunk-sharded x{world}", "cratio": round(N / Cb, 4)},
+                       "parallelism": f"chunk-sharded x{world}", "cratio": round(N / Cb, 4),
+                       "blosclz_mode": lz_name + (" (round-trip identical through the reference decoder; same "
+                                                  "grammar, greedy rule and probe decisions, parse-independent "
+                                                  "candidates: c-blosc2_amd/csrc/b2h_lzfast.h)" if lz_name == "fast"
+                                                  else " (byte-identical to the reference)")},
+            "modes": {("exact" if m == 0 else "fast"): summary(meas[m]) for m in modes},
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
@@ -456,12 +496,9 @@ def run(args):
             res["config"]["gatherv_s"] = round(gather_s, 4)
         if world == 1 and not args.no_cpu_baseline:
             host = src_u8.cpu().numpy()
-            host_comp = comp.cpu().numpy()
-            host_cb = cbytes.cpu().numpy()
-            ncpu = nch if args.workload == "T" else min(nch, 1000)
-            res["cpu_baseline"] = cpu_baseline(
-                host, chunk, ncpu, kw, lambda i: host_comp[i * stride:i * stride + int(host_cb[i])],
-                reps=5 if args.workload == "T" else 3)
+            ex = meas.get(0, {}).get("sample", {})
+            res["cpu_baseline"] = cpu_baseline(host, chunk, ncpu, kw, ex, meas.get(1, {}).get("sample", {}),
+                                               reps=5 if args.workload == "T" else 3)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
