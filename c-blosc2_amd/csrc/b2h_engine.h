@@ -39,10 +39,12 @@ struct CompressPlan {
 // Fill the plan from cparams-level values the way blosc2_compress_ctx does (initialize_context_
 // compression + write_compression_header, blosc/blosc2.c:2385-2533, 2911-3001).  Returns < 0 on
 // invalid parameters.  `ctx_blocksize` is the blocksize the context currently holds (0 = auto).
+// compcode: BloscLZ (0), LZ4 (1), or a user-registered codec id (> 31: compformat
+// BLOSC_UDCODEC_FORMAT, versionlz = user_version -- encoded by the host callback path).
 int make_compress_plan(CompressPlan* p, int32_t nbytes, int32_t destsize, int clevel, int32_t typesize,
                        int32_t ctx_blocksize, int32_t splitmode, const uint8_t* filters,
                        const uint8_t* filters_meta, int32_t* computed_blocksize, bool extended = true,
-                       int compcode = 0);
+                       int compcode = 0, int compcode_meta = 0, int user_version = 1);
 
 // Compress `nchunks` chunks: chunk i is d_src + i*src_stride, its output goes to
 // d_dst + i*dst_stride (capacity plan.destsize), its cbytes (>0, 0 = does not fit) to d_cbytes[i].
@@ -62,7 +64,7 @@ int compress_batch(const CompressPlan& plan, const uint8_t* d_src, int64_t src_s
 int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint8_t* const* d_dst,
                      const int32_t* d_dstsize, int32_t n, int64_t dst_bound, int32_t* d_status,
                      const uint8_t* d_maskout, hipStream_t stream, Workspace* ws = nullptr,
-                     int64_t src_bound = -1);
+                     int64_t src_bound = -1, int raw_streams = 0);
 
 // Strided convenience form: chunk i at d_src + i*src_stride with cbytes d_cbytes[i], output at
 // d_dst + i*dst_stride with capacity dst_cap.
@@ -79,6 +81,19 @@ int pack_chunks(const uint8_t* d_src, int64_t src_stride, const int32_t* d_sizes
                 int64_t* d_offsets, hipStream_t stream);
 int unpack_chunks(const uint8_t* d_src, const int64_t* d_offsets, int32_t n, uint8_t* d_dst, int64_t dst_stride,
                   int32_t* d_sizes, hipStream_t stream);
+
+// Single-chunk stages of host-driven pipelines (chunks with user-registered filters / codecs):
+// one forward filter slot of P over the blocks of `pass` (0 all, 1 block 0, 2 blocks >= 1); the
+// built-in codec stage from an already-filtered image; one backward filter over a pass.  Device
+// buffers need >= 256 bytes of slack.  decompress_batch(..., raw_streams = 1) decodes the streams
+// only, leaving the backward filters to the caller.
+int forward_filter_chunk(const CompressPlan& P, int slot, int pass, const uint8_t* d_in, uint8_t* d_out,
+                         const uint8_t* d_raw, hipStream_t stream);
+int encode_chunk_filtered(const CompressPlan& P, const uint8_t* d_filt, const uint8_t* d_raw, uint8_t* d_dst,
+                          int32_t* d_cbytes, hipStream_t stream, Workspace* ws = nullptr);
+int backward_filter_chunk(uint8_t filter, uint8_t meta, int32_t typesize, int32_t nbytes, int32_t blocksize,
+                          uint8_t version, int pass, const uint8_t* d_in, uint8_t* d_out, const uint8_t* d_final,
+                          hipStream_t stream);
 
 // Streaming D2D copy (bench.py's measured copy peak).
 int device_copy(uint8_t* d_dst, const uint8_t* d_src, int64_t nbytes, hipStream_t stream);

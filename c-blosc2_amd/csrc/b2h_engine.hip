@@ -959,9 +959,11 @@ static int32_t split_block(int32_t splitmode, int compcode, const uint8_t* filte
 
 int make_compress_plan(CompressPlan* p, int32_t nbytes, int32_t destsize, int clevel, int32_t typesize,
                        int32_t ctx_blocksize, int32_t splitmode, const uint8_t* filters,
-                       const uint8_t* filters_meta, int32_t* computed_blocksize, bool extended, int compcode) {
+                       const uint8_t* filters_meta, int32_t* computed_blocksize, bool extended, int compcode,
+                       int compcode_meta, int user_version) {
   memset(p, 0, sizeof *p);
-  if (compcode != 0 && compcode != 1) return -7;   // BLOSC2_ERROR_CODEC_SUPPORT: BloscLZ and LZ4 only
+  // BloscLZ and LZ4 on the device; user codecs (> BLOSC2_DEFINED_CODECS_STOP) through host callbacks
+  if (compcode != 0 && compcode != 1 && compcode <= 31) return -7;   // BLOSC2_ERROR_CODEC_SUPPORT
   p->compcode = compcode;
   p->overhead = extended ? kHdrExt : kHdrMin;
   if (nbytes > 0x7fffffff - kHdrExt) return E_MAXBUF;
@@ -972,7 +974,7 @@ int make_compress_plan(CompressPlan* p, int32_t nbytes, int32_t destsize, int cl
   if (nbytes < typesize) {
     bs = 1;
   } else {
-    const int32_t splitmode_nb = split_block(splitmode, 0, filters, typesize, nbytes);
+    const int32_t splitmode_nb = split_block(splitmode, compcode, filters, typesize, nbytes);
     bs = nbytes;
     if (ctx_blocksize) {
       bs = ctx_blocksize;
@@ -1016,7 +1018,8 @@ int make_compress_plan(CompressPlan* p, int32_t nbytes, int32_t destsize, int cl
     }
     p->split = split_block(splitmode, compcode, filters, ts, bs) != 0;
     if (!p->split) flags |= kFlagDontSplit;
-    flags |= (uint8_t)(compcode << 5);   // compformat (blosc/blosc2.c:2990-2991)
+    // compformat (compcode_to_compformat, blosc/blosc2.c:396-414, 2990-2991): user codecs -> UDCODEC (6)
+    flags |= (uint8_t)((compcode <= 1 ? compcode : 6) << 5);
   }
   p->memcpyed = memcpyed;
   int32_t hb = ctx_blocksize > 0 ? ctx_blocksize : bs;
@@ -1024,10 +1027,12 @@ int make_compress_plan(CompressPlan* p, int32_t nbytes, int32_t destsize, int cl
   p->header_blocksize = hb;
   uint8_t* h = p->header;
   memset(h, 0, 32);
-  h[0] = 5; h[1] = 1; h[2] = flags; h[3] = (uint8_t)ts;
+  // versionlz: compcode_to_compversion (blosc/blosc2.c:418-446), a user codec's registered version
+  h[0] = 5; h[1] = (uint8_t)(compcode <= 1 ? 1 : user_version); h[2] = flags; h[3] = (uint8_t)ts;
   for (int k = 0; k < 4; k++) { h[4 + k] = (uint8_t)(nbytes >> (8 * k)); h[8 + k] = (uint8_t)(hb >> (8 * k)); }
   for (int i = 0; i < 6; i++) { h[16 + i] = filters[i]; h[24 + i] = filters_meta[i]; }
   h[22] = (uint8_t)compcode;   // udcompcode = the codec (blosc/blosc2.c:1030)
+  h[23] = (uint8_t)compcode_meta;
   return 0;
 }
 
@@ -1107,15 +1112,9 @@ static int launch_encode(Workspace* ws, const CGeom& g, int hashlog, const uint8
   return launch_encode_shape<POS, 1, 4>(ws, g, hashlog, filt, res, ntot, next, porder, st);
 }
 
-int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stride, int32_t nchunks, uint8_t* d_dst,
-                   int64_t dst_stride, int32_t* d_cbytes, hipStream_t st, Workspace* wsx) {
-  if (nchunks <= 0) return 0;
-  Workspace* ws = wsx ? wsx : ws_for_current_device();
-  WsUse use(ws, st);
-  if (use.rc) return use.rc;
-  const int32_t n = P.nbytes;
-  // header template in device memory (tiny; kept in the mode scratch tail)
+static CGeom make_geom(const CompressPlan& P, int64_t src_stride, int64_t dst_stride) {
   CGeom g{};
+  const int32_t n = P.nbytes;
   g.nbytes = n;
   g.bs = P.blocksize;
   g.ts = P.typesize;
@@ -1126,6 +1125,29 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
   g.src_stride = src_stride;
   g.dst_stride = dst_stride;
   g.wstride = ((int64_t)n + 255) / 256 * 256 + 256;
+  if (!P.memcpyed && g.bs > 0) {
+    g.nblocks = n / g.bs + (n % g.bs ? 1 : 0);
+    g.leftover = n % g.bs;
+    g.spb = P.split ? g.ts : 1;
+    g.neblock = g.bs / g.spb;
+    const int32_t full = g.nblocks - (g.leftover ? 1 : 0);
+    g.nsc = full * g.spb + (g.leftover ? 1 : 0);
+  }
+  return g;
+}
+
+static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const uint8_t* filt, const uint8_t* raw,
+                        int64_t raw_stride, uint8_t* d_dst, int64_t dst_stride, int32_t* d_cbytes, int32_t nchunks,
+                        const uint8_t* htpl, int64_t ntot, hipStream_t st);
+
+int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stride, int32_t nchunks, uint8_t* d_dst,
+                   int64_t dst_stride, int32_t* d_cbytes, hipStream_t st, Workspace* wsx) {
+  if (nchunks <= 0) return 0;
+  Workspace* ws = wsx ? wsx : ws_for_current_device();
+  WsUse use(ws, st);
+  if (use.rc) return use.rc;
+  const int32_t n = P.nbytes;
+  CGeom g = make_geom(P, src_stride, dst_stride);
   if (P.memcpyed) {
     if (ws->mode.ensure(64) < 0) return E_MEMORY;
     uint8_t* htpl = ws->mode.as<uint8_t>();
@@ -1136,12 +1158,6 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
     HIPCHK(hipGetLastError());
     return 0;
   }
-  g.nblocks = n / g.bs + (n % g.bs ? 1 : 0);
-  g.leftover = n % g.bs;
-  g.spb = P.split ? g.ts : 1;
-  g.neblock = g.bs / g.spb;
-  const int32_t full = g.nblocks - (g.leftover ? 1 : 0);
-  g.nsc = full * g.spb + (g.leftover ? 1 : 0);
   const int64_t ntot = (int64_t)nchunks * g.nsc;
   if (ntot > 0x7fffffff) { snprintf(g_err, sizeof g_err, "too many streams"); return E_PARAM; }
 
@@ -1227,7 +1243,16 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
     filt = ws->t1.as<uint8_t>();
   }
   HIPCHK(hipGetLastError());
+  return encode_stage(ws, P, g, filt, raw, raw_stride, d_dst, dst_stride, d_cbytes, nchunks, htpl, ntot, st);
+}
 
+// The codec stage of a batch whose filtered images sit at filt + c * g.wstride: encode every stream,
+// then the serial-layout finalisation, the payload scatter and the memcpy fallbacks (from raw).
+static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const uint8_t* filt, const uint8_t* raw,
+                        int64_t raw_stride, uint8_t* d_dst, int64_t dst_stride, int32_t* d_cbytes, int32_t nchunks,
+                        const uint8_t* htpl, int64_t ntot, hipStream_t st) {
+  const int32_t n = P.nbytes;
+  int rc = 0;
   // encode
   ev_encode.start(st);
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
@@ -1278,6 +1303,86 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
   return 0;
 }
 
+// ------------------------------------------------- single-chunk stages (host-driven pipelines) ----
+// Chunks whose pipeline holds a user-registered filter or codec run the reference's per-block /
+// per-stream host callbacks between device stages (blosc2_api.cpp).  These are the device stages,
+// for ONE chunk in device buffers carrying >= 256 bytes of slack.
+
+// One forward filter (slot `slot` of P) over the blocks of `pass` (0 all, 1 block 0, 2 the others).
+int forward_filter_chunk(const CompressPlan& P, int slot, int pass, const uint8_t* d_in, uint8_t* d_out,
+                         const uint8_t* d_raw, hipStream_t st) {
+  CGeom g = make_geom(P, 0, 0);
+  const uint8_t f = P.filters[slot], meta = P.filters_meta[slot];
+  if (f == kNoFilter || g.nblocks == 0) return 0;
+  int zeroed = 0;
+  if (f == kTruncPrec && !hostside_trunc_ok((int8_t)meta, g.ts, &zeroed)) return E_FILTER;
+  if (f == kIntTrunc && !hostside_int_trunc_ok((int8_t)meta, P.typesize, &zeroed)) return E_FILTER;
+  if (f > kTruncPrec && f != kBytedelta && f != kIntTrunc) return E_FILTER;
+  const uint8_t kmeta = (f == kBytedelta && meta == 0) ? (uint8_t)g.ts : meta;
+  const int32_t nb = pass == 1 ? 1 : (pass == 2 ? g.nblocks - 1 : g.nblocks);
+  if (nb <= 0) return 0;
+  k_ffilter<<<dim3(nb, 1), kBlockThreads, 0, st>>>(g, pass, f, kmeta, d_in, 0, d_out, 0, d_raw, 0, zeroed);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// The codec stage for one chunk whose filtered image is d_filt (BloscLZ / LZ4): chunk -> d_dst,
+// cbytes -> *d_cbytes.  d_raw is what a memcpy fallback stores.
+int encode_chunk_filtered(const CompressPlan& P, const uint8_t* d_filt, const uint8_t* d_raw, uint8_t* d_dst,
+                          int32_t* d_cbytes, hipStream_t st, Workspace* wsx) {
+  Workspace* ws = wsx ? wsx : ws_for_current_device();
+  WsUse use(ws, st);
+  if (use.rc) return use.rc;
+  CGeom g = make_geom(P, 0, 0);
+  const int64_t ntot = g.nsc;
+  int rc = 0;
+  rc |= ws->sbuf.ensure((size_t)g.wstride);
+  rc |= ws->res.ensure(sizeof(StreamResult) * (size_t)std::max<int64_t>(1, ntot));
+  rc |= ws->place.ensure(sizeof(Place) * (size_t)std::max<int64_t>(1, ntot));
+  rc |= ws->mode.ensure(sizeof(int32_t) + 64);
+  if (rc) return E_MEMORY;
+  uint8_t* htpl = ws->mode.as<uint8_t>() + 16;
+  HIPCHK(hipMemcpyAsync(htpl, P.header, 32, hipMemcpyHostToDevice, st));
+  return encode_stage(ws, P, g, d_filt, d_raw, 0, d_dst, 0, d_cbytes, 1, htpl, ntot, st);
+}
+
+// One backward filter over the blocks of `pass` of one chunk: in -> out; delta's blocks >= 1 XOR
+// with the final output's block 0 (d_final), as pipeline_backward does (blosc/blosc2.c:1505-1529).
+__global__ __launch_bounds__(kBlockThreads) void k_dfilter_chunk(uint8_t filter, uint8_t meta, int32_t ts, int32_t nbytes,
+                                                                 int32_t bs, uint8_t version, int pass,
+                                                                 const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                                 const uint8_t* __restrict__ final_out) {
+  const int32_t nblocks = nbytes / bs + (nbytes % bs ? 1 : 0);
+  const int32_t b = pass == 2 ? (int32_t)blockIdx.x + 1 : (int32_t)blockIdx.x;
+  if (b >= nblocks) return;
+  const int32_t bsize = (b == nblocks - 1 && nbytes % bs) ? nbytes % bs : bs;
+  const int64_t off = (int64_t)b * bs;
+  switch (filter) {
+    case kShuffle: block_unshuffle(in + off, out + off, bsize, meta ? meta : ts); break;
+    case kBitshuffle: block_bitunshuffle(in + off, out + off, bsize, ts, version); break;
+    case kBytedelta: block_bytedelta_decode(in + off, out + off, bsize, meta ? meta : ts); break;
+    case kDelta:
+      if (b == 0) block_delta_decode_first(in + off, out + off, bsize, ts);
+      else block_delta_decode_rest(in + off, final_out, out + off, bsize, ts);
+      break;
+    default: break;
+  }
+}
+
+int backward_filter_chunk(uint8_t filter, uint8_t meta, int32_t typesize, int32_t nbytes, int32_t blocksize,
+                          uint8_t version, int pass, const uint8_t* d_in, uint8_t* d_out, const uint8_t* d_final,
+                          hipStream_t st) {
+  if (nbytes <= 0 || blocksize <= 0) return 0;
+  if (filter != kShuffle && filter != kBitshuffle && filter != kDelta && filter != kBytedelta) return E_FILTER;
+  const int32_t nblocks = nbytes / blocksize + (nbytes % blocksize ? 1 : 0);
+  const int32_t nb = pass == 1 ? 1 : (pass == 2 ? nblocks - 1 : nblocks);
+  if (nb <= 0) return 0;
+  k_dfilter_chunk<<<nb, kBlockThreads, 0, st>>>(filter, meta, typesize, nbytes, blocksize, version, pass, d_in, d_out,
+                                                 d_final);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 // ============================================================== decompression: planning ====
 __device__ __forceinline__ int32_t rd32(const uint8_t* p) {
   return (int32_t)((uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24));
@@ -1289,7 +1394,8 @@ __host__ __device__ __forceinline__ bool bwd_noop(uint8_t f) { return f == kNoFi
 
 // read_chunk_header + initialize_context_decompression (blosc/blosc2.c:738-852, 2688-2909)
 __global__ void k_dplan_chunks(const uint8_t* const* __restrict__ srcs, const int32_t* __restrict__ srcsize,
-                               const int32_t* __restrict__ dstsize, DChunk* __restrict__ ch, int32_t n) {
+                               const int32_t* __restrict__ dstsize, DChunk* __restrict__ ch, int32_t n,
+                               int raw_streams) {
   const int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= n) return;
   DChunk d;
@@ -1352,6 +1458,11 @@ __global__ void k_dplan_chunks(const uint8_t* const* __restrict__ srcs, const in
   if (ss < d.overhead + 4 * d.nblocks) return fail(E_READ);
   const int32_t spb = d.dont_split ? 1 : d.typesize;
   d.nstreams = (d.nblocks - (d.leftover ? 1 : 0)) * spb + (d.leftover ? 1 : 0);
+  if (raw_streams) {   // the caller applies the filters itself (host-driven pipelines)
+    d.nfilters_bwd = 0;
+    ch[c] = d;
+    return;
+  }
   // backward pipeline: active filters (not NOFILTER / TRUNC_PREC), applied high slot -> low
   int k = 0, K = 0;
   for (int i = 5; i >= 0; i--) if (!bwd_noop(d.filters[i])) K++;
@@ -1713,7 +1824,8 @@ static void launch_decode(const uint8_t* const* d_src, uint8_t* const* d_dst, DC
 
 static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const int32_t* d_srcsize,
                              uint8_t* const* d_dst, const int32_t* d_dstsize, int32_t n, int64_t dst_bound,
-                             int32_t* d_status, const uint8_t* d_maskout, hipStream_t st, int64_t src_bound) {
+                             int32_t* d_status, const uint8_t* d_maskout, hipStream_t st, int64_t src_bound,
+                             int raw_streams = 0) {
   if (ws->dchunks.ensure(sizeof(DChunk) * (size_t)n) < 0 || ws->dtotals.ensure(sizeof(DTotals)) < 0) return E_MEMORY;
   DChunk* ch = ws->dchunks.as<DChunk>();
   DTotals* tot = ws->dtotals.as<DTotals>();
@@ -1725,7 +1837,7 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
     cap_blocks = cap_streams = src_bound / 4 + 1;
     cap_stage = std::max<int64_t>(dst_bound, 0);
   }
-  k_dplan_chunks<<<(n + 255) / 256, 256, 0, st>>>(d_src, d_srcsize, d_dstsize, ch, n);
+  k_dplan_chunks<<<(n + 255) / 256, 256, 0, st>>>(d_src, d_srcsize, d_dstsize, ch, n, raw_streams);
   k_dscan<<<1, 1024, 0, st>>>(ch, n, tot, cap_blocks, cap_streams, cap_stage);
   HIPCHK(hipGetLastError());
   DTotals h{};
@@ -1800,12 +1912,13 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
 
 int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint8_t* const* d_dst,
                      const int32_t* d_dstsize, int32_t n, int64_t dst_bound, int32_t* d_status,
-                     const uint8_t* d_maskout, hipStream_t st, Workspace* wsx, int64_t src_bound) {
+                     const uint8_t* d_maskout, hipStream_t st, Workspace* wsx, int64_t src_bound, int raw_streams) {
   if (n <= 0) return 0;
   Workspace* ws = wsx ? wsx : ws_for_current_device();
   WsUse use(ws, st);
   if (use.rc) return use.rc;
-  return decompress_locked(ws, d_src, d_srcsize, d_dst, d_dstsize, n, dst_bound, d_status, d_maskout, st, src_bound);
+  return decompress_locked(ws, d_src, d_srcsize, d_dst, d_dstsize, n, dst_bound, d_status, d_maskout, st, src_bound,
+                           raw_streams);
 }
 
 __global__ void k_fill_ptrs(const uint8_t* src, int64_t src_stride, const int32_t* cbytes, uint8_t* dst, int64_t dst_stride,

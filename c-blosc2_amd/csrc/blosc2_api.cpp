@@ -7,6 +7,9 @@
 // without a usable GPU the compute entry points return BLOSC2_ERROR_FAILURE loudly.
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+
+#include <algorithm>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -176,9 +179,10 @@ int compname_to_code(const char* name) {
 }
 
 // Pipelines the device path executes: built-in filters and BloscLZ.
+// User-registered filters and codecs run through the host-callback pipelines below.
 int check_supported(const blosc2_context* c) {
-  if (c->compcode != BLOSC_BLOSCLZ && c->compcode != BLOSC_LZ4) {
-    TRACE_ERROR("codec %d is not implemented by the MI355X engine (BloscLZ and LZ4 only)", c->compcode);
+  if (c->compcode != BLOSC_BLOSCLZ && c->compcode != BLOSC_LZ4 && c->compcode <= BLOSC2_DEFINED_CODECS_STOP) {
+    TRACE_ERROR("codec %d is not implemented by the MI355X engine (BloscLZ, LZ4 and user codecs)", c->compcode);
     return BLOSC2_ERROR_CODEC_SUPPORT;
   }
   if (c->use_dict) {
@@ -187,10 +191,6 @@ int check_supported(const blosc2_context* c) {
   }
   for (int i = 0; i < 6; i++) {
     const uint8_t f = c->filters[i];
-    if (f > BLOSC_TRUNC_PREC && f != b2h::kBytedelta && f != b2h::kIntTrunc) {
-      TRACE_ERROR("filter %d runs on host callbacks; not part of the device pipeline", f);
-      return BLOSC2_ERROR_FILTER_PIPELINE;
-    }
     // bytedelta with meta 0 takes the super-chunk's typesize and fails without one
     // (plugins/filters/bytedelta/bytedelta.c:90-98 -> pipeline_forward returns NULL)
     if (f == b2h::kBytedelta && c->filters_meta[i] == 0 && c->schunk == nullptr) {
@@ -205,14 +205,23 @@ int check_supported(const blosc2_context* c) {
   return 0;
 }
 
+bool needs_host_callbacks(const uint8_t* filters, int compcode);
+int compress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void* dest, int32_t destsize,
+                    int32_t blocksize_in, bool sticky, bool extended);
+int decompress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void* dest, int32_t destsize,
+                      const std::vector<uint8_t>* mask);
+
 // Compress one host buffer through the engine (n = 1 batch).
 int compress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void* dest, int32_t destsize,
                   int32_t blocksize_in, bool sticky, bool extended) {
   if (srcsize < 0) return BLOSC2_ERROR_INVALID_PARAM;
+  if (needs_host_callbacks(ctx->filters, ctx->compcode))
+    return compress_hybrid(ctx, src, srcsize, dest, destsize, blocksize_in, sticky, extended);
   b2h::CompressPlan plan;
   int32_t computed = 0;
   int rc = b2h::make_compress_plan(&plan, srcsize, destsize, ctx->clevel, ctx->typesize, blocksize_in, ctx->splitmode,
-                                   ctx->filters, ctx->filters_meta, &computed, extended, ctx->compcode);
+                                   ctx->filters, ctx->filters_meta, &computed, extended, ctx->compcode,
+                                   ctx->compcode_meta);
   if (rc < 0) return rc;
   if (sticky) ctx->blocksize = computed;
   if ((rc = check_supported(ctx)) < 0) return rc;
@@ -263,6 +272,19 @@ int decompress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void*
                 mask->size(), nblocks);
     return BLOSC2_ERROR_DATA;
   }
+  {
+    // user filters / codecs in an extended header (not memcpyed, not special) -> host callbacks
+    const uint8_t* s = static_cast<const uint8_t*>(src);
+    const bool ext = (s[2] & BLOSC_DOSHUFFLE) && (s[2] & BLOSC_DOBITSHUFFLE);
+    if (ext && srcsize >= BLOSC_EXTENDED_HEADER_LENGTH && !(s[2] & BLOSC_MEMCPYED) && ((s[31] >> 4) & 7) == 0 &&
+        nbytes > 0) {
+      uint8_t fl[6];
+      for (int i = 0; i < 6; i++) fl[i] = s[16 + i];
+      if (s[0] == BLOSC2_VERSION_FORMAT_ALPHA) fl[5] = 0;
+      if (needs_host_callbacks(fl, (s[2] >> 5) == BLOSC_UDCODEC_FORMAT ? 255 : 0))
+        return decompress_hybrid(ctx, src, srcsize, dest, destsize, mask);
+    }
+  }
   Device& d = ctx->dev;
   if (!d.init()) return BLOSC2_ERROR_FAILURE;
   const size_t mask_bytes = mask ? mask->size() : 0;
@@ -307,6 +329,415 @@ int decompress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void*
     }
   }
   return status;
+}
+
+
+// ============================================================= host-callback pipelines ====
+// Chunks whose pipeline holds a user-registered filter (id > BLOSC2_DEFINED_FILTERS_STOP other
+// than the device plugins 35 / 36) or a user-registered codec (compcode > 31) run the reference's
+// semantics with the user's callbacks on host buffers and the built-in stages on the device:
+//   compress   pipeline_forward (blosc/blosc2.c:1055-1180): the active slots in order, buffers
+//              cycled src -> tmp -> tmp2 (the >= 3-filter rewrite of the input included), block 0
+//              first when DELTA is present (its reference is the input's block 0 as the serial
+//              walk leaves it); user forward(src, dst, bsize, meta, cparams*, id) per block;
+//              then blosc_c / serial_blosc / blosc_compress_context (2161-2228, 1210-1469,
+//              3004-3107): BloscLZ / LZ4 on the device, a user encoder(in, neblock, out, maxout,
+//              meta, cparams*, chunk) per stream with the same run detection, maxout, raw and
+//              memcpy / special-zero fallbacks;
+//   decompress blosc_d (1710-2157) with the user decoder per stream (or the device decoder for
+//              built-in codecs, streams only), then pipeline_backward (1473-1609) slot 5 -> 0 with
+//              user backward(...) per block and device un-filters, block 0 first with DELTA.
+// Callbacks run on the calling thread; with nthreads > 1 and blosc2_set_threads_callback, the
+// per-block filter callbacks and per-stream decoder callbacks go through the caller's backend.
+
+struct FilterInfo { char* forward; char* backward; };   // blosc-private.h filter_info
+struct CodecInfo { char* encoder; char* decoder; };     // blosc-private.h codec_info
+
+bool valid_plugin_name(const char* n) {
+  if (!n || !*n) return false;
+  for (const char* c = n; *c; c++)
+    if (!((*c >= 'a' && *c <= 'z') || (*c >= 'A' && *c <= 'Z') || (*c >= '0' && *c <= '9') || *c == '_')) return false;
+  return true;
+}
+
+// fill_filter / fill_codec (blosc/blosc2.c:913-971): lazy dlopen of libblosc2_<name>.so, symbol
+// `info` naming the callbacks (the python-path fallback of load_lib is not reproduced).
+void* load_plugin(const char* name) {
+  if (!valid_plugin_name(name)) return nullptr;
+  char path[512];
+  snprintf(path, sizeof path, "libblosc2_%s.so", name);
+  return dlopen(path, RTLD_LAZY);
+}
+
+bool lookup_filter(uint8_t id, blosc2_filter* out) {
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  for (auto& f : g_filters) {
+    if (f.id != id) continue;
+    if (f.forward == nullptr || f.backward == nullptr) {
+      void* lib = load_plugin(f.name);
+      FilterInfo* info = lib ? static_cast<FilterInfo*>(dlsym(lib, "info")) : nullptr;
+      if (!info) { TRACE_ERROR("Could not load filter %d", id); return false; }
+      f.forward = reinterpret_cast<blosc2_filter_forward_cb>(dlsym(lib, info->forward));
+      f.backward = reinterpret_cast<blosc2_filter_backward_cb>(dlsym(lib, info->backward));
+      if (!f.forward || !f.backward) { TRACE_ERROR("Wrong library loaded"); return false; }
+    }
+    *out = f;
+    return true;
+  }
+  return false;
+}
+
+bool lookup_codec(int compcode, blosc2_codec* out) {
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  for (auto& c : g_codecs) {
+    if (c.compcode != compcode) continue;
+    if (c.encoder == nullptr || c.decoder == nullptr) {
+      void* lib = load_plugin(c.compname);
+      CodecInfo* info = lib ? static_cast<CodecInfo*>(dlsym(lib, "info")) : nullptr;
+      if (!info) { TRACE_ERROR("Could not load codec %d.", compcode); return false; }
+      c.encoder = reinterpret_cast<blosc2_codec_encoder_cb>(dlsym(lib, info->encoder));
+      c.decoder = reinterpret_cast<blosc2_codec_decoder_cb>(dlsym(lib, info->decoder));
+      if (!c.encoder || !c.decoder) { TRACE_ERROR("encoder or decoder cannot be loaded"); return false; }
+    }
+    *out = c;
+    return true;
+  }
+  return false;
+}
+
+bool device_filter(uint8_t f) { return f <= BLOSC_TRUNC_PREC || f == b2h::kBytedelta || f == b2h::kIntTrunc; }
+
+bool needs_host_callbacks(const uint8_t* filters, int compcode) {
+  if (compcode > BLOSC2_DEFINED_CODECS_STOP) return true;
+  for (int i = 0; i < 6; i++)
+    if (!device_filter(filters[i])) return true;
+  return false;
+}
+
+// Runs job(i) for i in [0, n): through the caller's threads callback when one is set and the
+// context asks for threads (blosc2.c:181-185, 5399-5414), else in order.  Returns the first error.
+template <typename F>
+int run_jobs(int16_t nthreads, int n, F&& job) {
+  std::vector<int> rcs((size_t)std::max(n, 0), 0);
+  struct Job { F* fn; int i; int* rc; };
+  if (g_threads_cb && nthreads > 1 && n > 1) {
+    std::vector<Job> jobs((size_t)n);
+    for (int i = 0; i < n; i++) jobs[(size_t)i] = Job{&job, i, &rcs[(size_t)i]};
+    g_threads_cb(g_threads_cb_data, [](void* p) { Job* j = static_cast<Job*>(p); *j->rc = (*j->fn)(j->i); }, n,
+                 sizeof(Job), jobs.data());
+  } else {
+    for (int i = 0; i < n; i++) {
+      rcs[(size_t)i] = job(i);
+      if (rcs[(size_t)i]) break;
+    }
+  }
+  for (int r : rcs) if (r) return r;
+  return 0;
+}
+
+void cycle(uint8_t*& src, uint8_t*& dst, uint8_t*& tmp) {   // _cycle_buffers (blosc/blosc2.c:1048)
+  uint8_t* t = src;
+  src = dst;
+  dst = tmp;
+  tmp = t;
+}
+
+struct HybridBufs {   // per-call device buffers of the host-callback pipelines
+  DevBuf a, b, c, out;
+  ~HybridBufs() { a.release(); b.release(); c.release(); out.release(); }
+};
+
+int sync_to_host(hipStream_t st, void* h, const void* d, size_t n) {
+  if (n && hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, st) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+  return hipStreamSynchronize(st) == hipSuccess ? 0 : BLOSC2_ERROR_FAILURE;
+}
+int to_device(hipStream_t st, void* d, const void* h, size_t n) {
+  if (n && hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, st) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+  return 0;
+}
+
+int compress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void* dest, int32_t destsize,
+                    int32_t blocksize_in, bool sticky, bool extended) {
+  blosc2_codec codec{};
+  const bool ucodec = ctx->compcode > BLOSC2_DEFINED_CODECS_STOP;
+  if (ucodec && !lookup_codec(ctx->compcode, &codec)) {
+    TRACE_ERROR("User-defined compressor codec %d not found during compression", ctx->compcode);
+    return BLOSC2_ERROR_CODEC_SUPPORT;
+  }
+  b2h::CompressPlan P;
+  int32_t computed = 0;
+  int rc = b2h::make_compress_plan(&P, srcsize, destsize, ctx->clevel, ctx->typesize, blocksize_in, ctx->splitmode,
+                                   ctx->filters, ctx->filters_meta, &computed, extended, ctx->compcode,
+                                   ctx->compcode_meta, ucodec ? codec.version : 1);
+  if (rc < 0) return rc;
+  if (sticky) ctx->blocksize = computed;
+  if ((rc = check_supported(ctx)) < 0) return rc;
+  Device& d = ctx->dev;
+  if (!d.init()) return BLOSC2_ERROR_FAILURE;
+  const int32_t n = srcsize, ovh = P.overhead;
+  HybridBufs hb;
+  if (!hb.a.ensure((size_t)n) || !hb.b.ensure((size_t)n) || !hb.c.ensure((size_t)n) ||
+      !hb.out.ensure((size_t)destsize) || !d.small.ensure(64))
+    return BLOSC2_ERROR_MEMORY_ALLOC;
+  if ((rc = to_device(d.stream, hb.a.p, src, (size_t)n))) return rc;
+  int32_t* d_cb = reinterpret_cast<int32_t*>(d.small.p);
+  blosc2_cparams cp;
+  blosc2_ctx_get_cparams(ctx, &cp);
+  if (P.memcpyed) {   // chunk-level memcpy: no filter or codec runs
+    rc = b2h::compress_batch(P, hb.a.u8(), 0, 1, hb.out.u8(), 0, d_cb, d.stream, d.ws);
+    if (rc < 0) return rc;
+    int32_t cb = 0;
+    if ((rc = sync_to_host(d.stream, &cb, d_cb, 4))) return rc;
+    const int32_t ncopy = cb > 0 ? cb : std::min(destsize, ovh);
+    if (hipMemcpy(dest, hb.out.p, (size_t)ncopy, hipMemcpyDeviceToHost) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+    return cb;
+  }
+  const int32_t bs = P.blocksize, nblocks = n / bs + (n % bs ? 1 : 0);
+  bool has_delta = false;
+  for (int i = 0; i < 6; i++) has_delta |= P.filters[i] == BLOSC_DELTA;
+  // ---- forward pipeline (block 0 first with DELTA: the serial walk's order) ----
+  std::vector<uint8_t> hs, hd;
+  uint8_t* fsrc = hb.a.u8();
+  for (int pass = (has_delta && nblocks > 1) ? 1 : 0; pass <= ((has_delta && nblocks > 1) ? 2 : 0); pass++) {
+    uint8_t *s = hb.a.u8(), *t = hb.b.u8(), *u = hb.c.u8();
+    const int32_t b0 = pass == 2 ? 1 : 0, b1 = pass == 1 ? 1 : nblocks;
+    const int64_t lo = (int64_t)b0 * bs, hi = std::min<int64_t>((int64_t)b1 * bs, n);
+    for (int i = 0; i < 6; i++) {
+      const uint8_t f = P.filters[i];
+      if (f == BLOSC_NOFILTER) continue;
+      if (device_filter(f)) {
+        if ((rc = b2h::forward_filter_chunk(P, i, pass, s, t, hb.a.u8(), d.stream)) < 0) return rc;
+      } else {
+        blosc2_filter flt{};
+        if (!lookup_filter(f, &flt)) {
+          TRACE_ERROR("User-defined filter %d not found during compression", f);
+          return BLOSC2_ERROR_FILTER_PIPELINE;
+        }
+        hs.resize((size_t)n);
+        hd.resize((size_t)n);
+        if ((rc = sync_to_host(d.stream, hs.data() + lo, s + lo, (size_t)(hi - lo)))) return rc;
+        rc = run_jobs(ctx->nthreads, b1 - b0, [&](int k) {
+          const int32_t b = b0 + k;
+          const int32_t bsize = std::min<int32_t>(bs, n - b * bs);
+          blosc2_cparams cpl = cp;
+          const int r = flt.forward(hs.data() + (int64_t)b * bs, hd.data() + (int64_t)b * bs, bsize,
+                                    P.filters_meta[i], &cpl, f);
+          return r != BLOSC2_ERROR_SUCCESS ? (int)BLOSC2_ERROR_FILTER_PIPELINE : 0;
+        });
+        if (rc) { TRACE_ERROR("User-defined filter %d failed during compression", f); return rc; }
+        if ((rc = to_device(d.stream, t + lo, hd.data() + lo, (size_t)(hi - lo)))) return rc;
+      }
+      cycle(s, t, u);
+    }
+    fsrc = s;
+  }
+  // ---- codec ----
+  int32_t cb = 0;
+  if (!ucodec) {
+    rc = b2h::encode_chunk_filtered(P, fsrc, hb.a.u8(), hb.out.u8(), d_cb, d.stream, d.ws);
+    if (rc < 0) return rc;
+    if ((rc = sync_to_host(d.stream, &cb, d_cb, 4))) return rc;
+    const int32_t ncopy = cb > 0 ? cb : std::min(destsize, ovh);
+    if (hipMemcpy(dest, hb.out.p, (size_t)ncopy, hipMemcpyDeviceToHost) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+    return cb;
+  }
+  // user encoder per stream, serial layout (blosc_c / serial_blosc / blosc_compress_context)
+  std::vector<uint8_t> filt((size_t)n + 1), raw((size_t)n + 1), out((size_t)destsize + 1);
+  if ((rc = sync_to_host(d.stream, filt.data(), fsrc, (size_t)n))) return rc;
+  if ((rc = sync_to_host(d.stream, raw.data(), hb.a.p, (size_t)n))) return rc;   // memcpy source
+  uint8_t* o = out.data();
+  memcpy(o, P.header, (size_t)ovh);
+  int32_t ntbytes = ovh + 4 * nblocks;
+  const bool split = !((P.header[2] >> 4) & 1);
+  bool ok = ntbytes <= destsize;
+  for (int32_t b = 0; b < nblocks && ok; b++) {
+    const int32_t bsize = std::min<int32_t>(bs, n - b * bs);
+    const bool leftover = bsize < bs;
+    const int32_t ns = (split && !leftover) ? P.typesize : 1, neblock = bsize / ns;
+    const int32_t bstart = ntbytes;
+    memcpy(o + ovh + 4 * b, &bstart, 4);
+    for (int32_t j = 0; j < ns && ok; j++) {
+      const uint8_t* ip = filt.data() + (int64_t)b * bs + (int64_t)j * neblock;
+      ntbytes += 4;
+      if (extended && std::all_of(ip, ip + neblock, [&](uint8_t x) { return x == ip[0]; })) {
+        if (ntbytes > destsize) { ok = false; break; }
+        const int32_t v = -(int32_t)ip[0];
+        memcpy(o + ntbytes - 4, &v, 4);
+        if (ip[0]) {
+          ntbytes += 1;
+          if (ntbytes > destsize) { ok = false; break; }
+          o[ntbytes - 1] = 0x1;
+        }
+        continue;
+      }
+      int32_t maxout = neblock;
+      if (ntbytes + maxout > destsize) {
+        maxout = destsize - ntbytes;
+        if (maxout <= 0) { ok = false; break; }
+      }
+      blosc2_cparams cpl = cp;
+      int32_t c = codec.encoder(ip, neblock, o + ntbytes, maxout, ctx->compcode_meta, &cpl, raw.data());
+      if (c > maxout) return BLOSC2_ERROR_WRITE_BUFFER;
+      if (c < 0) return BLOSC2_ERROR_DATA;
+      if (c == 0) c = neblock;
+      if (c == neblock) {
+        if (ntbytes + neblock > destsize) { ok = false; break; }
+        memcpy(o + ntbytes, ip, (size_t)neblock);
+      }
+      memcpy(o + ntbytes - 4, &c, 4);
+      ntbytes += c;
+    }
+  }
+  if (ok) {
+    int32_t nstreams = nblocks;
+    if (split) nstreams = (n % bs) ? (nblocks - 1) * P.typesize + 1 : nblocks * P.typesize;
+    if (ntbytes == ovh + 4 * nblocks + 4 * nstreams) {   // every stream a zero run: SPECIAL_ZERO
+      o[31] |= (uint8_t)(BLOSC2_SPECIAL_ZERO << 4);
+      ntbytes = ovh;
+    }
+    cb = ntbytes;
+  } else if (n + ovh <= destsize) {   // memcpy fallback: the (possibly rewritten) input
+    o[2] |= BLOSC_MEMCPYED;
+    memcpy(o + ovh, raw.data(), (size_t)n);
+    cb = n + ovh;
+  } else {
+    cb = 0;
+  }
+  memcpy(o + 12, &cb, 4);
+  memcpy(dest, o, (size_t)(cb > 0 ? cb : std::min(destsize, ovh)));
+  return cb;
+}
+
+int decompress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void* dest, int32_t destsize,
+                      const std::vector<uint8_t>* mask) {
+  const uint8_t* s = static_cast<const uint8_t*>(src);
+  const int32_t nbytes = rd32(s + 4), cbytes = rd32(s + 12);
+  int32_t bs = rd32(s + 8);
+  const int ts = s[3];
+  if (nbytes > 0 && bs > nbytes) bs = nbytes;
+  const int32_t nblocks = nbytes > 0 ? nbytes / bs + (nbytes % bs ? 1 : 0) : 0;
+  const bool ucodec = (s[2] >> 5) == BLOSC_UDCODEC_FORMAT;
+  const int ccode = s[22], cmeta = s[23];
+  const int32_t ovh = BLOSC_EXTENDED_HEADER_LENGTH;
+  if (srcsize < ovh + 4 * nblocks) return BLOSC2_ERROR_READ_BUFFER;
+  blosc2_codec codec{};
+  if (ucodec && !lookup_codec(ccode, &codec)) {
+    TRACE_ERROR("User-defined compressor codec %d not found during decompression", ccode);
+    return BLOSC2_ERROR_CODEC_SUPPORT;
+  }
+  Device& d = ctx->dev;
+  if (!d.init()) return BLOSC2_ERROR_FAILURE;
+  HybridBufs hb;
+  if (!hb.a.ensure((size_t)std::max(cbytes, nbytes)) || !hb.b.ensure((size_t)nbytes) || !hb.c.ensure((size_t)nbytes) ||
+      !hb.out.ensure((size_t)nbytes) || !d.small.ensure(64))
+    return BLOSC2_ERROR_MEMORY_ALLOC;
+  blosc2_dparams dp;
+  blosc2_ctx_get_dparams(ctx, &dp);
+  int rc = 0;
+  uint8_t* unf = hb.b.u8();   // the decoded, still filtered image
+  if (ucodec) {
+    // blosc_d per stream with the user decoder (blosc/blosc2.c:1987-2136)
+    std::vector<uint8_t> img((size_t)nbytes + 1);
+    const bool split = !((s[2] >> 4) & 1);
+    std::vector<std::pair<int32_t, int32_t>> streams;   // (src offset of the csize word, dst offset)
+    for (int32_t b = 0; b < nblocks; b++) {
+      const int32_t bsize = std::min<int32_t>(bs, nbytes - b * bs);
+      const int32_t ns = (split && bsize == bs) ? ts : 1, neblock = bsize / ns;
+      int32_t pos = rd32(s + ovh + 4 * b);
+      for (int32_t j = 0; j < ns; j++) {
+        if (pos < 0 || pos + 4 > srcsize) return BLOSC2_ERROR_READ_BUFFER;
+        const int32_t cs = rd32(s + pos);
+        streams.push_back({pos, b * bs + j * neblock});
+        pos += 4 + (cs > 0 ? cs : (cs < 0 ? 1 : 0));
+        (void)neblock;
+      }
+    }
+    rc = run_jobs(ctx->nthreads, (int)streams.size(), [&](int k) {
+      const int32_t pos = streams[(size_t)k].first, off = streams[(size_t)k].second;
+      const int32_t b = off / bs;
+      const int32_t bsize = std::min<int32_t>(bs, nbytes - b * bs);
+      const int32_t ns = (split && bsize == bs) ? ts : 1, neblock = bsize / ns;
+      const int32_t cs = rd32(s + pos);
+      const uint8_t* in = s + pos + 4;
+      uint8_t* o = img.data() + off;
+      if (cs == 0) { memset(o, 0, (size_t)neblock); return 0; }
+      if (cs < 0) {
+        if (!(in[0] & 1) || cs < -255) return (int)BLOSC2_ERROR_RUN_LENGTH;
+        memset(o, -cs, (size_t)neblock);
+        return 0;
+      }
+      if (pos + 4 + cs > srcsize) return (int)BLOSC2_ERROR_READ_BUFFER;
+      if (cs == neblock) { memcpy(o, in, (size_t)neblock); return 0; }
+      blosc2_dparams dpl = dp;
+      const int r = codec.decoder(in, cs, o, neblock, (uint8_t)cmeta, &dpl, src);
+      return r != neblock ? (int)BLOSC2_ERROR_DATA : 0;
+    });
+    if (rc) return rc;
+    if ((rc = to_device(d.stream, unf, img.data(), (size_t)nbytes))) return rc;
+  } else {
+    // device decode of the streams only (the filters follow below)
+    struct Ptrs { const uint8_t* s; uint8_t* o; int32_t ss, ds, status, pad; } h{hb.a.u8(), unf, cbytes, nbytes, 0, 0};
+    uint8_t* sm = d.small.u8();
+    if ((rc = to_device(d.stream, hb.a.p, src, (size_t)cbytes)) || (rc = to_device(d.stream, sm, &h, sizeof h))) return rc;
+    Ptrs* dptr = reinterpret_cast<Ptrs*>(sm);
+    rc = b2h::decompress_batch(reinterpret_cast<const uint8_t* const*>(&dptr->s), &dptr->ss,
+                               reinterpret_cast<uint8_t* const*>(&dptr->o), &dptr->ds, 1, nbytes, &dptr->status, nullptr,
+                               d.stream, d.ws, cbytes, 1);
+    if (rc < 0) return rc;
+    int32_t status = 0;
+    if ((rc = sync_to_host(d.stream, &status, &dptr->status, 4))) return rc;
+    if (status != nbytes) return status < 0 ? status : BLOSC2_ERROR_DATA;
+  }
+  // ---- pipeline_backward, slots 5 -> 0, block 0 first with DELTA ----
+  uint8_t filters[6], fmeta[6];
+  for (int i = 0; i < 6; i++) { filters[i] = s[16 + i]; fmeta[i] = s[24 + i]; }
+  if (s[0] == BLOSC2_VERSION_FORMAT_ALPHA) { filters[5] = 0; fmeta[5] = 0; }
+  bool has_delta = false;
+  for (int i = 0; i < 6; i++) has_delta |= filters[i] == BLOSC_DELTA;
+  std::vector<uint8_t> hs, hd;
+  uint8_t* fin = hb.out.u8();
+  for (int pass = (has_delta && nblocks > 1) ? 1 : 0; pass <= ((has_delta && nblocks > 1) ? 2 : 0); pass++) {
+    uint8_t *cur = unf, *nxt = hb.c.u8();
+    const int32_t b0 = pass == 2 ? 1 : 0, b1 = pass == 1 ? 1 : nblocks;
+    const int64_t lo = (int64_t)b0 * bs, hi = std::min<int64_t>((int64_t)b1 * bs, nbytes);
+    for (int i = 5; i >= 0; i--) {
+      const uint8_t f = filters[i];
+      if (f == BLOSC_NOFILTER || f == BLOSC_TRUNC_PREC || f == b2h::kIntTrunc) continue;   // nothing to undo
+      if (device_filter(f)) {
+        if ((rc = b2h::backward_filter_chunk(f, fmeta[i], ts, nbytes, bs, s[0], pass, cur, nxt, fin, d.stream)) < 0)
+          return rc;
+      } else {
+        blosc2_filter flt{};
+        if (!lookup_filter(f, &flt)) {
+          TRACE_ERROR("User-defined filter %d not found during decompression.", f);
+          return BLOSC2_ERROR_FILTER_PIPELINE;
+        }
+        hs.resize((size_t)nbytes);
+        hd.resize((size_t)nbytes);
+        if ((rc = sync_to_host(d.stream, hs.data() + lo, cur + lo, (size_t)(hi - lo)))) return rc;
+        rc = run_jobs(ctx->nthreads, b1 - b0, [&](int k) {
+          const int32_t b = b0 + k;
+          const int32_t bsize = std::min<int32_t>(bs, nbytes - b * bs);
+          blosc2_dparams dpl = dp;
+          return flt.backward(hs.data() + (int64_t)b * bs, hd.data() + (int64_t)b * bs, bsize, fmeta[i], &dpl, f);
+        });
+        if (rc) { TRACE_ERROR("User-defined filter %d failed during decompression.", f); return rc; }
+        if ((rc = to_device(d.stream, nxt + lo, hd.data() + lo, (size_t)(hi - lo)))) return rc;
+      }
+      std::swap(cur, nxt);
+    }
+    if (hipMemcpyAsync(fin + lo, cur + lo, (size_t)(hi - lo), hipMemcpyDeviceToDevice, d.stream) != hipSuccess)
+      return BLOSC2_ERROR_FAILURE;
+  }
+  if (nbytes > destsize) return BLOSC2_ERROR_WRITE_BUFFER;
+  if (hipStreamSynchronize(d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+  for (int32_t b = 0; b < nblocks; b++) {
+    if (mask && (*mask)[(size_t)b]) continue;
+    const int64_t off = (int64_t)b * bs, len = std::min<int64_t>(bs, nbytes - off);
+    if (hipMemcpy(static_cast<uint8_t*>(dest) + off, fin + off, (size_t)len, hipMemcpyDeviceToHost) != hipSuccess)
+      return BLOSC2_ERROR_FAILURE;
+  }
+  return nbytes;
 }
 
 blosc2_context* g_global_cctx = nullptr;
@@ -785,7 +1216,7 @@ static int special_chunk(const blosc2_cparams& cp, int32_t nbytes, void* dest, i
   b2h::CompressPlan plan;
   int32_t bs = 0;
   const int rc = b2h::make_compress_plan(&plan, nbytes, destsize, cp.clevel, cp.typesize, cp.blocksize, cp.splitmode,
-                                         cp.filters, cp.filters_meta, &bs, true, cp.compcode);
+                                         cp.filters, cp.filters_meta, &bs, true, cp.compcode, cp.compcode_meta);
   if (rc < 0) return rc;
   uint8_t h[BLOSC_EXTENDED_HEADER_LENGTH];
   memset(h, 0, sizeof h);
@@ -872,10 +1303,14 @@ int b2h_compress_batch(const blosc2_cparams* cp, const void* d_src, int32_t chun
   tmp.tuner_id = cp->tuner_id;
   int rc = check_supported(&tmp);
   if (rc < 0) return rc;
+  if (needs_host_callbacks(cp->filters, cp->compcode)) {
+    TRACE_ERROR("user filters / codecs run per chunk through blosc2_compress_ctx, not the device batch API");
+    return BLOSC2_ERROR_FILTER_PIPELINE;
+  }
   b2h::CompressPlan plan;
   int32_t computed = 0;
   rc = b2h::make_compress_plan(&plan, chunk_nbytes, dst_capacity, cp->clevel, cp->typesize, cp->blocksize,
-                               cp->splitmode, cp->filters, cp->filters_meta, &computed, true, cp->compcode);
+                               cp->splitmode, cp->filters, cp->filters_meta, &computed, true, cp->compcode, cp->compcode_meta);
   if (rc < 0) return rc;
   return b2h::compress_batch(plan, static_cast<const uint8_t*>(d_src), src_stride, nchunks,
                              static_cast<uint8_t*>(d_dst), dst_stride, d_cbytes, static_cast<hipStream_t>(stream));

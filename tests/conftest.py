@@ -5,6 +5,7 @@ import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "c-blosc2_amd"))
 
 
 def pytest_configure(config):
