@@ -55,7 +55,8 @@ int compress_batch(const CompressPlan& plan, const uint8_t* d_src, int64_t src_s
 
 // Decompress `n` arbitrary chunks (device pointer arrays).  d_status[i] = nbytes or BLOSC2_ERROR_*.
 // `dst_bound` is an upper bound of the sum of decompressed sizes (sizes the staging scratch).
-// d_maskout (optional, only with n == 1): one byte per block, nonzero = skip (blosc2_set_maskout).
+// d_maskout (optional): one byte per block, nonzero = skip (blosc2_set_maskout); chunk c's mask
+// starts at d_maskout + c * mask_stride (mask_stride 0: one mask shared by every chunk).
 // `src_bound` >= 0: an upper bound of the sum of the chunks' compressed sizes; the block and stream
 // tables are then sized from it (every block has a 4-byte bstart, every stream a 4-byte csize word)
 // and the call never waits on the host (a batch that exceeds the bounds fails per chunk with
@@ -64,7 +65,7 @@ int compress_batch(const CompressPlan& plan, const uint8_t* d_src, int64_t src_s
 int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint8_t* const* d_dst,
                      const int32_t* d_dstsize, int32_t n, int64_t dst_bound, int32_t* d_status,
                      const uint8_t* d_maskout, hipStream_t stream, Workspace* ws = nullptr,
-                     int64_t src_bound = -1, int raw_streams = 0);
+                     int64_t src_bound = -1, int raw_streams = 0, int32_t mask_stride = 0);
 
 // Strided convenience form: chunk i at d_src + i*src_stride with cbytes d_cbytes[i], output at
 // d_dst + i*dst_stride with capacity dst_cap.

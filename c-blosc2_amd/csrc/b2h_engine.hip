@@ -1629,13 +1629,13 @@ __global__ void k_dplan_blocks(const uint8_t* const* __restrict__ srcs, const in
 template <int RLOG>
 __device__ __forceinline__ void decode_stream(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
                                               DChunk* __restrict__ ch, const DStream& st, uint8_t* __restrict__ stage,
-                                              const uint8_t* __restrict__ maskout, B2H_LDS uint8_t* ring,
-                                              int32_t* kind_out) {
+                                              const uint8_t* __restrict__ maskout, int32_t mask_stride,
+                                              B2H_LDS uint8_t* ring, int32_t* kind_out) {
   const int lane = lane_id();
   const int32_t c = st.chunk;
   const DChunk d = ch[c];
   if (d.status < 0 || st.neblock < 0) return;
-  if (maskout && maskout[st.dst_off / d.blocksize]) return;
+  if (maskout && maskout[(int64_t)c * mask_stride + st.dst_off / d.blocksize]) return;
   gin_t in = (gin_t)(srcs[c] + st.src);
   gout_t out = (gout_t)((d.nfilters_bwd ? stage + d.stage_off : dsts[c]) + st.dst_off);
   const int32_t nb = st.neblock;
@@ -1669,8 +1669,8 @@ template <int RLOG>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RLOG == 12 ? 8 : 1, 8))) void k_decode(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
                                                DChunk* __restrict__ ch, const DStream* __restrict__ streams,
                                                uint8_t* __restrict__ stage, const DTotals* __restrict__ tot,
-                                               const uint8_t* __restrict__ maskout, int32_t* __restrict__ next,
-                                               int64_t* __restrict__ dbg) {
+                                               const uint8_t* __restrict__ maskout, int32_t mask_stride,
+                                               int32_t* __restrict__ next, int64_t* __restrict__ dbg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   B2H_LDS uint8_t* ring = (B2H_LDS uint8_t*)smem;
   const int32_t nstreams_total = __builtin_amdgcn_readfirstlane(tot->nstreams);
@@ -1680,7 +1680,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RLOG == 12 ?
     if (s >= nstreams_total) return;
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     int32_t kind = 0;
-    decode_stream<RLOG>(srcs, dsts, ch, streams[s], stage, maskout, ring, &kind);
+    decode_stream<RLOG>(srcs, dsts, ch, streams[s], stage, maskout, mask_stride, ring, &kind);
     if (dbg && lane_id() == 0) {
       dbg[2 * s] = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
       dbg[2 * s + 1] = kind;
@@ -1704,7 +1704,7 @@ __device__ __forceinline__ bool fused_delta_shuffle(const DChunk& d, int32_t bsi
 __device__ __forceinline__ void dfilter_block(DChunk* __restrict__ ch, const DBlock* __restrict__ blocks,
                                               uint8_t* const* __restrict__ dsts, uint8_t* __restrict__ stage,
                                               uint8_t* __restrict__ stage2, int slot, int pass, int32_t idx,
-                                              const uint8_t* __restrict__ maskout) {
+                                              const uint8_t* __restrict__ maskout, int32_t mask_stride) {
   const DBlock bk = blocks[idx];
   if (pass == 1 && bk.block != 0) return;
   if (pass == 2 && bk.block == 0) return;
@@ -1712,7 +1712,7 @@ __device__ __forceinline__ void dfilter_block(DChunk* __restrict__ ch, const DBl
   if (d.status < 0) return;
   const uint8_t f = d.filters[slot];
   if (bwd_noop(f)) return;
-  if (maskout && maskout[bk.block]) return;
+  if (maskout && maskout[(int64_t)bk.chunk * mask_stride + bk.block]) return;
   const bool lo = (bk.block == d.nblocks - 1) && d.leftover;
   const int32_t bsize = lo ? d.leftover : d.blocksize;
   const int64_t off = (int64_t)bk.block * d.blocksize;
@@ -1756,7 +1756,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_dfilter(DChunk* __restrict__ 
                                                            uint8_t* const* __restrict__ dsts, uint8_t* __restrict__ stage,
                                                            uint8_t* __restrict__ stage2, int slot, int pass,
                                                            const DTotals* __restrict__ tot,
-                                                           const uint8_t* __restrict__ maskout) {
+                                                           const uint8_t* __restrict__ maskout, int32_t mask_stride) {
   if (!((tot->slot_mask >> slot) & 1)) return;
   if (!tot->any_delta) {
     if (pass == 2) return;
@@ -1764,7 +1764,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_dfilter(DChunk* __restrict__ 
   }
   const int32_t nb = tot->nblocks;
   for (int32_t idx = blockIdx.x; idx < nb; idx += gridDim.x)
-    dfilter_block(ch, blocks, dsts, stage, stage2, slot, pass, idx, maskout);
+    dfilter_block(ch, blocks, dsts, stage, stage2, slot, pass, idx, maskout, mask_stride);
 }
 
 // memcpyed / special chunks (blosc/blosc2.c:1865-1935): grid (pieces, chunks), chunks strided.
@@ -1815,17 +1815,17 @@ static int dec_ring_log() {
 template <int RLOG>
 static void launch_decode(const uint8_t* const* d_src, uint8_t* const* d_dst, DChunk* ch, const DStream* streams,
                           uint8_t* stage, const DTotals* tot, int64_t nstreams_bound, const uint8_t* d_maskout,
-                          int32_t* next, int64_t* dbg, hipStream_t st) {
+                          int32_t mask_stride, int32_t* next, int64_t* dbg, hipStream_t st) {
   const size_t lds = size_t(1) << RLOG;
   const int slots = resident_slots(reinterpret_cast<const void*>(&k_decode<RLOG>), lds);
   const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(nstreams_bound, slots));
-  k_decode<RLOG><<<grid, 64, lds, st>>>(d_src, d_dst, ch, streams, stage, tot, d_maskout, next, dbg);
+  k_decode<RLOG><<<grid, 64, lds, st>>>(d_src, d_dst, ch, streams, stage, tot, d_maskout, mask_stride, next, dbg);
 }
 
 static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const int32_t* d_srcsize,
                              uint8_t* const* d_dst, const int32_t* d_dstsize, int32_t n, int64_t dst_bound,
                              int32_t* d_status, const uint8_t* d_maskout, hipStream_t st, int64_t src_bound,
-                             int raw_streams = 0) {
+                             int raw_streams = 0, int32_t mask_stride = 0) {
   if (ws->dchunks.ensure(sizeof(DChunk) * (size_t)n) < 0 || ws->dtotals.ensure(sizeof(DTotals)) < 0) return E_MEMORY;
   DChunk* ch = ws->dchunks.as<DChunk>();
   DTotals* tot = ws->dtotals.as<DTotals>();
@@ -1876,10 +1876,10 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
       }
       const int rlog = dec_ring_log();
       uint8_t* stage = ws->stage.as<uint8_t>();
-      if (rlog == 12) launch_decode<12>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, next, dbg, st);
-      else if (rlog == 13) launch_decode<13>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, next, dbg, st);
-      else if (rlog == 14) launch_decode<14>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, next, dbg, st);
-      else launch_decode<15>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, next, dbg, st);
+      if (rlog == 12) launch_decode<12>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, dbg, st);
+      else if (rlog == 13) launch_decode<13>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, dbg, st);
+      else if (rlog == 14) launch_decode<14>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, dbg, st);
+      else launch_decode<15>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, dbg, st);
     }
     ev_decode.stop(st);
     ev_unfilter.start(st);
@@ -1892,7 +1892,7 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
         for (int slot = 5; slot >= 0; slot--)
           if ((h.slot_mask >> slot) & 1)
             k_dfilter<<<grid, kBlockThreads, 0, st>>>(ch, blocks, d_dst, ws->stage.as<uint8_t>(),
-                                                     ws->stage2.as<uint8_t>(), slot, pass, tot, d_maskout);
+                                                     ws->stage2.as<uint8_t>(), slot, pass, tot, d_maskout, mask_stride);
       }
     }
     ev_unfilter.stop(st);
@@ -1912,13 +1912,14 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
 
 int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint8_t* const* d_dst,
                      const int32_t* d_dstsize, int32_t n, int64_t dst_bound, int32_t* d_status,
-                     const uint8_t* d_maskout, hipStream_t st, Workspace* wsx, int64_t src_bound, int raw_streams) {
+                     const uint8_t* d_maskout, hipStream_t st, Workspace* wsx, int64_t src_bound, int raw_streams,
+                     int32_t mask_stride) {
   if (n <= 0) return 0;
   Workspace* ws = wsx ? wsx : ws_for_current_device();
   WsUse use(ws, st);
   if (use.rc) return use.rc;
   return decompress_locked(ws, d_src, d_srcsize, d_dst, d_dstsize, n, dst_bound, d_status, d_maskout, st, src_bound,
-                           raw_streams);
+                           raw_streams, mask_stride);
 }
 
 __global__ void k_fill_ptrs(const uint8_t* src, int64_t src_stride, const int32_t* cbytes, uint8_t* dst, int64_t dst_stride,

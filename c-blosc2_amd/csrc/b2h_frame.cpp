@@ -86,8 +86,11 @@ int upload(b2h_frame* f) {
 }
 
 // Decode `n` chunks of the frame (device copy) into device outputs; status per chunk.
+// With `masks` (n * mask_stride bytes, nonzero = skip the block), only the unmasked blocks of each
+// chunk are decoded (blosc2_set_maskout per chunk, blosc/blosc2.c:1734-1737).
 int decode_chunks(b2h_frame* f, const std::vector<int64_t>& idx, const std::vector<uint8_t*>& outs,
-                  const std::vector<int32_t>& caps, std::vector<int32_t>* status) {
+                  const std::vector<int32_t>& caps, std::vector<int32_t>* status,
+                  const std::vector<uint8_t>* masks = nullptr, int32_t mask_stride = 0) {
   const int32_t n = (int32_t)idx.size();
   if (n == 0) return 0;
   std::vector<const uint8_t*> srcs(n);
@@ -101,7 +104,8 @@ int decode_chunks(b2h_frame* f, const std::vector<int64_t>& idx, const std::vect
     bound += caps[k];
   }
   void* blob = nullptr;
-  const size_t bytes = (size_t)n * (2 * sizeof(void*) + 3 * sizeof(int32_t));
+  const size_t mask_bytes = masks ? masks->size() : 0;
+  const size_t bytes = (size_t)n * (2 * sizeof(void*) + 3 * sizeof(int32_t)) + mask_bytes;
   if (hipMalloc(&blob, bytes) != hipSuccess) return BLOSC2_ERROR_MEMORY_ALLOC;
   uint8_t* b = static_cast<uint8_t*>(blob);
   const uint8_t** d_srcs = reinterpret_cast<const uint8_t**>(b);
@@ -109,7 +113,10 @@ int decode_chunks(b2h_frame* f, const std::vector<int64_t>& idx, const std::vect
   int32_t* d_sizes = reinterpret_cast<int32_t*>(b + (size_t)n * 2 * sizeof(void*));
   int32_t* d_caps = d_sizes + n;
   int32_t* d_status = d_caps + n;
+  uint8_t* d_masks = masks ? reinterpret_cast<uint8_t*>(d_status + n) : nullptr;
   int rc = 0;
+  if (masks && hipMemcpyAsync(d_masks, masks->data(), mask_bytes, hipMemcpyHostToDevice, f->stream) != hipSuccess)
+    rc = BLOSC2_ERROR_FAILURE;
   if (hipMemcpyAsync(d_srcs, srcs.data(), n * sizeof(void*), hipMemcpyHostToDevice, f->stream) != hipSuccess ||
       hipMemcpyAsync(d_dsts, outs.data(), n * sizeof(void*), hipMemcpyHostToDevice, f->stream) != hipSuccess ||
       hipMemcpyAsync(d_sizes, sizes.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, f->stream) != hipSuccess ||
@@ -118,8 +125,8 @@ int decode_chunks(b2h_frame* f, const std::vector<int64_t>& idx, const std::vect
   }
   int64_t src_bound = 0;
   for (int32_t k = 0; k < n; k++) src_bound += sizes[k];
-  if (!rc) rc = b2h::decompress_batch(d_srcs, d_sizes, d_dsts, d_caps, n, bound, d_status, nullptr, f->stream, f->ws,
-                                      src_bound);
+  if (!rc) rc = b2h::decompress_batch(d_srcs, d_sizes, d_dsts, d_caps, n, bound, d_status, d_masks, f->stream, f->ws,
+                                      src_bound, 0, mask_stride);
   status->assign(n, 0);
   if (!rc && hipMemcpyAsync(status->data(), d_status, n * sizeof(int32_t), hipMemcpyDeviceToHost, f->stream) != hipSuccess)
     rc = BLOSC2_ERROR_FAILURE;
@@ -214,6 +221,41 @@ int fill_special(b2h_frame* f, int64_t special, uint8_t* d_dst, int32_t nbytes) 
     return hipGetLastError() == hipSuccess ? 0 : BLOSC2_ERROR_FAILURE;
   }
   return BLOSC2_ERROR_DATA;
+}
+
+// Geometry of a stored chunk from its own header: blocksize, block count, and whether its
+// pipeline holds DELTA (whose blocks >= 1 XOR with block 0, so block 0 is always decoded).
+struct ChunkGeom { int32_t blocksize = 0, nblocks = 0; bool delta = false; };
+ChunkGeom chunk_geom(const b2h_frame* f, int64_t i) {
+  ChunkGeom g;
+  const uint8_t* h = f->host + f->header_len + f->offsets[i];
+  const int32_t nb = le32(h + 4), bs = le32(h + 8);
+  if (bs <= 0 || nb <= 0) return g;
+  g.blocksize = std::min(bs, nb);
+  g.nblocks = nb / g.blocksize + (nb % g.blocksize ? 1 : 0);
+  if ((h[2] & BLOSC_DOSHUFFLE) && (h[2] & BLOSC_DOBITSHUFFLE)) {
+    for (int k = 0; k < 6; k++) g.delta |= h[16 + k] == BLOSC_DELTA;
+  } else {
+    g.delta = (h[2] & BLOSC_DODELTA) != 0;
+  }
+  return g;
+}
+
+// Unmask the blocks of chunk i holding bytes [a, b) (chunk-relative) in m[0 .. stride).
+void unmask_range(const ChunkGeom& g, int64_t a, int64_t b, uint8_t* m) {
+  if (g.blocksize <= 0) return;
+  for (int64_t k = a / g.blocksize; k <= (b - 1) / g.blocksize && k < g.nblocks; k++) m[k] = 0;
+  if (g.delta) m[0] = 0;
+}
+
+// out[dst[k] * ts + j] = scratch[src[k] + j]: the sparse reader's item gather.
+__global__ void k_gather_items(const uint8_t* __restrict__ scratch, const int64_t* __restrict__ src,
+                               const int64_t* __restrict__ dst, int64_t n, int32_t ts, uint8_t* __restrict__ out) {
+  const int64_t total = n * ts;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = i / ts, j = i - k * ts;
+    out[dst[k] * ts + j] = scratch[src[k] + j];
+  }
 }
 
 }  // namespace
@@ -318,9 +360,11 @@ int b2h_frame_decompress_chunk(b2h_frame* f, int64_t nchunk, void* dest, int32_t
 }
 
 // blosc2_schunk_get_slice_buffer (blosc/schunk.c:1662-1760): items [start, stop) of the frame into
-// device memory.  The reference walks the touched chunks one by one (getitem for partial chunks);
-// here the chunks wholly inside the slice decode straight into place and the (at most two) partial
-// edge chunks decode into scratch, all in ONE device batch, then the edges are copied in.
+// device memory.  The reference decodes chunks wholly inside the slice and getitem's the partial
+// edge chunks (which decodes only the touched blocks).  Here the whole chunks decode straight into
+// place and the (at most two) edge chunks decode only their touched blocks (plus block 0 under
+// DELTA) into scratch, all in ONE device batch with per-chunk block masks; the edges are then
+// copied in.
 int b2h_frame_get_slice(b2h_frame* f, int64_t start, int64_t stop, void* d_dst) {
   if (!f || !d_dst) return BLOSC2_ERROR_NULL_POINTER;
   const int64_t ts = f->typesize > 0 ? f->typesize : 1;
@@ -336,6 +380,9 @@ int b2h_frame_get_slice(b2h_frame* f, int64_t start, int64_t stop, void* d_dst) 
   std::vector<int32_t> caps, st;
   struct Edge { uint8_t* from; uint8_t* to; int64_t n; };
   std::vector<Edge> edges;
+  struct Part { int64_t a, b; bool whole; ChunkGeom g; };
+  std::vector<Part> parts;
+  int32_t stride = 0;
   int rc = 0;
   for (int64_t i = c0; i <= c1 && !rc; i++) {
     const int64_t lo = i * cs, n = chunk_nbytes(f, i);
@@ -347,11 +394,23 @@ int b2h_frame_get_slice(b2h_frame* f, int64_t start, int64_t stop, void* d_dst) 
     }
     uint8_t* o = whole ? out + (lo - b0) : scratch + (i == c0 ? 0 : cs);
     if (!whole) edges.push_back({o + (a - lo), out + (a - b0), b - a});
+    const ChunkGeom g = chunk_geom(f, i);
+    stride = std::max(stride, g.nblocks);
+    parts.push_back({a - lo, b - lo, whole, g});
     idx.push_back(i);
     outs.push_back(o);
     caps.push_back((int32_t)n);
   }
-  if (!rc) rc = decode_chunks(f, idx, outs, caps, &st);
+  std::vector<uint8_t> masks((size_t)stride * parts.size(), 0);
+  bool any_masked = false;
+  for (size_t k = 0; k < parts.size(); k++) {
+    if (parts[k].whole || parts[k].g.blocksize <= 0) continue;
+    uint8_t* m = masks.data() + k * (size_t)stride;
+    memset(m, 1, (size_t)parts[k].g.nblocks);
+    unmask_range(parts[k].g, parts[k].a, parts[k].b, m);
+    any_masked = true;
+  }
+  if (!rc) rc = decode_chunks(f, idx, outs, caps, &st, any_masked ? &masks : nullptr, stride);
   for (size_t k = 0; !rc && k < idx.size(); k++)
     if (st[k] != caps[k]) rc = st[k] < 0 ? st[k] : BLOSC2_ERROR_DATA;
   for (const Edge& e : edges) {
@@ -360,6 +419,118 @@ int b2h_frame_get_slice(b2h_frame* f, int64_t start, int64_t stop, void* d_dst) 
   }
   if (hipStreamSynchronize(f->stream) != hipSuccess && !rc) rc = BLOSC2_ERROR_FAILURE;
   (void)hipFree(scratch);
+  return rc;
+}
+
+// blosc2_schunk_get_sparse_buffer (blosc/schunk.c:1921-2110): items at arbitrary coordinates, in
+// coordinate order, into a host buffer.  The reference sorts the coordinates, groups them by
+// (chunk, block) and decodes each touched block with blosc2_decompress_block_ctx on a thread pool
+// (getitem per coordinate under DELTA).  Here every touched chunk of a group goes through ONE
+// device batch with per-chunk block masks (only touched blocks, plus block 0 under DELTA, are
+// decoded), and one gather kernel pulls the items.  Groups bound the scratch to ~1 GiB.
+int b2h_frame_get_sparse_buffer(b2h_frame* f, int64_t ncoords, const int64_t* coords, void* buffer) {
+  if (!f) return BLOSC2_ERROR_INVALID_PARAM;
+  if (ncoords < 0) return BLOSC2_ERROR_INVALID_PARAM;
+  if (ncoords == 0) return BLOSC2_ERROR_SUCCESS;
+  if (!coords || !buffer) return BLOSC2_ERROR_INVALID_PARAM;
+  if (f->typesize <= 0 || f->chunksize <= 0 || f->blocksize <= 0) return BLOSC2_ERROR_INVALID_PARAM;
+  if (f->chunksize % f->typesize || f->blocksize % f->typesize) return BLOSC2_ERROR_INVALID_PARAM;
+  const int64_t ts = f->typesize, cs = f->chunksize, nitems = f->nbytes / ts, chunk_nitems = cs / ts;
+  for (int64_t i = 0; i < ncoords; i++)
+    if (coords[i] < 0 || coords[i] >= nitems) return BLOSC2_ERROR_INVALID_PARAM;
+  // coordinate order sorted by chunk (stable: equal chunks keep the caller's order)
+  std::vector<int64_t> order((size_t)ncoords);
+  for (int64_t i = 0; i < ncoords; i++) order[(size_t)i] = i;
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int64_t x, int64_t y) { return coords[x] / chunk_nitems < coords[y] / chunk_nitems; });
+  const int64_t group_max = std::max<int64_t>(1, std::min<int64_t>(4096, (int64_t(1) << 30) / cs));
+  uint8_t *scratch = nullptr, *d_out = nullptr;
+  int64_t* d_idx = nullptr;
+  int rc = 0;
+  if (hipMalloc(&d_out, (size_t)(ncoords * ts)) != hipSuccess) return BLOSC2_ERROR_MEMORY_ALLOC;
+  size_t scratch_bytes = 0, idx_cap = 0;
+  for (size_t pos = 0; pos < order.size() && !rc;) {
+    // one group: up to group_max distinct chunks
+    std::vector<int64_t> idx;
+    std::vector<uint8_t*> outs;
+    std::vector<int32_t> caps, st;
+    std::vector<ChunkGeom> geo;
+    std::vector<int64_t> src, dst;
+    std::vector<int32_t> kof;                              // per item: decoded-chunk index, -1 special
+    std::vector<int64_t> dslot;                            // per decoded chunk: its scratch slot
+    std::vector<std::pair<int64_t, int64_t>> specials;   // (chunk, slot)
+    size_t end = pos;
+    int64_t nslots = 0;
+    while (end < order.size()) {
+      const int64_t c = coords[order[end]] / chunk_nitems;
+      if (nslots == group_max) break;
+      size_t e2 = end;
+      while (e2 < order.size() && coords[order[e2]] / chunk_nitems == c) e2++;
+      const int64_t slot = nslots++;
+      int32_t kk = -1;
+      if (f->offsets[c] < 0) {
+        specials.push_back({c, slot});
+      } else {
+        kk = (int32_t)idx.size();
+        idx.push_back(c);
+        caps.push_back(chunk_nbytes(f, c));
+        geo.push_back(chunk_geom(f, c));
+        dslot.push_back(slot);
+      }
+      for (size_t k = end; k < e2; k++) {
+        src.push_back(slot * cs + (coords[order[k]] % chunk_nitems) * ts);
+        dst.push_back(order[k]);
+        kof.push_back(kk);
+      }
+      end = e2;
+    }
+    if ((size_t)(nslots * cs) > scratch_bytes) {
+      if (scratch) (void)hipFree(scratch);
+      scratch_bytes = (size_t)(nslots * cs);
+      if (hipMalloc(&scratch, scratch_bytes) != hipSuccess) { scratch = nullptr; rc = BLOSC2_ERROR_MEMORY_ALLOC; break; }
+    }
+    for (int64_t sl : dslot) outs.push_back(scratch + sl * cs);
+    for (auto& sp : specials) {
+      if (rc) break;
+      rc = fill_special(f, f->offsets[sp.first], scratch + sp.second * cs, chunk_nbytes(f, sp.first));
+    }
+    int32_t stride = 0;
+    for (auto& g : geo) stride = std::max(stride, g.nblocks);
+    std::vector<uint8_t> masks((size_t)stride * idx.size(), 1);
+    for (size_t q = 0; q < kof.size(); q++) {   // touched blocks, per decoded chunk
+      if (kof[q] < 0) continue;                  // special chunk: filled whole
+      const int64_t byte = src[q] % cs;
+      unmask_range(geo[(size_t)kof[q]], byte, byte + ts, masks.data() + (size_t)kof[q] * (size_t)stride);
+    }
+    if (!rc) rc = decode_chunks(f, idx, outs, caps, &st, &masks, stride);
+    for (size_t k = 0; !rc && k < idx.size(); k++)
+      if (st[k] != caps[k]) rc = st[k] < 0 ? st[k] : BLOSC2_ERROR_FAILURE;
+    const int64_t n = (int64_t)src.size();
+    if (!rc && (size_t)(2 * n) > idx_cap) {
+      if (d_idx) (void)hipFree(d_idx);
+      idx_cap = (size_t)(2 * n);
+      if (hipMalloc(reinterpret_cast<void**>(&d_idx), idx_cap * sizeof(int64_t)) != hipSuccess) {
+        d_idx = nullptr;
+        rc = BLOSC2_ERROR_MEMORY_ALLOC;
+      }
+    }
+    if (!rc && (hipMemcpyAsync(d_idx, src.data(), (size_t)n * 8, hipMemcpyHostToDevice, f->stream) != hipSuccess ||
+                hipMemcpyAsync(d_idx + n, dst.data(), (size_t)n * 8, hipMemcpyHostToDevice, f->stream) != hipSuccess))
+      rc = BLOSC2_ERROR_FAILURE;
+    if (!rc) {
+      const int64_t total = n * ts;
+      const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 4096));
+      k_gather_items<<<grid, 256, 0, f->stream>>>(scratch, d_idx, d_idx + n, n, (int32_t)ts, d_out);
+      if (hipGetLastError() != hipSuccess) rc = BLOSC2_ERROR_FAILURE;
+    }
+    // the host vectors of this group are re-used next round: drain the stream first
+    if (hipStreamSynchronize(f->stream) != hipSuccess && !rc) rc = BLOSC2_ERROR_FAILURE;
+    pos = end;
+  }
+  if (!rc && hipMemcpy(buffer, d_out, (size_t)(ncoords * ts), hipMemcpyDeviceToHost) != hipSuccess) rc = BLOSC2_ERROR_FAILURE;
+  if (scratch) (void)hipFree(scratch);
+  if (d_idx) (void)hipFree(d_idx);
+  (void)hipFree(d_out);
   return rc;
 }
 

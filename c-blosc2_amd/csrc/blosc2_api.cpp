@@ -911,6 +911,81 @@ int blosc2_decompress_ctx(blosc2_context* context, const void* src, int32_t srcs
   return decompress_host(context, src, srcsize, dest, destsize, has_mask ? &mask : nullptr);
 }
 
+// blosc2_decompress_block_ctx (blosc/blosc2.c:4580-4687; declared in blosc-private.h:29 and used
+// by the sparse reader, schunk.c:1858): block `nblock` of a chunk into dest, returning its size.
+// The block is carved out as a one-block chunk (header with nbytes = blocksize = the block's size,
+// one bstart, the block's streams) and decoded on the device.  Being block 0 of that chunk, a
+// DELTA pipeline decodes it against itself -- exactly the reference's serial result, where
+// blosc_d runs with dest_offset 0 (delta_decoder's offset == 0 branch, delta.c:96-100).  A
+// leftover last block is never split (blosc_d), so its carved header sets DONT_SPLIT.
+int blosc2_decompress_block_ctx(blosc2_context* context, const void* src, int32_t srcsize, int32_t nblock, void* dest,
+                                int32_t destsize) {
+  if (!context || !src) return BLOSC2_ERROR_NULL_POINTER;
+  int32_t nbytes, cbytes, bs;
+  int rc = peek_header(src, srcsize, &nbytes, &cbytes, &bs);
+  if (rc < 0) return rc;
+  const uint8_t* s = static_cast<const uint8_t*>(src);
+  const bool ext = (s[2] & BLOSC_DOSHUFFLE) && (s[2] & BLOSC_DOBITSHUFFLE);
+  const int32_t ovh = ext ? BLOSC_EXTENDED_HEADER_LENGTH : BLOSC_MIN_HEADER_LENGTH;
+  if (srcsize < ovh || cbytes > srcsize) return BLOSC2_ERROR_READ_BUFFER;
+  if (ext && (s[BLOSC2_CHUNK_BLOSC2_FLAGS2] & BLOSC2_VL_BLOCKS)) {
+    TRACE_ERROR("block decompression is not supported for VL-block chunks.");
+    return BLOSC2_ERROR_INVALID_PARAM;
+  }
+  const int special = ext ? (s[BLOSC2_CHUNK_BLOSC2_FLAGS] >> 4) & BLOSC2_SPECIAL_MASK : 0;
+  if (special > BLOSC2_SPECIAL_LASTID) {
+    TRACE_ERROR("Unknown special values ID (%d) ", special);
+    return BLOSC2_ERROR_DATA;
+  }
+  // blosc2_calculate_blocks: nblocks = ceil(nbytes / blocksize), leftover = nbytes % blocksize
+  const int32_t nblocks = nbytes / bs + (nbytes % bs ? 1 : 0);
+  if (nblock < 0 || nblock >= nblocks) {
+    TRACE_ERROR("`nblock` out of bounds.");
+    return BLOSC2_ERROR_INVALID_PARAM;
+  }
+  const bool memcpyed = (s[2] & BLOSC_MEMCPYED) || special;
+  if (!memcpyed && (int64_t)ovh + 4 * (int64_t)nblocks > srcsize) {
+    TRACE_ERROR("`bstarts` out of bounds.");
+    return BLOSC2_ERROR_READ_BUFFER;
+  }
+  const bool leftover = nblock == nblocks - 1 && nbytes % bs > 0;
+  const int32_t bsize = leftover ? nbytes % bs : bs;
+  if (destsize < bsize) {
+    TRACE_ERROR("Destination is too small for block.");
+    return BLOSC2_ERROR_WRITE_BUFFER;
+  }
+  std::vector<uint8_t> one;
+  auto put32 = [&](size_t at, int32_t v) { memcpy(one.data() + at, &v, 4); };
+  if (special) {                      // header (+ the repeated value) only
+    one.assign(s, s + cbytes);
+  } else if (s[2] & BLOSC_MEMCPYED) {   // the block's raw bytes
+    const int64_t at = (int64_t)ovh + (int64_t)nblock * bs;
+    if (at + bsize > cbytes) return BLOSC2_ERROR_READ_BUFFER;
+    one.assign(s, s + ovh);
+    one.insert(one.end(), s + at, s + at + bsize);
+  } else {                            // one bstart + the block's streams
+    const int32_t b0 = rd32(s + ovh + 4 * nblock);
+    if (b0 < ovh + 4 * nblocks || b0 >= cbytes) return BLOSC2_ERROR_READ_BUFFER;
+    int32_t b1 = cbytes;              // the next stored block (threaded writers store blocks out of order)
+    for (int32_t k = 0; k < nblocks; k++) {
+      const int32_t o = rd32(s + ovh + 4 * k);
+      if (o > b0 && o < b1) b1 = o;
+    }
+    one.assign(s, s + ovh);
+    one.resize((size_t)ovh + 4);
+    put32((size_t)ovh, ovh + 4);
+    one.insert(one.end(), s + b0, s + b1);
+    if (leftover) one[2] |= 0x10;   // dont_split, bit 4 of the flags (blosc/blosc2.c:1719)
+  }
+  put32(4, bsize);
+  put32(8, bsize);
+  if (!special) put32(12, (int32_t)one.size());
+  std::lock_guard<std::mutex> g(context->mu);
+  rc = decompress_host(context, one.data(), (int32_t)one.size(), dest, destsize, nullptr);
+  if (rc < 0) return rc;
+  return bsize;
+}
+
 // blosc/blosc2.c:4265-4474 / 4541-4550: decode only the blocks overlapping [start, start+nitems)
 int blosc2_getitem_ctx(blosc2_context* context, const void* src, int32_t srcsize, int start, int nitems, void* dest,
                        int32_t destsize) {

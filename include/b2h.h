@@ -101,6 +101,14 @@ BLOSC_EXPORT int b2h_frame_decompress_chunk(b2h_frame *frame, int64_t nchunk, vo
  * BLOSC2_ERROR_* code (INVALID_PARAM for a range outside the frame).  Synchronous. */
 BLOSC_EXPORT int b2h_frame_get_slice(b2h_frame *frame, int64_t start, int64_t stop, void *d_dst);
 
+/* blosc2_schunk_get_sparse_buffer (ref blosc/schunk.c:1921-2110, include/blosc2.h): the items at
+ * coords[0 .. ncoords) (item indices), in that order, into the HOST buffer (ncoords * typesize
+ * bytes).  Only the blocks holding a coordinate (plus block 0 under DELTA) are decoded, all touched
+ * chunks in one device batch per group.  Errors as the reference: BLOSC2_ERROR_INVALID_PARAM for
+ * negative ncoords, NULL coords/buffer, out-of-range coordinates, non-positive typesize /
+ * chunksize / blocksize, or sizes that are not multiples of typesize. */
+BLOSC_EXPORT int b2h_frame_get_sparse_buffer(b2h_frame *frame, int64_t ncoords, const int64_t *coords, void *buffer);
+
 /* BloscLZ encoder mode (process-wide), returns the previous one.
  *   0 exact (default): byte-identical to blosclz_compress (blosc/blosclz.c:422-619).
  *   1 fast: same token grammar, greedy rule, limits, entropy-probe thresholds and emission, but the

@@ -352,6 +352,11 @@ BLOSC_EXPORT int blosc2_compress_ctx(blosc2_context *context, const void *src, i
                                      int32_t destsize);
 BLOSC_EXPORT int blosc2_decompress_ctx(blosc2_context *context, const void *src, int32_t srcsize, void *dest,
                                        int32_t destsize);
+/* one block of a chunk (ref blosc/blosc2.c:4580-4687; declared in blosc/blosc-private.h:29 and
+ * exported by the reference library; the sparse reader's per-block decode, schunk.c:1858).
+ * Returns the block's size or a BLOSC2_ERROR_* code. */
+BLOSC_EXPORT int blosc2_decompress_block_ctx(blosc2_context *context, const void *src, int32_t srcsize, int32_t nblock,
+                                             void *dest, int32_t destsize);
 /* partial decode: include/blosc2.h:1698 (blosc2_getitem_ctx), 722 (blosc2_getitem) */
 BLOSC_EXPORT int blosc2_getitem_ctx(blosc2_context *context, const void *src, int32_t srcsize, int start, int nitems,
                                     void *dest, int32_t destsize);
