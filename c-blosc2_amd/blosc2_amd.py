@@ -75,6 +75,7 @@ def _bind(lib):
         "blosc2_cbuffer_sizes": ([vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)], C.c_int),
         "blosc2_get_version_string": ([], C.c_char_p),
         "b2h_compress_batch": ([C.POINTER(CParams), vp, i32, i32, i64, vp, i64, i32, vp, vp], C.c_int),
+        "b2h_compress_batch_sizes": ([C.POINTER(CParams), vp, vp, i32, i64, vp, i64, i32, vp, vp], C.c_int),
         "b2h_decompress_batch": ([vp, i64, vp, i32, vp, i64, i32, vp, vp], C.c_int),
         "b2h_pack_chunks": ([vp, i64, vp, i32, vp, vp, vp], C.c_int),
         "b2h_unpack_chunks": ([vp, vp, i32, vp, i64, vp, vp], C.c_int),
@@ -163,6 +164,17 @@ def compress_batch(cp: CParams, d_src: int, chunk_nbytes: int, nchunks: int, src
                                   C.c_void_p(stream))
     if rc < 0:
         raise RuntimeError(f"b2h_compress_batch: {rc} {lib().b2h_last_error()}")
+
+
+def compress_batch_sizes(cp: CParams, d_src: int, nbytes, src_stride: int, d_dst: int, dst_stride: int,
+                         dst_capacity: int, d_cbytes: int, stream: int = 0):
+    """Chunks of per-chunk sizes (host sequence `nbytes`), e.g. a super-chunk's ragged tail."""
+    sizes = (C.c_int32 * len(nbytes))(*nbytes)
+    rc = lib().b2h_compress_batch_sizes(C.byref(cp), C.c_void_p(d_src), sizes, len(nbytes), src_stride,
+                                        C.c_void_p(d_dst), dst_stride, dst_capacity, C.c_void_p(d_cbytes),
+                                        C.c_void_p(stream))
+    if rc < 0:
+        raise RuntimeError(f"b2h_compress_batch_sizes: {rc} {lib().b2h_last_error()}")
 
 
 def decompress_batch(d_src: int, src_stride: int, d_cbytes: int, nchunks: int, d_dst: int,

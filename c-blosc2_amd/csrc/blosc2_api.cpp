@@ -1391,6 +1391,34 @@ int b2h_compress_batch(const blosc2_cparams* cp, const void* d_src, int32_t chun
                              static_cast<uint8_t*>(d_dst), dst_stride, d_cbytes, static_cast<hipStream_t>(stream));
 }
 
+// Chunks of per-chunk sizes (a super-chunk's ragged last chunk: blosc2_schunk_append_buffer,
+// blosc/schunk.c:1459-1477, compresses every chunk into nbytes + BLOSC2_MAX_OVERHEAD).  Runs of
+// equal sizes share one plan and one engine batch; all batches are queued on `stream` back to
+// back with no host wait.  dst_capacity <= 0: each chunk's own nbytes + BLOSC2_MAX_OVERHEAD.
+int b2h_compress_batch_sizes(const blosc2_cparams* cp, const void* d_src, const int32_t* nbytes, int32_t nchunks,
+                             int64_t src_stride, void* d_dst, int64_t dst_stride, int32_t dst_capacity,
+                             int32_t* d_cbytes, void* stream) {
+  if (!cp || (nchunks > 0 && !nbytes)) return BLOSC2_ERROR_NULL_POINTER;
+  if (nchunks < 0) return BLOSC2_ERROR_INVALID_PARAM;
+  for (int32_t i = 0; i < nchunks; i++) {
+    if (nbytes[i] < 0 || (int64_t)nbytes[i] > src_stride) return BLOSC2_ERROR_INVALID_PARAM;
+    const int64_t cap = dst_capacity > 0 ? dst_capacity : (int64_t)nbytes[i] + BLOSC2_MAX_OVERHEAD;
+    if (cap > dst_stride && nchunks > 1) return BLOSC2_ERROR_INVALID_PARAM;   // outputs would overlap
+  }
+  const uint8_t* src = static_cast<const uint8_t*>(d_src);
+  uint8_t* dst = static_cast<uint8_t*>(d_dst);
+  for (int32_t i = 0; i < nchunks;) {
+    int32_t j = i + 1;
+    while (j < nchunks && nbytes[j] == nbytes[i]) j++;
+    const int32_t cap = dst_capacity > 0 ? dst_capacity : nbytes[i] + BLOSC2_MAX_OVERHEAD;
+    const int rc = b2h_compress_batch(cp, src + (int64_t)i * src_stride, nbytes[i], j - i, src_stride,
+                                      dst + (int64_t)i * dst_stride, dst_stride, cap, d_cbytes + i, stream);
+    if (rc < 0) return rc;
+    i = j;
+  }
+  return 0;
+}
+
 int b2h_decompress_batch(const void* d_src, int64_t src_stride, const int32_t* d_cbytes, int32_t nchunks, void* d_dst,
                          int64_t dst_stride, int32_t dst_capacity, int32_t* d_status, void* stream) {
   return b2h::decompress_batch_strided(static_cast<const uint8_t*>(d_src), src_stride, d_cbytes, nchunks,

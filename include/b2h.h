@@ -30,6 +30,15 @@ BLOSC_EXPORT int b2h_compress_batch(const blosc2_cparams *cparams, const void *d
                                     int32_t nchunks, int64_t src_stride, void *d_dst, int64_t dst_stride,
                                     int32_t dst_capacity, int32_t *d_cbytes, void *stream);
 
+/* Chunks of per-chunk sizes nbytes[i] (HOST array), e.g. a super-chunk whose last chunk is short:
+ * chunk i = d_src + i*src_stride, output at d_dst + i*dst_stride, capacity dst_capacity (<= 0:
+ * nbytes[i] + BLOSC2_MAX_OVERHEAD, the destsize blosc2_schunk_append_buffer uses, ref
+ * blosc/schunk.c:1459-1477).  Runs of equal sizes go through one engine batch each, queued back
+ * to back on `stream` without any host wait.  Byte-identical per chunk to blosc2_compress_ctx. */
+BLOSC_EXPORT int b2h_compress_batch_sizes(const blosc2_cparams *cparams, const void *d_src, const int32_t *nbytes,
+                                          int32_t nchunks, int64_t src_stride, void *d_dst, int64_t dst_stride,
+                                          int32_t dst_capacity, int32_t *d_cbytes, void *stream);
+
 /* Decompress chunk i = d_src + i*src_stride (d_cbytes[i] bytes, at most src_stride: chunks do not
  * overlap) into d_dst + i*dst_stride (capacity dst_capacity).  d_status[i] = decompressed bytes or
  * BLOSC2_ERROR_*.  Stream-ordered: never waits on the host (the plan tables are sized from

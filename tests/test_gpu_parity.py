@@ -239,6 +239,52 @@ def test_device_batch_matches_per_chunk(B):
             assert torch.equal(dout, dsrc)
 
 
+def test_ragged_batch_matches_oracle_without_host_wait(B):
+    """b2h_compress_batch_sizes: a super-chunk's chunks with a short last one (ref
+    blosc2_schunk_append_buffer, blosc/schunk.c:1459-1477: destsize nbytes + 32 per chunk) ride in
+    one call, byte-identical per chunk to the oracle, queued without a host wait; the strided batch
+    decompression restores every chunk, the short one included."""
+    import time
+    import torch
+    chunk, nfull, tail = 1 << 20, 6, 123_457 * 4
+    sizes = [chunk] * nfull + [tail]
+    host = gen_f32(3, (nfull * chunk + tail) // 4)
+    raw = host.view(np.uint8)
+    stride = chunk + 256
+    dsrc = torch.zeros(len(sizes) * stride, dtype=torch.uint8, device="cuda")
+    for i, n in enumerate(sizes):
+        dsrc[i * stride:i * stride + n] = torch.from_numpy(raw[i * chunk:i * chunk + n].copy()).cuda()
+    ddst = torch.zeros(len(sizes) * stride, dtype=torch.uint8, device="cuda")
+    dcb = torch.zeros(len(sizes), dtype=torch.int32, device="cuda")
+    for kw in (dict(clevel=5, typesize=4, filters=(0, 0, 0, 0, 0, 1)),
+               dict(clevel=9, typesize=4, filters=(0, 0, 0, 0, 3, 1), blocksize=65536)):
+        cp = B.cparams(**kw)
+        s = torch.cuda.Stream()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            torch.cuda._sleep(200_000_000)   # keep the stream busy: a host wait inside would block here
+            t0 = time.perf_counter()
+            B.compress_batch_sizes(cp, dsrc.data_ptr(), sizes, stride, ddst.data_ptr(), stride, 0, dcb.data_ptr(),
+                                   s.cuda_stream)
+            queued = time.perf_counter() - t0
+        s.synchronize()
+        assert queued < 0.05, queued
+        cbytes = dcb.cpu().numpy()
+        out = ddst.cpu().numpy()
+        for i, n in enumerate(sizes):
+            want = oracle_compress(raw[i * chunk:i * chunk + n].copy().view(np.float32), **kw)
+            assert cbytes[i] == want.nbytes and np.array_equal(out[i * stride:i * stride + cbytes[i]], want), (kw, i)
+        dout = torch.zeros(len(sizes) * chunk, dtype=torch.uint8, device="cuda")
+        dst = torch.zeros(len(sizes), dtype=torch.int32, device="cuda")
+        B.decompress_batch(ddst.data_ptr(), stride, dcb.data_ptr(), len(sizes), dout.data_ptr(), chunk, chunk,
+                           dst.data_ptr())
+        torch.cuda.synchronize()
+        assert list(dst.cpu().numpy()) == sizes
+        back = dout.cpu().numpy()
+        for i, n in enumerate(sizes):
+            assert np.array_equal(back[i * chunk:i * chunk + n], raw[i * chunk:i * chunk + n]), i
+
+
 @pytest.mark.slow
 def test_c2_shuffle_256mib_roundtrip(B):
     """C2 at full size: 256 MiB float32 shuffle ts=4 on device vs a numpy transpose (bit-exact)."""
