@@ -192,7 +192,7 @@ int debug_decode_cycles(void* host, int32_t n) {
 
 // Resident single-wave workgroups of `fn` with `lds` bytes of dynamic LDS (the grid size of the
 // persistent work-pulling kernels), cached per (fn, lds).
-static int resident_slots(const void* fn, size_t lds) {
+static int resident_slots(const void* fn, size_t lds, int block = 64) {
   static std::mutex m;
   static std::vector<std::pair<std::pair<const void*, size_t>, int>> cache;
   std::lock_guard<std::mutex> g(m);
@@ -201,7 +201,7 @@ static int resident_slots(const void* fn, size_t lds) {
   int dev = 0, per_cu = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, lds) != hipSuccess) per_cu = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, lds) != hipSuccess) per_cu = 1;
   const int slots = std::max(1, per_cu) * std::max(1, ncu);
   cache.push_back({{fn, lds}, slots});
   return slots;
@@ -437,18 +437,27 @@ __global__ __launch_bounds__(64 * (NLDS + NGLB)) void k_encode(CGeom g, const ui
 }
 
 // ------------------------------------------------------------------ BloscLZ fast mode ----
-// One wave per workgroup (persistent, pulling streams like k_encode), the LDS holding the wave's
-// u32 hash table (2^tablog entries) and its output ring.  b2h_lzfast.h has the algorithm.
+// One stream per workgroup of two waves: wave 0 matches, wave 1 parses (b2h_lzfast.h);
+// persistent, pulling streams like k_encode.  LDS per workgroup: table + output ring + hand-over
+// slots.
+__host__ __device__ constexpr size_t fast_lds(size_t pos_bytes, int tablog) {
+  return (pos_bytes << tablog) + kOutRing + ((sizeof(FastShared) + 15) & ~size_t(15));
+}
 template <typename POS>
-__global__ __launch_bounds__(64) void k_encode_fast(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
-                                                    StreamResult* __restrict__ res, int32_t nstreams_total,
-                                                    int32_t* __restrict__ next, int tablog,
-                                                    const int32_t* __restrict__ porder) {
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4, 8)))   // <= 128 VGPRs: 16 waves per CU
+void k_encode_fast(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
+                   StreamResult* __restrict__ res, int32_t nstreams_total, int32_t* __restrict__ next, int tablog,
+                   const int32_t* __restrict__ porder) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   B2H_LDS uint8_t* tab = (B2H_LDS uint8_t*)smem;
   B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + (sizeof(POS) << tablog));
+  B2H_LDS FastShared* sh = (B2H_LDS FastShared*)(smem + (sizeof(POS) << tablog) + kOutRing);
+  const bool matcher = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
   for (;;) {
-    const int32_t i = __builtin_amdgcn_readfirstlane(atomicAdd(next, lane_id() == 0 ? 1 : 0));
+    if (threadIdx.x == 0) sh->pull = atomicAdd(next, 1);
+    __syncthreads();
+    const int32_t i = __builtin_amdgcn_readfirstlane(sh->pull);
+    __syncthreads();
     if (i >= nstreams_total) return;
     const int32_t s = __builtin_amdgcn_readfirstlane(pull_to_stream(g, porder, g.front, i, nstreams_total));
     const int32_t c = s / g.nsc, l = s - c * g.nsc;
@@ -458,10 +467,11 @@ __global__ __launch_bounds__(64) void k_encode_fast(CGeom g, const uint8_t* __re
     gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
-    StreamResult r = encode_stream_fast<POS>(in, len, g.clevel, out, tab, tablog, oring, g.overhead == kHdrExt);
+    StreamResult r = encode_stream_fast<POS>(in, len, g.clevel, out, tab, tablog, oring, sh, g.overhead == kHdrExt,
+                                             matcher);
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
-    if (lane_id() == 0) res[s] = r;
+    if (!matcher && lane_id() == 0) res[s] = r;
   }
 }
 
@@ -495,16 +505,16 @@ static int launch_encode_fast_t(Workspace* ws, const CGeom& g, const uint8_t* fi
                                 int32_t* next, const int32_t* porder, hipStream_t st) {
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
   const int tablog = std::min(fast_tablog(), hashlog);
-  const size_t lds = (sizeof(POS) << tablog) + kOutRing;
+  const size_t lds = fast_lds(sizeof(POS), tablog);
   const void* fn = reinterpret_cast<const void*>(&k_encode_fast<POS>);
   static bool attr_set = false;
   if (!attr_set) {   // > 64 KiB of dynamic LDS (u32, tablog 14): opt in once
     HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  const int slots = resident_slots(fn, lds);
+  const int slots = resident_slots(fn, lds, 128);
   const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(ntot, slots));
-  k_encode_fast<POS><<<grid, 64, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog, porder);
+  k_encode_fast<POS><<<grid, 128, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog, porder);
   HIPCHK(hipGetLastError());
   return 0;
 }

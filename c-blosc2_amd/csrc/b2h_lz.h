@@ -640,6 +640,28 @@ __device__ __forceinline__ bool wave_is_run(gin_t s, int32_t n) {
   return true;
 }
 
+// Whether s[from, n) is all `first` (the second half of a split run test).
+__device__ __forceinline__ bool wave_is_run_from(gin_t s, int32_t from, int32_t n, uint8_t first) {
+  const int lane = lane_id();
+  const uint32_t rep = first * 0x01010101u;
+  const bool aligned = (reinterpret_cast<uintptr_t>(s + from) & 15) == 0;
+  for (int32_t base = from; base < n; base += 64 * 64) {
+    bool bad = false;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int32_t i = base + (u * 64 + lane) * 16;
+      if (aligned && i + 16 <= n) {
+        const B2H_GLB uint32_t* w = reinterpret_cast<const B2H_GLB uint32_t*>(s + i);
+        bad |= (w[0] != rep) | (w[1] != rep) | (w[2] != rep) | (w[3] != rep);
+      } else {
+        for (int32_t k = i; k < min(i + 16, n); k++) bad |= s[k] != first;
+      }
+    }
+    if (__ballot(bad)) return false;
+  }
+  return true;
+}
+
 // Full per-stream encode with maxout = neblock: run test, entropy probe, main pass.
 template <typename TAB>
 __device__ __forceinline__ StreamResult encode_stream(gin_t in, int32_t n, int clevel, gout_t out,

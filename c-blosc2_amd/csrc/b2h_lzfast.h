@@ -6,21 +6,20 @@
 // only the positions its serial walk visits, so every candidate depends on the whole parse before
 // it and the walk is a latency chain (exact mode, b2h_lz.h, ~9 000 cycles per 64 positions on T's
 // smooth plane).  Fast mode inserts positions in TILES of 64, in tile order, independently of the
-// parse (semantics and their CPU model: tools/fm_model.c):
+// parse (semantics and their CPU model: tools/fm_model.c): entering tile T, the parse inserts T
+// (if a jump skipped it) and T + 1; tiles a long match jumps over are never inserted.
 //
 //   * one LDS atomic exchange per lane swaps the lane's position into its bucket and returns the
 //     bucket's previous position -- the most recent earlier position with that hash, earlier lanes
 //     of the same tile included (LDS applies the lanes of one instruction in lane order);
 //   * so a tile's candidates, their 60-byte compares and match lengths are known before the parse
-//     reaches it: the kernel software-pipelines tiles T (compare + parse), T + 1 (table exchange +
-//     candidate loads) and T + 2 (input loads), and the parse itself is the exact-mode window code
-//     (ballot chain walk, DPP prefix-sum emission through the LDS output ring) started at the
-//     parse position's lane;
-//   * a match that jumps past tile T + 1 restarts the pipeline at its end (the tiles it covers are
-//     never inserted, like the reference's skipped positions).
+//     reaches it.  Two waves of a workgroup share one stream's table: the MATCHER exchanges and
+//     compares tile T + 1 while the PARSER parses tile T with the exact-mode window code (ballot
+//     chain walk, DPP prefix-sum emission through the LDS output ring), the two meeting at one
+//     barrier per tile.
 //
 // Every match is verified byte for byte against its candidate, so any output decodes with
-// blosclz_decompress; the ratio on T is the reference's (2^13 table) or better (2^14).
+// blosclz_decompress; the ratio on T is within 0.1 % of the reference's.
 #pragma once
 #include "b2h_lz.h"
 
@@ -77,301 +76,315 @@ __device__ __forceinline__ void rawc_load(gin_t p, RawCmp& r) {
 }
 __device__ __forceinline__ uint32_t rawc_word(const RawCmp& r, int i) { return funnel(r.d[i], r.d[i + 1], r.sh); }
 
+// ============================================================ matcher / parser workgroup ====
+// One stream per workgroup of two waves (k_encode_fast):
+//   wave 0, the MATCHER: tile exchanges, candidate loads and 60-byte compares -- for each lane of a
+//     tile its candidate distance, first mismatch and input byte, handed over through LDS;
+//   wave 1, the PARSER: chain walk, token emission, output ring and flushes.
+// Lockstep, one barrier per tile.  A match jumping past tile T + 1 costs one step in which the
+// matcher produces the jump target and the parser waits.  The split keeps each wave within 128
+// VGPRs, so a CU holds 8 streams x 2 waves (measured: the encoder is issue-bound at that
+// occupancy, so a deeper matcher pipeline -- exchange T + 2 while comparing T + 1 -- ran slower).
+struct FastShared {          // per workgroup, after the table and the output ring
+  uint32_t dist[2][64];      // hand-over slots: candidate distance
+  uint32_t aux[2][64];       //   (first mismatch + 1) | input byte << 8 (mismatch + 1 == 0: no candidate)
+  int32_t ctrl[2];           // parser -> matcher: next tile, or -1 (stop); by iteration parity
+  int32_t decide[2];         // the stream's probe decision / run verdict (parser -> both)
+  int32_t pull;              // the stream index the workgroup pulled
+};
+
 template <bool PROBE, typename POS>
 __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int probe_hashlog, int tablog, gout_t out,
-                                                  int32_t maxout, B2H_LDS uint8_t* tab, B2H_LDS uint8_t* oring,
-                                                  int clevel) {
+                                                   int32_t maxout, B2H_LDS uint8_t* tab, B2H_LDS uint8_t* oring,
+                                                   B2H_LDS FastShared* sh, int clevel, bool matcher) {
   const int lane = lane_id();
   constexpr int32_t ORM = kOutRing - 1;
-  int32_t F = 0;   // output [0, F) already in `out`
-  auto flush = [&](int32_t to) {
-    for (int32_t y = F + lane; y < to; y += 64) out[y] = oring[y & ORM];
-    F = to;
-  };
   int32_t limit = length;
   if (PROBE) {
     const int32_t hl = 1 << probe_hashlog;
     limit = length > hl ? hl : length;
   }
   const int32_t bound = limit - 1, loop_end = limit - 12;
-  {  // clear the table (16-byte LDS stores)
+  {  // clear the table: each wave half of it
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     B2H_LDS u32x4* t16 = (B2H_LDS u32x4*)tab;
     const int32_t n16 = (int32_t)((sizeof(POS) << tablog) / 16);
-    for (int32_t i = lane; i < n16; i += 64) t16[i] = u32x4{0u, 0u, 0u, 0u};
-    asm volatile("" ::: "memory");
+    const int32_t h = n16 / 2;
+    for (int32_t i = (matcher ? 0 : h) + lane; i < (matcher ? h : n16); i += 64) t16[i] = u32x4{0u, 0u, 0u, 0u};
   }
   LzPassOut r;
   int32_t windows = 0;
-  int32_t o = 5, lit = 4, pos;
-  uint32_t byte0 = kLzMaxCopy - 1;   // out[0] is patched at the end (marker bit)
-  if (PROBE) {
-    pos = 0;
-  } else {
-    pos = 4;
-    if (lane < 5) oring[lane] = lane == 0 ? (uint8_t)(kLzMaxCopy - 1) : in[lane - 1];
-  }
+  int32_t F = 0;   // parser: output [0, F) already in `out`
+  auto flush = [&](int32_t to) {
+    for (int32_t y = F + lane; y < to; y += 64) out[y] = oring[y & ORM];
+    F = to;
+  };
+  int32_t o = 5, lit = 4, pos = PROBE ? 0 : 4;
+  uint32_t byte0 = kLzMaxCopy - 1;
+  if (!PROBE && !matcher && lane < 5) oring[lane] = lane == 0 ? (uint8_t)(kLzMaxCopy - 1) : in[lane - 1];
   int32_t peak = 0;
-  bool fail = false;
+  bool fail = false, early = false, sure = false;
   const double thr_o = PROBE ? 0.999 * (clevel == 1 ? 2.0 : clevel == 2 ? 1.5 : clevel <= 6 ? 1.2
                                         : clevel == 7 ? 1.15 : clevel == 8 ? 1.1 : 1.0) : 0.0;
   const double thr_s = thr_o * (1.001 / 0.999);
-  bool early = false, sure = false;
   EPROF_DECL;
 
-  // ---- pipeline state: tile T (a, rr, cand), tiles T + 1 and T + 2 (a), the loads of T + 3 ----
-  // Input loads are consumed two tiles after issue (an input line is an HBM miss every other
-  // tile), candidate loads one tile after (recent positions: cache hits); vmcnt is in order, so
-  // consuming tile T + 1's candidates leaves tile T + 3's input loads in flight.
-  int32_t T = pos / kFastTile;
-  RawCmp ca, crr, na, nna;
-  uint32_t ccand = 0;
+  // ---- matcher: the input words of tile `ant` (prefetched one step ahead) ----
+  RawCmp na;
+  int32_t ant = -1;
   auto load_a = [&](int32_t t, RawCmp& a) {
     const int32_t p = t * kFastTile + lane;
     rawc_load(in + (p < loop_end ? p : 0), a);
   };
-  auto exchange_and_load = [&](int32_t t, const RawCmp& a, uint32_t& cand, RawCmp& rr) {
+  // insert tile t, test every lane's candidate, hand the results over in slot `slot`
+  auto produce = [&](int32_t t, int slot) {
+    RawCmp a;
+    if (t == ant) a = na;
+    else load_a(t, a);
     const int32_t p = t * kFastTile + lane;
     const bool valid = p < loop_end;
-    cand = fast_exchange<POS>(rawc_word(a, 0), p, valid, tablog, tab);
-    const int32_t q = fast_cand_ok(p, cand, valid) ? (int32_t)cand : (valid ? p : 0);
-    rawc_load(in + q, rr);
-  };
-  if (pos < loop_end) {
-    load_a(T, ca);
-    exchange_and_load(T, ca, ccand, crr);
-    load_a(T + 1, na);
-    load_a(T + 2, nna);
-  }
-  while (pos < loop_end) {
-    if (PROBE) {
-      if ((double)(limit + 64) < thr_o * (double)o) { early = true; break; }
-      const int32_t R = loop_end - pos;
-      if ((double)loop_end >= thr_s * (double)(o + R + R / 16 + 16)) { sure = true; break; }
-    }
-    windows++;
-    EPROF_T(t0);
-    if (!PROBE && o - F >= 1024) flush(F + 512);   // a tile emits < 512 bytes
-    EPROF_T(t0f);
-    EPROF_ADD(6, t0, t0f);
-    const int32_t P = T * kFastTile;
-    const int32_t p = P + lane;
-    const bool valid = p < loop_end;
-    const int32_t s0 = pos - P;                            // the parse enters the tile here
-    const int32_t lim = min(kFastTile, loop_end - P);      // lanes below lim are main-loop positions
-    // ---- stage B of tile T + 1 (table exchange, candidate loads) and stage A of tile T + 2: issued
-    // first, consumed one tile later ----
-    RawCmp nrr, n3a;
-    uint32_t ncand = 0;
-    exchange_and_load(T + 1, na, ncand, nrr);
-    load_a(T + 3, n3a);
-    EPROF_T(t1);
-    EPROF_ADD(0, t0f, t1);
-    // ---- stage C of tile T: candidate test (exactly as the serial loop decides) ----
-    const uint32_t v = rawc_word(ca, 0);
-    const uint32_t dist = (uint32_t)(p - (int32_t)ccand);
-    // first mismatching byte of in[p..p+59] vs the candidate's (60: all equal), for every lane
-    // with a usable candidate (mmd = -1 otherwise): the chain walk extends long matches from the
-    // compares of later lanes that sit at the same distance
-    const bool cok = fast_cand_ok(p, ccand, valid);
-    int32_t mm = kCmpBytes;
-#pragma unroll
-    for (int i = kCmpWords - 1; i >= 0; i--) {
-      const uint32_t x = rawc_word(ca, i) ^ rawc_word(crr, i);
-      if (x) mm = 4 * i + (__builtin_ctz(x) >> 3);
-    }
-    const int32_t mmd = cok ? mm : -1;
-    bool accept = false;
-    int32_t lenx = 0;   // match length, or -1: the first kCmpBytes all match (extend later)
-    if (lane >= s0 && cok && mm >= 4) {
-      const int32_t e = min(mm < kCmpBytes ? p + mm + 1 : 0x7fffffff, bound);
-      const int32_t len = e - 4 - p;
-      accept = len >= 4 && (PROBE || !(len <= 5 && (dist - 1) >= kLzNear));
-      lenx = (mm < kCmpBytes || p + kCmpBytes + 1 >= bound) ? len : -1;
-    }
-
-    const uint64_t am = __ballot(accept);
-    EPROF_T(t2);
-    EPROF_ADD(1, t1, t2);
-    if (PROBE && am == 0) {
-      // all-literal probe tile: closed-form count of lanes s0 .. lim-1
-      const int32_t cnt = lim - s0;
-      o += cnt + (lit + cnt) / 32;
-      lit = (lit + cnt) & 31;
-      pos = P + lim;
+    const uint32_t cand = fast_exchange<POS>(rawc_word(a, 0), p, valid, tablog, tab);
+    const bool cok = fast_cand_ok(p, cand, valid);
+    // the candidate's first word decides most tiles: when no lane's 4 bytes match, every first
+    // mismatch lies in word 0 and the other 14 words are neither loaded nor compared
+    gin_t cq = in + (cok ? (int32_t)cand : (valid ? p : 0));
+    const B2H_GLB uint32_t* cw = align4(cq);
+    const uint32_t csh = (uint32_t)(reinterpret_cast<uintptr_t>(cq) & 3);
+    const uint32_t c0 = cw[0], c1 = cw[1];
+    load_a(t + 1, na);   // issued after the candidate loads: the compare waits for those only
+    ant = t + 1;
+    const uint32_t x0 = rawc_word(a, 0) ^ funnel(c0, c1, csh);
+    int32_t mm;
+    if (__ballot(cok && x0 == 0) == 0) {
+      mm = x0 ? (int32_t)(__builtin_ctz(x0) >> 3) : 4;
     } else {
-      // ---- chain walk: the matches the greedy parse takes in this tile ----
-      uint64_t chain = 0;
-      int32_t ser = -1;    // a match with length-extension bytes (scalar token path)
-      int32_t endc2 = -1;  // end + 2 of the last chain match, relative to P
-      {
-        uint64_t rem = am;
-        while (rem) {
-          const int32_t m = __builtin_ctzll(rem);
-          int32_t lm = rdlane(lenx, m);
-          if (lm < 0) {
-            EPROF_T(te0);
-            // bytes [p_m, p_m + L) are verified; lane m + 56 k compared the next 60 at the same
-            // distance if its candidate sits there: follow those lanes, go to memory only past them
-            const int32_t pm = P + m;
-            const uint32_t dm = (uint32_t)rdlane((int32_t)dist, m);
-            int32_t L = kCmpBytes, e = -1;
-            for (int32_t j = m + kNbrStride; j < kFastTile; j += kNbrStride) {
-              if (pm + L >= bound) { e = bound; break; }
-              const int32_t mj = rdlane(mmd, j);
-              if (mj < 0 || (uint32_t)rdlane((int32_t)dist, j) != dm) break;
-              if (mj < kCmpBytes) { e = min(P + j + mj + 1, bound); break; }
-              L = j - m + kCmpBytes;
-            }
-            if (e < 0) e = pm + L >= bound ? bound : wave_match_end(in, pm + L, dm, bound);
-            lm = e - 4 - pm;
-            lenx = lane == m ? lm : lenx;
-            EPROF_T(te1);
-            EPROF_ADD(5, te0, te1);
-          }
-          if (lm >= 262) { ser = m; break; }   // (len - 7) / 255 extension bytes
-          chain |= 1ull << m;
-          const int32_t c2 = m + lm + 2;         // the greedy parse resumes at the match end + 2
-          endc2 = c2;
-          if (c2 >= kFastTile) break;
-          rem = am & (~0ull << c2);
-        }
-      }
-      EPROF_T(t3);
-      EPROF_ADD(2, t2, t3);
-      // ---- all tokens of the tile at once (the exact-mode window emission, entered at s0) ----
-      const bool ischain = (chain >> lane) & 1ull;
-      // chain matches do not overlap, so their resume points c2 grow with the lane: the last one
-      // strictly before each lane is a max-scan shifted by one lane (DPP wave_shr:1, lane 0: -1)
-      const int32_t c2v = lane + lenx + 2;
-      const int32_t c2incl = wave_scan_max(ischain ? c2v : -1);
-      const int32_t pc2 = __builtin_amdgcn_update_dpp(-1, c2incl, 0x138, 0xf, 0xf, false);
-      const bool hasprev = pc2 >= 0;
-      const int32_t segstart = hasprev ? pc2 : s0;
-      const int32_t lpos = (hasprev ? 0 : lit) + lane - segstart;
-      const int32_t lit_end = ser >= 0 ? ser : lim;
-      const bool islit = !ischain && lane >= segstart && lane < lit_end;
-      const int32_t rr5 = lpos & 31;
-      const uint32_t bd = dist - 1;
-      const bool near = bd < kLzNear;
-      const uint32_t ulen = (uint32_t)lenx;
-      const int32_t tok = ulen < 7 ? (near ? 2 : 4) : (near ? 3 : 5);
-      int32_t contrib = 0;
-      if (islit) contrib = 1 + (rr5 == 31 ? 1 : 0);
-      if (ischain) contrib = tok + 1 - (rr5 == 0 ? 1 : 0);
-      const int32_t incl = wave_scan_add(contrib);
-      const int32_t excl = incl - contrib;
-      const uint64_t litm = __ballot(islit);
-      const uint64_t elems = litm | chain;
-      if (elems) {
-        const int32_t le = 63 - __builtin_clzll(elems);
-        const bool lelit = (litm >> le) & 1ull;
-        if (!PROBE) {
-          const int32_t base = o + excl;
-          const int32_t ts = base - (rr5 == 0 ? 1 : 0);
-          const int32_t req = lelit ? rdlane(base, le) + 2 : rdlane(ts + tok + 1, le);
-          peak = max(peak, req);
-          if (req > maxout) { fail = true; break; }
-          // Every element writes a fixed 6-byte slot from its start in DESCENDING byte order: a
-          // position's owner always has the lowest byte index among the elements that touch it
-          // (the others start earlier), so the owner's byte lands last and the bytes past an
-          // element's end need no masks: the next element's first byte replaces a literal's
-          // pending run marker or a token's trailing marker exactly as the reference overwrites it.
-          // Token bytes (MATCH_SHORT/LONG/_FAR, blosc/blosclz.c:270-316) + the marker opening the
-          // next literal run, built without branches.
-          if (islit || ischain) {
-            const uint32_t fd = bd - kLzNear;
-            const bool lng = ulen >= 7;
-            const uint32_t b0 = (lng ? (7u << 5) : (ulen << 5)) + (near ? (bd >> 8) : 31u);
-            const uint32_t dbytes = near ? (bd & 255u) : (255u | ((fd >> 8) << 8) | ((fd & 255u) << 16));
-            uint64_t rest = (uint64_t)dbytes | (31ull << (near ? 8 : 24));
-            if (lng) rest = (uint64_t)(ulen - 7) | (rest << 8);
-            const uint64_t bytes = islit ? (uint64_t)((v & 0xffu) | ((uint32_t)(kLzMaxCopy - 1) << 8))
-                                         : ((uint64_t)b0 | (rest << 8));
-            const int32_t start = islit ? base : ts;
+      uint32_t c[kCmpWords + 1];
+      c[0] = c0;
+      c[1] = c1;
 #pragma unroll
-            for (int i = 5; i >= 0; i--) oring[(start + i) & ORM] = (uint8_t)(bytes >> (8 * i));
-          }
-          if (ischain && rr5 > 0) oring[(ts - rr5 - 1) & ORM] = (uint8_t)(rr5 - 1);
-          const uint64_t z = __ballot(ischain && rr5 > 0 && ts - rr5 - 1 == 0);
-          if (z) byte0 = (uint32_t)(rdlane(rr5, __builtin_ctzll(z)) - 1);
-        }
-        lit = lelit ? ((rdlane(lpos, le) + 1) & 31) : 0;
+      for (int i = 2; i < kCmpWords + 1; i++) c[i] = cw[i];
+      mm = kCmpBytes;
+#pragma unroll
+      for (int i = kCmpWords - 1; i >= 1; i--) {
+        const uint32_t x = rawc_word(a, i) ^ funnel(c[i], c[i + 1], csh);
+        if (x) mm = 4 * i + (__builtin_ctz(x) >> 3);
       }
-      o += rdlane(incl, 63);
-      EPROF_T(t4);
-      EPROF_ADD(3, t3, t4);
-      int32_t next_rel = max(endc2, lim);
-      // ---- a match with extension bytes: the scalar token path ----
-      if (ser >= 0) {
-        const uint32_t dm = (uint32_t)rdlane((int32_t)dist, ser);
-        const int32_t lm = rdlane(lenx, ser);
-        const uint32_t sbd = dm - 1;
-        const uint32_t sulen = (uint32_t)lm;
-        const bool snear = sbd < kLzNear;
-        int32_t at = -1;
-        const uint32_t hdr = (uint32_t)(lit - 1);
-        if (lit) {
-          at = o - lit - 1;
-          if (!PROBE && at == 0) byte0 = hdr;
+      if (x0) mm = (int32_t)(__builtin_ctz(x0) >> 3);
+    }
+    sh->dist[slot][lane] = (uint32_t)(p - (int32_t)cand);
+    sh->aux[slot][lane] = (uint32_t)(cok ? mm + 1 : 0) | ((rawc_word(a, 0) & 0xffu) << 8);
+  };
+
+  int32_t T = pos / kFastTile, pend = -1;
+  int cur = 0, it = 0;
+  const bool any = pos < loop_end;
+  __syncthreads();                           // table cleared
+  if (any && matcher) produce(T, 0);         // entering T: T and T + 1
+  __syncthreads();
+  while (any) {
+    if (matcher) {
+      if (pend >= 0) produce(pend, cur ^ 1);               // the parser jumps to `pend`
+      else if ((T + 1) * kFastTile < loop_end) produce(T + 1, cur ^ 1);
+    } else if (pend < 0) {
+      // ================= parser: tile T from slot `cur` =================
+      int32_t nt = -1;
+      do {
+        if (PROBE) {
+          if ((double)(limit + 64) < thr_o * (double)o) { early = true; break; }
+          const int32_t R = loop_end - pos;
+          if ((double)loop_end >= thr_s * (double)(o + R + R / 16 + 16)) { sure = true; break; }
+        }
+        windows++;
+        EPROF_T(t0);
+        if (!PROBE && o - F >= 1024) flush(F + 512);   // a tile emits < 512 bytes
+        const int32_t P = T * kFastTile;
+        const int32_t p = P + lane;
+        const int32_t s0 = pos - P;
+        const int32_t lim = min(kFastTile, loop_end - P);
+        const uint32_t dist = sh->dist[cur][lane];
+        const uint32_t ax = sh->aux[cur][lane];
+        const int32_t mmd = (int32_t)(ax & 0xffu) - 1;   // -1: no usable candidate
+        const uint32_t vbyte = (ax >> 8) & 0xffu;
+        bool accept = false;
+        int32_t lenx = 0;
+        if (lane >= s0 && mmd >= 4) {
+          const int32_t e = min(mmd < kCmpBytes ? p + mmd + 1 : 0x7fffffff, bound);
+          const int32_t len = e - 4 - p;
+          accept = len >= 4 && (PROBE || !(len <= 5 && (dist - 1) >= kLzNear));
+          lenx = (mmd < kCmpBytes || p + kCmpBytes + 1 >= bound) ? len : -1;
+        }
+        const uint64_t am = __ballot(accept);
+        EPROF_T(t2);
+        EPROF_ADD(1, t0, t2);
+        if (PROBE && am == 0) {
+          const int32_t cnt = lim - s0;
+          o += cnt + (lit + cnt) / 32;
+          lit = (lit + cnt) & 31;
+          pos = P + lim;
         } else {
-          o--;
-        }
-        lit = 0;
-        const int32_t ext = (int32_t)((sulen - 7) / 255);
-        const int32_t stok = 1 + ext + (snear ? 2 : 4);
-        if (!PROBE) {
-          peak = max(peak, o + stok + 1);
-          if (o + stok + 1 > maxout) {
-            fail = true;
-          } else {
-            if (lane == 0 && at >= 0) oring[at & ORM] = (uint8_t)hdr;
-            const uint32_t remlen = (sulen - 7) - 255u * (uint32_t)ext;
-            const uint32_t fd = sbd - kLzNear;
-            if (lane == 0) oring[o & ORM] = (uint8_t)((7u << 5) + (snear ? (sbd >> 8) : 31u));
-            for (int32_t i0 = 0; i0 < ext; i0 += 512) {
-              if (o + 1 + i0 + 512 - F > kOutRing) flush(o + 1 + i0);
-              for (int32_t i = i0 + lane; i < min(ext, i0 + 512); i += 64) oring[(o + 1 + i) & ORM] = 255;
-            }
-            if (o + 1 + ext + 5 - F > kOutRing) flush(o + 1 + ext);
-            if (lane == 0) {
-              const int32_t qq = o + 1 + ext;
-              oring[qq & ORM] = (uint8_t)remlen;
-              if (snear) { oring[(qq + 1) & ORM] = (uint8_t)(sbd & 255); oring[(qq + 2) & ORM] = (uint8_t)(kLzMaxCopy - 1); }
-              else { oring[(qq + 1) & ORM] = 255; oring[(qq + 2) & ORM] = (uint8_t)(fd >> 8); oring[(qq + 3) & ORM] = (uint8_t)(fd & 255); oring[(qq + 4) & ORM] = (uint8_t)(kLzMaxCopy - 1); }
+          uint64_t chain = 0;
+          int32_t ser = -1, endc2 = -1;
+          {
+            uint64_t rem = am;
+            while (rem) {
+              const int32_t m = __builtin_ctzll(rem);
+              int32_t lm = rdlane(lenx, m);
+              if (lm < 0) {
+                EPROF_T(te0);
+                const int32_t pm = P + m;
+                const uint32_t dm = (uint32_t)rdlane((int32_t)dist, m);
+                int32_t L = kCmpBytes, e = -1;
+                for (int32_t j = m + kNbrStride; j < kFastTile; j += kNbrStride) {
+                  if (pm + L >= bound) { e = bound; break; }
+                  const int32_t mj = rdlane(mmd, j);
+                  if (mj < 0 || (uint32_t)rdlane((int32_t)dist, j) != dm) break;
+                  if (mj < kCmpBytes) { e = min(P + j + mj + 1, bound); break; }
+                  L = j - m + kCmpBytes;
+                }
+                if (e < 0) e = pm + L >= bound ? bound : wave_match_end(in, pm + L, dm, bound);
+                lm = e - 4 - pm;
+                lenx = lane == m ? lm : lenx;
+                EPROF_T(te1);
+                EPROF_ADD(5, te0, te1);
+              }
+              if (lm >= 262) { ser = m; break; }
+              chain |= 1ull << m;
+              const int32_t c2 = m + lm + 2;
+              endc2 = c2;
+              if (c2 >= kFastTile) break;
+              rem = am & (~0ull << c2);
             }
           }
+          EPROF_T(t3);
+          EPROF_ADD(2, t2, t3);
+          const bool ischain = (chain >> lane) & 1ull;
+          const int32_t c2v = lane + lenx + 2;
+          const int32_t c2incl = wave_scan_max(ischain ? c2v : -1);
+          const int32_t pc2 = __builtin_amdgcn_update_dpp(-1, c2incl, 0x138, 0xf, 0xf, false);
+          const bool hasprev = pc2 >= 0;
+          const int32_t segstart = hasprev ? pc2 : s0;
+          const int32_t lpos = (hasprev ? 0 : lit) + lane - segstart;
+          const int32_t lit_end = ser >= 0 ? ser : lim;
+          const bool islit = !ischain && lane >= segstart && lane < lit_end;
+          const int32_t rr5 = lpos & 31;
+          const uint32_t bd = dist - 1;
+          const bool near = bd < kLzNear;
+          const uint32_t ulen = (uint32_t)lenx;
+          const int32_t tok = ulen < 7 ? (near ? 2 : 4) : (near ? 3 : 5);
+          int32_t contrib = 0;
+          if (islit) contrib = 1 + (rr5 == 31 ? 1 : 0);
+          if (ischain) contrib = tok + 1 - (rr5 == 0 ? 1 : 0);
+          const int32_t incl = wave_scan_add(contrib);
+          const int32_t excl = incl - contrib;
+          const uint64_t litm = __ballot(islit);
+          const uint64_t elems = litm | chain;
+          if (elems) {
+            const int32_t le = 63 - __builtin_clzll(elems);
+            const bool lelit = (litm >> le) & 1ull;
+            if (!PROBE) {
+              const int32_t base = o + excl;
+              const int32_t ts = base - (rr5 == 0 ? 1 : 0);
+              const int32_t req = lelit ? rdlane(base, le) + 2 : rdlane(ts + tok + 1, le);
+              peak = max(peak, req);
+              if (req > maxout) { fail = true; break; }
+              // Every element writes a fixed 6-byte slot from its start in DESCENDING byte order: a
+              // position's owner always has the lowest byte index among the elements that touch it
+              // (the others start earlier), so the owner's byte lands last and the bytes past an
+              // element's end need no masks: the next element's first byte replaces a literal's
+              // pending run marker or a token's trailing marker exactly as the reference overwrites it.
+              // Token bytes (MATCH_SHORT/LONG/_FAR, blosc/blosclz.c:270-316) + the marker opening the
+              // next literal run, built without branches.
+              if (islit || ischain) {
+                const uint32_t fd = bd - kLzNear;
+                const bool lng = ulen >= 7;
+                const uint32_t b0 = (lng ? (7u << 5) : (ulen << 5)) + (near ? (bd >> 8) : 31u);
+                const uint32_t dbytes = near ? (bd & 255u) : (255u | ((fd >> 8) << 8) | ((fd & 255u) << 16));
+                uint64_t rest = (uint64_t)dbytes | (31ull << (near ? 8 : 24));
+                if (lng) rest = (uint64_t)(ulen - 7) | (rest << 8);
+                const uint64_t bytes = islit ? (uint64_t)(vbyte | ((uint32_t)(kLzMaxCopy - 1) << 8))
+                                             : ((uint64_t)b0 | (rest << 8));
+                const int32_t start = islit ? base : ts;
+#pragma unroll
+                for (int i = 5; i >= 0; i--) oring[(start + i) & ORM] = (uint8_t)(bytes >> (8 * i));
+              }
+              if (ischain && rr5 > 0) oring[(ts - rr5 - 1) & ORM] = (uint8_t)(rr5 - 1);
+              const uint64_t z = __ballot(ischain && rr5 > 0 && ts - rr5 - 1 == 0);
+              if (z) byte0 = (uint32_t)(rdlane(rr5, __builtin_ctzll(z)) - 1);
+            }
+            lit = lelit ? ((rdlane(lpos, le) + 1) & 31) : 0;
+          }
+          o += rdlane(incl, 63);
+          EPROF_T(t4);
+          EPROF_ADD(3, t3, t4);
+          int32_t next_rel = max(endc2, lim);
+          if (ser >= 0) {   // a match with length-extension bytes: the scalar token path
+            const uint32_t dm = (uint32_t)rdlane((int32_t)dist, ser);
+            const int32_t lm = rdlane(lenx, ser);
+            const uint32_t sbd = dm - 1;
+            const uint32_t sulen = (uint32_t)lm;
+            const bool snear = sbd < kLzNear;
+            int32_t at = -1;
+            const uint32_t hdr = (uint32_t)(lit - 1);
+            if (lit) {
+              at = o - lit - 1;
+              if (!PROBE && at == 0) byte0 = hdr;
+            } else {
+              o--;
+            }
+            lit = 0;
+            const int32_t ext = (int32_t)((sulen - 7) / 255);
+            const int32_t stok = 1 + ext + (snear ? 2 : 4);
+            if (!PROBE) {
+              peak = max(peak, o + stok + 1);
+              if (o + stok + 1 > maxout) {
+                fail = true;
+              } else {
+                if (lane == 0 && at >= 0) oring[at & ORM] = (uint8_t)hdr;
+                const uint32_t remlen = (sulen - 7) - 255u * (uint32_t)ext;
+                const uint32_t fd = sbd - kLzNear;
+                if (lane == 0) oring[o & ORM] = (uint8_t)((7u << 5) + (snear ? (sbd >> 8) : 31u));
+                for (int32_t i0 = 0; i0 < ext; i0 += 512) {
+                  if (o + 1 + i0 + 512 - F > kOutRing) flush(o + 1 + i0);
+                  for (int32_t i = i0 + lane; i < min(ext, i0 + 512); i += 64) oring[(o + 1 + i) & ORM] = 255;
+                }
+                if (o + 1 + ext + 5 - F > kOutRing) flush(o + 1 + ext);
+                if (lane == 0) {
+                  const int32_t qq = o + 1 + ext;
+                  oring[qq & ORM] = (uint8_t)remlen;
+                  if (snear) { oring[(qq + 1) & ORM] = (uint8_t)(sbd & 255); oring[(qq + 2) & ORM] = (uint8_t)(kLzMaxCopy - 1); }
+                  else { oring[(qq + 1) & ORM] = 255; oring[(qq + 2) & ORM] = (uint8_t)(fd >> 8); oring[(qq + 3) & ORM] = (uint8_t)(fd & 255); oring[(qq + 4) & ORM] = (uint8_t)(kLzMaxCopy - 1); }
+                }
+              }
+            }
+            o += stok + 1;
+            next_rel = ser + lm + 2;
+          }
+          if (fail) break;
+          pos = P + next_rel;
         }
-        o += stok + 1;
-        next_rel = ser + lm + 2;
-      }
-      if (fail) break;
-      pos = P + next_rel;
+        if (pos < loop_end) nt = pos / kFastTile;
+      } while (false);
+      if (lane == 0) sh->ctrl[it & 1] = nt;
     }
-    // ---- advance the pipeline ----
-    EPROF_T(t5);
-    const int32_t NT = pos / kFastTile;
-    if (pos >= loop_end) break;
-    if (NT == T + 1) {
-      ca = na;
-      crr = nrr;
-      na = nna;
-      nna = n3a;
-      ccand = ncand;
-      T = NT;
-    } else {   // a match jumped past tile T + 1: restart at its end
-      T = NT;
-      load_a(T, ca);
-      exchange_and_load(T, ca, ccand, crr);
-      load_a(T + 1, na);
-      load_a(T + 2, nna);
+    __syncthreads();
+    if (pend >= 0) {   // the matcher produced the jump target: the parser takes it next
+      T = pend;
+      cur ^= 1;
+      pend = -1;
+      continue;
     }
-    EPROF_T(t6);
-    EPROF_ADD(4, t5, t6);
+    const int32_t c = sh->ctrl[it & 1];
+    it++;
+    if (c < 0) break;
+    if (c == T + 1) {
+      T = c;
+      cur ^= 1;
+    } else {
+      pend = c;
+    }
   }
   EPROF_FLUSH;
-
-  if (!PROBE && !fail) {
+  if (!matcher && !PROBE && !fail) {
     // tail literals [pos, bound]
     while (pos <= bound) {
       if (o - F >= 1024) flush(F + 512);
@@ -401,7 +414,7 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
         flush(o);
       } else {
         flush(o);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the flushed byte 0 first
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) out[0] = (uint8_t)(byte0 | 0x20u);
       }
     }
@@ -416,35 +429,49 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
   return r;
 }
 
-// Fast-mode stream encode with maxout = neblock: run test, fast probe (the reference's decision
-// rule over a fast-mode parse), fast main pass.  tablog: the LDS table (<= the clevel's hashlog).
+// Two-wave fast-mode stream encode: both waves run this; the parser's StreamResult is the one
+// to keep.  The run test is split between the waves; decisions travel through sh->decide.
 template <typename POS>
 __device__ __forceinline__ StreamResult encode_stream_fast(gin_t in, int32_t n, int clevel, gout_t out,
-                                                           B2H_LDS uint8_t* tab, int tablog, B2H_LDS uint8_t* oring,
-                                                           bool allow_runs) {
+                                                            B2H_LDS uint8_t* tab, int tablog, B2H_LDS uint8_t* oring,
+                                                            B2H_LDS FastShared* sh, bool allow_runs, bool matcher) {
   StreamResult res;
   res.windows = 0;
   res.cycles = 0;
   res.peak = 0;
-  if (allow_runs && wave_is_run(in, n)) {
-    res.size = in[0];
-    res.kind = res.size ? kStreamByteRun : kStreamZeroRun;
-    return res;
-  }
   res.kind = kStreamRaw;
   res.size = 0;
+  if (allow_runs) {
+    // each wave tests its half against in[0]; both read both verdicts
+    const int32_t h = (n / 2) & ~15;
+    const bool half_run = matcher ? wave_is_run(in, h + 1) : wave_is_run_from(in, h, n, in[0]);
+    if (lane_id() == 0) sh->decide[matcher ? 0 : 1] = half_run ? 1 : 0;
+    __syncthreads();
+    const bool run = sh->decide[0] && sh->decide[1];
+    __syncthreads();   // both read before the next write
+    if (run) {
+      res.size = in[0];
+      res.kind = res.size ? kStreamByteRun : kStreamZeroRun;
+      return res;
+    }
+  }
   const int hashlog = clevel == 1 ? 12 : (clevel == 2 ? 13 : 14);
   const int tl = min(tablog, hashlog);
   int32_t maxlen = n;
   if (clevel < 2) maxlen /= 8;
   else if (clevel < 4) maxlen /= 4;
   else if (clevel < 7) maxlen /= 2;
-  const LzPassOut pr = lz_pass_fast<true, POS>(in + (n - maxlen), maxlen, hashlog, tl, out, 0, tab, oring, clevel);
+  const LzPassOut pr = lz_pass_fast<true, POS>(in + (n - maxlen), maxlen, hashlog, tl, out, 0, tab, oring, sh, clevel,
+                                                matcher);
   res.windows = pr.windows;
   const double ratio = (double)pr.pos / (double)pr.o;
   const double thr = clevel == 1 ? 2.0 : clevel == 2 ? 1.5 : clevel <= 6 ? 1.2 : clevel == 7 ? 1.15 : clevel == 8 ? 1.1 : 1.0;
-  if (pr.early || (!pr.sure && ratio < thr) || n < 16 || n < 66) return res;
-  const LzPassOut em = lz_pass_fast<false, POS>(in, n, hashlog, tl, out, n, tab, oring, clevel);
+  if (!matcher && lane_id() == 0) sh->decide[0] = (pr.early || (!pr.sure && ratio < thr) || n < 66) ? 0 : 1;
+  __syncthreads();
+  const bool go = sh->decide[0] != 0;
+  __syncthreads();
+  if (!go) return res;
+  const LzPassOut em = lz_pass_fast<false, POS>(in, n, hashlog, tl, out, n, tab, oring, sh, clevel, matcher);
   res.windows += em.windows;
   if (em.fail) return res;
   res.kind = kStreamLz;

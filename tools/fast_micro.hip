@@ -1,5 +1,6 @@
-// Fast-mode encoder micro-benchmark (diagnostics only): encode one stream per wave with the
-// product encode_stream_fast, many waves, and report cycles per stream and per-phase sums.
+// Fast-mode encoder micro-benchmark (diagnostics only): encode one stream per two-wave workgroup
+// with the product encode_stream_fast (matcher + parser), many workgroups, and report cycles per
+// stream and the parser's per-phase sums.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../c-blosc2_amd/csrc fast_micro.hip -o fast_micro
 //   ./fast_micro plane.bin [clevel] [tablog]
 #include <hip/hip_runtime.h>
@@ -15,16 +16,18 @@
 #include "b2h_lzfast.h"
 using namespace b2h;
 
-__global__ __launch_bounds__(64) void k_enc(const uint8_t* in, int32_t n, int clevel, int tablog, uint8_t* out,
-                                            int64_t* cycles, StreamResult* res) {
+__global__ __launch_bounds__(128) void k_enc(const uint8_t* in, int32_t n, int clevel, int tablog, uint8_t* out,
+                                             int64_t* cycles, StreamResult* res) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   B2H_LDS uint8_t* tab = (B2H_LDS uint8_t*)smem;
   B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + ((size_t)FM_POSB << tablog));
+  B2H_LDS FastShared* sh = (B2H_LDS FastShared*)(smem + ((size_t)FM_POSB << tablog) + kOutRing);
+  const bool matcher = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
   StreamResult r = encode_stream_fast<FM_POS>((gin_t)in, n, clevel, (gout_t)(out + (size_t)blockIdx.x * (n + 64)), tab,
-                                      tablog, oring, true);
+                                              tablog, oring, sh, true, matcher);
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
-  if (threadIdx.x == 0) { cycles[blockIdx.x] = (int64_t)(t1 - t0); res[blockIdx.x] = r; }
+  if (threadIdx.x == 64) { cycles[blockIdx.x] = (int64_t)(t1 - t0); res[blockIdx.x] = r; }
 }
 
 static std::vector<uint8_t> slurp(const char* f) {
@@ -52,14 +55,14 @@ int main(int argc, char** argv) {
   hipMalloc(&dout, (size_t)maxblk * (n + 64));
   int64_t* dc; StreamResult* dr;
   hipMalloc(&dc, maxblk * 8); hipMalloc(&dr, maxblk * sizeof(StreamResult));
-  const size_t lds = ((size_t)FM_POSB << tablog) + kOutRing;
+  const size_t lds = ((size_t)FM_POSB << tablog) + kOutRing + ((sizeof(FastShared) + 15) & ~size_t(15));
   hipFuncSetAttribute(reinterpret_cast<const void*>(&k_enc), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   for (int nblk : {1, 256, 1024, 4096}) {
     uint64_t z[16] = {0};
     hipMemcpyToSymbol(HIP_SYMBOL(g_enc_prof), z, sizeof z);
     hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
     hipEventRecord(a);
-    k_enc<<<nblk, 64, lds>>>(din, n, clevel, tablog, dout, dc, dr);
+    k_enc<<<nblk, 128, lds>>>(din, n, clevel, tablog, dout, dc, dr);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms = 0; hipEventElapsedTime(&ms, a, b);

@@ -12,12 +12,13 @@
  *                     cand[p] = tab[hash(in[p..p+3])]; tab[hash] = p
  *
  * and the parse consumes tiles: entering tile T (the one holding the parse position) it inserts T
- * if no later tile was inserted yet, then T + 1 (the GPU kernel issues T + 1's table exchange and
- * candidate loads before it parses T); tiles a long match jumps over are never inserted.  A
+ * if no later tile was inserted yet, then T + 1 (the GPU kernel's matcher wave exchanges and
+ * compares T + 1 while the parser wave parses T); tiles a long match jumps over are never
+ * inserted.  A
  * candidate is only a suggestion: every match is verified byte for byte and bounded exactly as in
  * the reference, so any stream this produces decodes with blosclz_decompress (blosclz.c:685-795).
  *
- * The GPU kernel (b2h_lz.h lz_pass_fast) runs the tile inserts as one LDS atomic exchange per
+ * The GPU kernel (b2h_lzfast.h lz_pass_fast) runs the tile inserts as one LDS atomic exchange per
  * lane; LDS applies the lanes of one instruction in lane order, so it reproduces this model byte
  * for byte (tests/test_fast_mode.py checks both that and the reference decoder round trip).
  */
