@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libblosc2.so")
+# B2H_LIB: an alternative build of the same library (diagnostic A/B runs of build variants)
+LIB_PATH = os.environ.get("B2H_LIB") or os.path.join(HERE, "lib", "libblosc2.so")
 
 MAX_FILTERS = 6
 NOFILTER, SHUFFLE, BITSHUFFLE, DELTA, TRUNC_PREC = 0, 1, 2, 3, 4
