@@ -79,7 +79,7 @@ struct Scratch {
 struct Workspace {
   Scratch t1, t2, work, sbuf, res, place, mode, qctr, gtab, porder;    // compress
   bool porder_init = false;
-  Scratch dchunks, dstreams, dblocks, dtotals, stage, stage2, ptrs, dqctr, ddbg;  // decompress
+  Scratch dchunks, dstreams, dblocks, dtotals, stage, stage2, ptrs, dqctr, ddbg, dorder;  // decompress
   std::mutex mu;
   hipEvent_t done = nullptr;       // recorded after the last kernel of the latest call
   hipStream_t last = nullptr;      // the stream that call ran on
@@ -98,7 +98,7 @@ struct Workspace {
   void free_all() {
     if (used && done) (void)hipEventSynchronize(done);
     for (Scratch* s : {&t1, &t2, &work, &sbuf, &res, &place, &mode, &qctr, &gtab, &porder, &dchunks, &dstreams,
-                       &dblocks, &dtotals, &stage, &stage2, &ptrs, &dqctr, &ddbg})
+                       &dblocks, &dtotals, &stage, &stage2, &ptrs, &dqctr, &ddbg, &dorder})
       s->release();
     if (done) (void)hipEventDestroy(done);
     done = nullptr;
@@ -1575,9 +1575,13 @@ __device__ int32_t find_chunk(const DChunk* ch, int32_t n, int32_t idx) {
   return lo;
 }
 
+// Pull order of the decoder: LZ / LZ4 streams (thousands of tokens each; on T one per block, ~90 %
+// of the decode wave-time) from the front, raw copies and runs (a 64 KiB memcpy / memset) from the
+// back, so the long streams start first and the short ones fill the end of the launch.
 __device__ void dplan_block(const uint8_t* const* __restrict__ srcs, const int32_t* __restrict__ srcsize,
                             DChunk* __restrict__ ch, int32_t n, DBlock* __restrict__ blocks,
-                            DStream* __restrict__ streams, int32_t idx) {
+                            DStream* __restrict__ streams, int32_t idx, int32_t* __restrict__ order,
+                            int32_t* __restrict__ octr, int32_t nstreams) {
   const int32_t c = find_chunk(ch, n, idx);
   const DChunk d = ch[c];
   const int32_t b = idx - d.block_base;
@@ -1615,16 +1619,20 @@ __device__ void dplan_block(const uint8_t* const* __restrict__ srcs, const int32
     }
     if (err) st.neblock = -1;
     streams[sbase + j] = st;
+    const bool heavy = st.neblock > 0 && st.csize > 0 && st.csize != st.neblock;
+    const int32_t slot = heavy ? atomicAdd(&octr[0], 1) : nstreams - 1 - atomicAdd(&octr[1], 1);
+    order[slot] = sbase + j;
   }
   if (err) atomicMin(&ch[c].status, err);
 }
 
 __global__ void k_dplan_blocks(const uint8_t* const* __restrict__ srcs, const int32_t* __restrict__ srcsize,
                                DChunk* __restrict__ ch, int32_t n, DBlock* __restrict__ blocks,
-                               DStream* __restrict__ streams, const DTotals* __restrict__ tot) {
-  const int32_t nb = tot->nblocks;
+                               DStream* __restrict__ streams, const DTotals* __restrict__ tot,
+                               int32_t* __restrict__ order, int32_t* __restrict__ octr) {
+  const int32_t nb = tot->nblocks, ns = tot->nstreams;
   for (int32_t idx = blockIdx.x * blockDim.x + threadIdx.x; idx < nb; idx += gridDim.x * blockDim.x)
-    dplan_block(srcs, srcsize, ch, n, blocks, streams, idx);
+    dplan_block(srcs, srcsize, ch, n, blocks, streams, idx, order, octr, ns);
 }
 
 // Decoder: one wave per stream, persistent (as many single-wave workgroups as the LDS ring
@@ -1680,14 +1688,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RLOG == 12 ?
                                                DChunk* __restrict__ ch, const DStream* __restrict__ streams,
                                                uint8_t* __restrict__ stage, const DTotals* __restrict__ tot,
                                                const uint8_t* __restrict__ maskout, int32_t mask_stride,
-                                               int32_t* __restrict__ next, int64_t* __restrict__ dbg) {
+                                               int32_t* __restrict__ next, const int32_t* __restrict__ order,
+                                               int64_t* __restrict__ dbg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   B2H_LDS uint8_t* ring = (B2H_LDS uint8_t*)smem;
   const int32_t nstreams_total = __builtin_amdgcn_readfirstlane(tot->nstreams);
   for (;;) {
-    // branch-free grab (see k_encode)
-    const int32_t s = __builtin_amdgcn_readfirstlane(atomicAdd(next, lane_id() == 0 ? 1 : 0));
-    if (s >= nstreams_total) return;
+    // branch-free grab (see k_encode), then the planner's pull order (LZ streams first)
+    const int32_t i = __builtin_amdgcn_readfirstlane(atomicAdd(next, lane_id() == 0 ? 1 : 0));
+    if (i >= nstreams_total) return;
+    const int32_t s = __builtin_amdgcn_readfirstlane(order[i]);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     int32_t kind = 0;
     decode_stream<RLOG>(srcs, dsts, ch, streams[s], stage, maskout, mask_stride, ring, &kind);
@@ -1825,11 +1835,12 @@ static int dec_ring_log() {
 template <int RLOG>
 static void launch_decode(const uint8_t* const* d_src, uint8_t* const* d_dst, DChunk* ch, const DStream* streams,
                           uint8_t* stage, const DTotals* tot, int64_t nstreams_bound, const uint8_t* d_maskout,
-                          int32_t mask_stride, int32_t* next, int64_t* dbg, hipStream_t st) {
+                          int32_t mask_stride, int32_t* next, const int32_t* order, int64_t* dbg, hipStream_t st) {
   const size_t lds = size_t(1) << RLOG;
   const int slots = resident_slots(reinterpret_cast<const void*>(&k_decode<RLOG>), lds);
   const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(nstreams_bound, slots));
-  k_decode<RLOG><<<grid, 64, lds, st>>>(d_src, d_dst, ch, streams, stage, tot, d_maskout, mask_stride, next, dbg);
+  k_decode<RLOG><<<grid, 64, lds, st>>>(d_src, d_dst, ch, streams, stage, tot, d_maskout, mask_stride, next, order,
+                                        dbg);
 }
 
 static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const int32_t* d_srcsize,
@@ -1870,14 +1881,16 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
     rc |= ws->stage.ensure((size_t)h.stage_bytes);
     if (h.max_filters >= 2) rc |= ws->stage2.ensure((size_t)h.stage_bytes);
     if (rc) return E_MEMORY;
+    if (ws->dorder.ensure(sizeof(int32_t) * (size_t)h.nstreams)) return E_MEMORY;
     DBlock* blocks = ws->dblocks.as<DBlock>();
     DStream* streams = ws->dstreams.as<DStream>();
-    const int64_t pb_grid = std::max<int64_t>(1, std::min<int64_t>((h.nblocks + 255) / 256, 4096));
-    k_dplan_blocks<<<(uint32_t)pb_grid, 256, 0, st>>>(d_src, d_srcsize, ch, n, blocks, streams, tot);
+    int32_t* order = ws->dorder.as<int32_t>();
     if (ws->dqctr.ensure(16)) return E_MEMORY;
-    int32_t* next = ws->dqctr.as<int32_t>();
+    int32_t* next = ws->dqctr.as<int32_t>();   // [0]: the decoder's pull counter, [1..2]: the order's ends
+    HIPCHK(hipMemsetAsync(next, 0, 4 * sizeof(int32_t), st));
+    const int64_t pb_grid = std::max<int64_t>(1, std::min<int64_t>((h.nblocks + 255) / 256, 4096));
+    k_dplan_blocks<<<(uint32_t)pb_grid, 256, 0, st>>>(d_src, d_srcsize, ch, n, blocks, streams, tot, order, next + 1);
     ev_decode.start(st);
-    HIPCHK(hipMemsetAsync(next, 0, sizeof(int32_t), st));
     {
       int64_t* dbg = nullptr;
       if (g_ddebug) {
@@ -1886,10 +1899,10 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
       }
       const int rlog = dec_ring_log();
       uint8_t* stage = ws->stage.as<uint8_t>();
-      if (rlog == 12) launch_decode<12>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, dbg, st);
-      else if (rlog == 13) launch_decode<13>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, dbg, st);
-      else if (rlog == 14) launch_decode<14>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, dbg, st);
-      else launch_decode<15>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, dbg, st);
+      if (rlog == 12) launch_decode<12>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, order, dbg, st);
+      else if (rlog == 13) launch_decode<13>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, order, dbg, st);
+      else if (rlog == 14) launch_decode<14>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, order, dbg, st);
+      else launch_decode<15>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, order, dbg, st);
     }
     ev_decode.stop(st);
     ev_unfilter.start(st);

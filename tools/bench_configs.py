@@ -7,8 +7,9 @@ Each prints one JSON line; every run checks its own results.
       global index): exact round trip; the first chunks byte-identical to the oracle.
   C4  schunk of 10 000 x 1 MiB chunks, DELTA + SHUFFLE + BloscLZ clevel 5, int64 ramp (ts=8, auto
       512 KiB blocks): exact round trip, sample chunks byte-identical to the oracle.
-  E2E the T workload from and back to pinned host memory: H2D + compress + D2H of the compressed
-      bytes, and H2D of the compressed bytes + decompress + D2H (PCIe-inclusive; never `value`).
+  E2E the T workload from and back to pinned host memory over 3 streams in 64-chunk groups:
+      H2D + compress + pack + D2H of the packed compressed bytes, and H2D of those bytes + unpack
+      + decompress + D2H (PCIe-inclusive; never `value`); exact host round trip.
 
     python tools/bench_configs.py [--only C2,C3,C4,E2E] [--steps K]
 """
@@ -130,51 +131,115 @@ def c4(steps):
                             src, chunk, nch, cp, steps, _oracle_check(src, chunk, (0, 1, 5000, 9999), kw))
 
 
-def e2e(steps):
-    """T from pinned host memory and back (PCIe-inclusive wall clock, one direction at a time)."""
+def e2e(steps, group_chunks=64, nstreams=3):
+    """T from pinned host memory and back, PCIe-inclusive, pipelined over `nstreams` streams in
+    groups of `group_chunks` chunks.
+      compress:   H2D raw group -> b2h_compress_batch -> b2h_pack_chunks (sizes scan + copy) ->
+                  D2H of exactly the packed compressed bytes (+ the group's offsets);
+      decompress: H2D of the packed bytes from host -> b2h_unpack_chunks -> b2h_decompress_batch
+                  -> D2H of the raw group.
+    The decompress direction starts from the host copy only (its device buffers are separate and
+    zeroed), so the check host-out == host-in proves the compressed bytes crossed PCIe intact.
+    Group g's D2H is queued once its offsets are on the host (event wait on the host thread), two
+    groups behind the compute, so copies overlap the next groups' kernels."""
     chunk, nch = 4 << 20, 1024
     N = chunk * nch
+    G, GN = nch // group_chunks, group_chunks * chunk
     dev = torch.device("cuda")
     h_src = torch.empty(N, dtype=torch.uint8, pin_memory=True)
     h_src.copy_(gen_f32_device(0, N // 4, dev).view(torch.uint8).cpu())
     cap = chunk + 32
     stride = (cap + 255) // 256 * 256
-    d_src = torch.empty(N, dtype=torch.uint8, device=dev)
-    comp = torch.empty(nch * stride, dtype=torch.uint8, device=dev)
-    cb = torch.zeros(nch, dtype=torch.int32, device=dev)
-    out = torch.empty(N, dtype=torch.uint8, device=dev)
-    status = torch.zeros(nch, dtype=torch.int32, device=dev)
-    h_comp = torch.empty(nch * stride, dtype=torch.uint8, pin_memory=True)
-    h_out = torch.empty(N, dtype=torch.uint8, pin_memory=True)
     cp = B.cparams(clevel=5, typesize=4, filters=(0, 0, 0, 0, 0, B.SHUFFLE))
-    st = torch.cuda.current_stream().cuda_stream
-    d_src.copy_(h_src)
-    B.compress_batch(cp, d_src.data_ptr(), chunk, nch, chunk, comp.data_ptr(), stride, cap, cb.data_ptr(), st)
-    torch.cuda.synchronize()
-    C = int(cb.sum().item())
+    streams = [torch.cuda.Stream() for _ in range(nstreams)]
+
+    def bufs():
+        return dict(raw=torch.empty(GN, dtype=torch.uint8, device=dev),
+                    comp=torch.zeros(group_chunks * stride, dtype=torch.uint8, device=dev),
+                    packed=torch.zeros(group_chunks * stride, dtype=torch.uint8, device=dev),
+                    cb=torch.zeros(group_chunks, dtype=torch.int32, device=dev),
+                    off=torch.zeros(group_chunks + 1, dtype=torch.int64, device=dev),
+                    status=torch.zeros(group_chunks, dtype=torch.int32, device=dev))
+    cbuf = [bufs() for _ in range(nstreams)]
+    dbuf = [bufs() for _ in range(nstreams)]
+    h_off = [torch.zeros(group_chunks + 1, dtype=torch.int64, pin_memory=True) for _ in range(G)]
+    h_packed = torch.empty(nch * stride, dtype=torch.uint8, pin_memory=True)
+    h_out = torch.empty(N, dtype=torch.uint8, pin_memory=True)
+    base = [0] * (G + 1)
+    statuses = torch.zeros(nch, dtype=torch.int32, device=dev)
+
+    def compress_all():
+        evs = [None] * G
+
+        def drain(g):   # the group's compressed bytes to the host, packed
+            evs[g].synchronize()
+            n = int(h_off[g][group_chunks])
+            base[g + 1] = base[g] + n
+            k = g % nstreams
+            with torch.cuda.stream(streams[k]):
+                h_packed[base[g]:base[g] + n].copy_(cbuf[k]["packed"][:n], non_blocking=True)
+        for g in range(G):
+            k = g % nstreams
+            s, b = streams[k], cbuf[k]
+            with torch.cuda.stream(s):
+                b["raw"].copy_(h_src[g * GN:(g + 1) * GN], non_blocking=True)
+                B.compress_batch(cp, b["raw"].data_ptr(), chunk, group_chunks, chunk, b["comp"].data_ptr(), stride, cap,
+                                 b["cb"].data_ptr(), s.cuda_stream)
+                B.pack_chunks(b["comp"].data_ptr(), stride, b["cb"].data_ptr(), group_chunks, b["packed"].data_ptr(),
+                              b["off"].data_ptr(), s.cuda_stream)
+                h_off[g].copy_(b["off"], non_blocking=True)
+                evs[g] = torch.cuda.Event()
+                evs[g].record(s)
+            if g >= nstreams - 1:
+                drain(g - (nstreams - 1))
+        for g in range(max(0, G - (nstreams - 1)), G):
+            drain(g)
+        torch.cuda.synchronize()
+
+    def decompress_all():
+        for g in range(G):
+            k = g % nstreams
+            s, b = streams[k], dbuf[k]
+            n = base[g + 1] - base[g]
+            with torch.cuda.stream(s):
+                b["packed"][:n].copy_(h_packed[base[g]:base[g + 1]], non_blocking=True)
+                b["off"].copy_(h_off[g], non_blocking=True)
+                B.unpack_chunks(b["packed"].data_ptr(), b["off"].data_ptr(), group_chunks, b["comp"].data_ptr(), stride,
+                                b["cb"].data_ptr(), s.cuda_stream)
+                B.decompress_batch(b["comp"].data_ptr(), stride, b["cb"].data_ptr(), group_chunks, b["raw"].data_ptr(),
+                                   chunk, chunk, b["status"].data_ptr(), s.cuda_stream)
+                statuses[g * group_chunks:(g + 1) * group_chunks].copy_(b["status"], non_blocking=True)
+                h_out[g * GN:(g + 1) * GN].copy_(b["raw"], non_blocking=True)
+        torch.cuda.synchronize()
+
+    compress_all()   # warmup (and the sizes)
+    decompress_all()
     tc, td = [], []
     for _ in range(steps):
+        h_out.zero_()
+        for b in dbuf:
+            b["comp"].zero_()
+            b["packed"].zero_()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        d_src.copy_(h_src, non_blocking=True)
-        B.compress_batch(cp, d_src.data_ptr(), chunk, nch, chunk, comp.data_ptr(), stride, cap, cb.data_ptr(), st)
-        h_comp[:C].copy_(comp[:C], non_blocking=True)   # the compressed bytes (chunk gather not timed apart)
-        torch.cuda.synchronize()
+        compress_all()
         t1 = time.perf_counter()
-        comp[:C].copy_(h_comp[:C], non_blocking=True)
-        B.decompress_batch(comp.data_ptr(), stride, cb.data_ptr(), nch, out.data_ptr(), chunk, chunk,
-                           status.data_ptr(), st)
-        h_out.copy_(out, non_blocking=True)
-        torch.cuda.synchronize()
+        decompress_all()
         t2 = time.perf_counter()
         tc.append(t1 - t0)
         td.append(t2 - t1)
-    exact = bool(torch.equal(h_out, h_src))
+    C = base[G]
+    exact = bool(torch.equal(h_out, h_src)) and bool((statuses == chunk).all())
     tcm, tdm = float(np.median(tc)), float(np.median(td))
-    return {"config": "E2E: T from/to pinned host memory (H2D + compress + D2H of C bytes; H2D of C bytes + "
-                      "decompress + D2H)", "round_trip_exact": exact, "cratio": round(N / C, 4),
+    mode = "fast" if B.lib().b2h_set_blosclz_mode(-1) == 1 else "exact"
+    return {"config": f"E2E: T from/to pinned host memory, {nstreams} streams x groups of {group_chunks} chunks "
+                      "(H2D + compress + pack + D2H of the packed bytes; H2D of the packed bytes + unpack + "
+                      "decompress + D2H)", "blosclz_mode": mode,
+            "round_trip_exact": exact, "compressed_bytes_over_pcie": C, "cratio": round(N / C, 4),
             "compress_GiBps": round(N / GiB / tcm, 3), "decompress_GiBps": round(N / GiB / tdm, 3),
-            "GiBps_c_plus_d": round(N / GiB / (tcm + tdm), 3)}
+            "GiBps_c_plus_d": round(N / GiB / (tcm + tdm), 3),
+            "pcie_bytes_per_s": {"compress": round((N + C) / tcm / 1e9, 2), "decompress": round((N + C) / tdm / 1e9, 2),
+                                 "unit": "GB/s (H2D + D2H bytes / wall)"}}
 
 
 def lz4t(steps):
@@ -192,8 +257,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="C2,C3,C4,E2E")
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--lz-mode", default="exact", choices=["exact", "fast"])
     args = ap.parse_args()
     torch.cuda.set_device(0)
+    B.lib().b2h_set_blosclz_mode(1 if args.lz_mode == "fast" else 0)
     for name in args.only.split(","):
         r = {"C2": c2, "C3": c3, "C4": c4, "E2E": e2e, "LZ4": lz4t}[name](args.steps)
         print(json.dumps(r), flush=True)

@@ -94,14 +94,20 @@ int main(int argc, char** argv) {
     hipMemcpy(r.data(), dr, nblk * sizeof(StreamResult), hipMemcpyDeviceToHost);
     std::vector<uint8_t> o(r[0].size > 0 ? r[0].size : 1);
     hipMemcpy(o.data(), dout, o.size(), hipMemcpyDeviceToHost);
-    const bool ok = r[0].kind == kStreamLz && o.size() == want.size() && o == want;
+    // the kind blosc_c gives this stream (blosc/blosc2.c:1290-1340 run test before the codec;
+    // an empty reference output = blosclz_compress returned 0 = stored raw), and for LZ streams
+    // the reference's bytes
+    bool same = true;
+    for (uint8_t x : in) same &= x == in[0];
+    const int want_kind = same ? (in[0] ? kStreamByteRun : kStreamZeroRun) : (want.empty() ? kStreamRaw : kStreamLz);
+    const bool ok = r[0].kind == want_kind && (want_kind != kStreamLz || (o.size() == want.size() && o == want));
     if (!ok && r[0].kind == kStreamLz && argc > 5) {   // dump the stream for offline comparison
       FILE* fo = fopen(argv[5], "wb");
       if (fo) { fwrite(o.data(), 1, o.size(), fo); fclose(fo); }
     }
     double mean = 0; for (auto x : c) mean += x; mean /= nblk;
     printf("blocks %5d: %.3f ms, cycles/stream %.0f, kind %d size %d windows %d %s\n", nblk, ms, mean, r[0].kind,
-           r[0].size, r[0].windows, ok ? "output OK" : "OUTPUT MISMATCH");
+           r[0].size, r[0].windows, ok ? "output OK (expected kind)" : "OUTPUT MISMATCH");
 #ifndef ENC_NOPROF
     uint64_t pr[16];
     hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_enc_prof), sizeof pr);
