@@ -1,6 +1,8 @@
 """The other BASELINE.json configurations on one MI355X (bench.py measures the headline one, T).
 Each prints one JSON line; every run checks its own results.
 
+  C1  b2bench's own config (1e6 int32 get_value(i, 19), 67 x 4 MB, clevel 5 shuffle BloscLZ), GPU
+      batch vs the reference library built here at nthreads 1.
   C2  shuffle filter only, ts=4, 256 MiB gen_f32: one blosc2_shuffle over the whole buffer and the
       unshuffle back, bit-exact against the oracle restatement (blosc/shuffle-generic.c).
   C3  bitshuffle + BloscLZ clevel 5, ts=4, 256 KiB blocks x 4096 chunks (1 GiB gen_f32, continuing
@@ -11,7 +13,7 @@ Each prints one JSON line; every run checks its own results.
       H2D + compress + pack + D2H of the packed compressed bytes, and H2D of those bytes + unpack
       + decompress + D2H (PCIe-inclusive; never `value`); exact host round trip.
 
-    python tools/bench_configs.py [--only C2,C3,C4,E2E] [--steps K]
+    python tools/bench_configs.py [--only C1,C2,C3,C4,E2E,LZ4] [--steps K] [--lz-mode exact|fast]
 """
 import argparse
 import json
@@ -89,7 +91,8 @@ def _batch_roundtrip(name, src_u8, chunk, nch, cp, steps, check):
     exact = bool(torch.equal(out, src_u8[:nch * chunk])) and bool((status == chunk).all())
     C = int(cb.sum().item())
     N = nch * chunk
-    sample_ok = check(comp, cb, stride)
+    # fast mode is round-trip identical, not byte-identical: the oracle comparison is exact mode's
+    sample_ok = check(comp, cb, stride) if B.lib().b2h_set_blosclz_mode(-1) == 0 else "n/a (fast mode)"
     return {"config": name, "round_trip_exact": exact, "sample_chunks_match_oracle": sample_ok,
             "cratio": round(N / C, 4), "compress_ms": round(t_c, 3), "decompress_ms": round(t_d, 3),
             "GiBps_c_plus_d": round(N / GiB / ((t_c + t_d) * 1e-3), 3),
@@ -242,6 +245,64 @@ def e2e(steps, group_chunks=64, nstreams=3):
                                  "unit": "GB/s (H2D + D2H bytes / wall)"}}
 
 
+def c1(steps, nchunks=67, clevel=5):
+    """C1, the reference's own headline CPU benchmark (`b2bench blosclz shuffle single 1 4000000 4
+    19`, bench/b2bench.c:105-274): 1e6 int32 get_value(i, 19) (b2bench.c:73-81), the same 4 MB
+    buffer compressed into 67 chunks (the 256 MiB working set), clevel 5, SHUFFLE, ts 4, BloscLZ.
+    GPU: one batch over the 67 chunks (src_stride 0: every chunk reads the same buffer); CPU: the
+    reference library built here (oracle/_ref), nthreads 1, as b2bench runs it.  MB/s = 1e6 B/s."""
+    from datagen import b2bench_values
+    from oracle_lib import oracle_compress, p, ref
+    size = 4_000_000
+    src = b2bench_values(1_000_000, 19)
+    cap = size + 32
+    stride = (cap + 255) // 256 * 256
+    d_src = torch.from_numpy(src.view(np.uint8).copy()).cuda()
+    comp = torch.empty(nchunks * stride, dtype=torch.uint8, device="cuda")
+    cb = torch.zeros(nchunks, dtype=torch.int32, device="cuda")
+    out = torch.empty(nchunks * size, dtype=torch.uint8, device="cuda")
+    status = torch.zeros(nchunks, dtype=torch.int32, device="cuda")
+    cp = B.cparams(clevel=clevel, typesize=4, filters=(0, 0, 0, 0, 0, B.SHUFFLE))
+    st = torch.cuda.current_stream().cuda_stream
+    t_c = _timed(lambda: B.compress_batch(cp, d_src.data_ptr(), size, nchunks, 0, comp.data_ptr(), stride, cap,
+                                          cb.data_ptr(), st), steps, st)
+    t_d = _timed(lambda: B.decompress_batch(comp.data_ptr(), stride, cb.data_ptr(), nchunks, out.data_ptr(), size,
+                                            size, status.data_ptr(), st), steps, st)
+    cbh = cb.cpu().numpy()
+    want = oracle_compress(src, clevel=clevel, typesize=4, filters=(0, 0, 0, 0, 0, 1))
+    chunk0 = comp[:int(cbh[0])].cpu().numpy()
+    exact = bool((status == size).all()) and bool(torch.equal(out.view(nchunks, size)[nchunks - 1], d_src))
+    res = {"config": "C1: b2bench blosclz shuffle single 1 4000000 4 19 (67 x 4 MB, clevel 5)",
+           "chunk_matches_oracle": bool(np.array_equal(chunk0, want)), "round_trip_exact": exact,
+           "cratio": round(size / float(cbh[0]), 2),
+           "gpu_compress_MBps": round(nchunks * size / (t_c * 1e-3) / 1e6, 1),
+           "gpu_decompress_MBps": round(nchunks * size / (t_d * 1e-3) / 1e6, 1)}
+    R = ref()
+    if R is not None:
+        R.blosc1_set_compressor(b"blosclz")
+        R.blosc2_set_nthreads(1)
+        rsrc = src.copy()
+        dst = np.zeros((nchunks, cap), np.uint8)
+        back = np.zeros(size, np.uint8)
+        tc, td = [], []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            for i in range(nchunks):
+                n = R.blosc1_compress(clevel, 1, 4, size, p(rsrc), p(dst[i]), cap)
+            t1 = time.perf_counter()
+            for i in range(nchunks):
+                R.blosc1_decompress(p(dst[i]), p(back), size)
+            t2 = time.perf_counter()
+            tc.append(t1 - t0)
+            td.append(t2 - t1)
+        res["cpu_reference_nthreads1"] = {
+            "compress_MBps": round(nchunks * size / float(np.median(tc)) / 1e6, 1),
+            "decompress_MBps": round(nchunks * size / float(np.median(td)) / 1e6, 1),
+            "chunk_bytes_equal_gpu": bool(n == int(cbh[0]) and np.array_equal(dst[0][:n], chunk0)),
+            "note": "oracle/_ref, blosc1_compress / blosc1_decompress per chunk, median of 3"}
+    return res
+
+
 def lz4t(steps):
     """T's workload with the LZ4 codec: float32 ts=4 SHUFFLE+LZ4 clevel 5,
     256 KiB blocks (4 x 64 KiB streams), 4 MiB chunks x 1024."""
@@ -255,14 +316,14 @@ def lz4t(steps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="C2,C3,C4,E2E")
+    ap.add_argument("--only", default="C1,C2,C3,C4,E2E")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--lz-mode", default="exact", choices=["exact", "fast"])
     args = ap.parse_args()
     torch.cuda.set_device(0)
     B.lib().b2h_set_blosclz_mode(1 if args.lz_mode == "fast" else 0)
     for name in args.only.split(","):
-        r = {"C2": c2, "C3": c3, "C4": c4, "E2E": e2e, "LZ4": lz4t}[name](args.steps)
+        r = {"C1": c1, "C2": c2, "C3": c3, "C4": c4, "E2E": e2e, "LZ4": lz4t}[name](args.steps)
         print(json.dumps(r), flush=True)
         torch.cuda.empty_cache()
 
