@@ -182,9 +182,12 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
   if (any && matcher) produce(T, 0);         // entering T: T and T + 1
   __syncthreads();
   while (any) {
+    EPROF_T(tm0);
     if (matcher) {
       if (pend >= 0) produce(pend, cur ^ 1);               // the parser jumps to `pend`
       else if ((T + 1) * kFastTile < loop_end) produce(T + 1, cur ^ 1);
+      EPROF_T(tm1);
+      EPROF_ADD(0, tm0, tm1);   // diagnostics: matcher busy
     } else if (pend < 0) {
       // ================= parser: tile T from slot `cur` =================
       int32_t nt = -1;
@@ -366,7 +369,11 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
       } while (false);
       if (lane == 0) sh->ctrl[it & 1] = nt;
     }
+    EPROF_T(tb0);
     __syncthreads();
+    EPROF_T(tb1);
+    if (matcher) EPROF_ADD(4, tb0, tb1);   // diagnostics: barrier wait, matcher / parser
+    else EPROF_ADD(6, tb0, tb1);
     if (pend >= 0) {   // the matcher produced the jump target: the parser takes it next
       T = pend;
       cur ^= 1;

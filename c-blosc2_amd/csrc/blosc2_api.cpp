@@ -762,6 +762,15 @@ void blosc2_destroy(void) {
   g_initlib = false;
 }
 
+int blosc2_free_resources(void) {
+  std::lock_guard<std::mutex> g(g_global_mu);
+  if (!g_initlib) return BLOSC2_ERROR_FAILURE;
+  if (g_global_cctx) g_global_cctx->dev.release();
+  if (g_global_dctx) g_global_dctx->dev.release();
+  b2h::release_device_workspaces();
+  return 0;
+}
+
 const char* blosc2_get_version_string(void) { return BLOSC2_VERSION_STRING; }
 
 // blosc/blosc2.c:6040-6251 (validation + environment overrides)

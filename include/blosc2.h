@@ -329,6 +329,10 @@ typedef struct {
 /* library lifetime: include/blosc2.h:540 (blosc2_init), 551 (blosc2_destroy) */
 BLOSC_EXPORT void blosc2_init(void);
 BLOSC_EXPORT void blosc2_destroy(void);
+/* include/blosc2.h:872 (blosc2_free_resources, blosc/blosc2.c:6001-6006): releases the engine's
+ * device scratch (per-device workspaces, the global contexts' staging); they are re-created on
+ * the next call.  BLOSC2_ERROR_FAILURE when the library is not initialised. */
+BLOSC_EXPORT int blosc2_free_resources(void);
 /* include/blosc2.h:843 (blosc2_get_version_string) */
 BLOSC_EXPORT const char *blosc2_get_version_string(void);
 

@@ -259,3 +259,26 @@ def test_pack_unpack_chunks(B):
     bh = back.cpu().numpy()
     for i in range(n):
         assert np.array_equal(bh[i * stride:i * stride + sizes[i]], h[i * stride:i * stride + sizes[i]]), i
+
+
+# ------------------------------------------------------------------ resource lifetime ----
+def test_free_resources_then_reuse(B):
+    """blosc2_free_resources (ref include/blosc2.h:872, blosc/blosc2.c:6001-6006) releases the
+    engine's device scratch; the next call re-creates it.  Before blosc2_init it fails."""
+    L = B.lib()
+    L.blosc2_free_resources.restype = C.c_int
+    src = gen_f32(3, 1 << 18)
+    want = oracle_compress(src, clevel=5, typesize=4)
+    L.blosc2_init()
+    L.blosc1_set_compressor(b"blosclz")   # the global API's settings (other tests change them)
+    L.blosc1_set_blocksize(C.c_size_t(0))
+    L.blosc1_set_splitmode(4)
+    L.blosc2_set_delta(0)
+    for _ in range(2):
+        out = np.zeros(src.nbytes + 32, np.uint8)
+        n = L.blosc2_compress(5, 1, 4, B._p(src), src.nbytes, B._p(out), out.nbytes)
+        assert n == want.nbytes and np.array_equal(out[:n], want)
+        assert L.blosc2_free_resources() == 0
+    L.blosc2_destroy()
+    assert L.blosc2_free_resources() == -1   # BLOSC2_ERROR_FAILURE: not initialised
+    L.blosc2_init()

@@ -75,7 +75,7 @@ int main(int argc, char** argv) {
            r[0].kind, r[0].size, r[0].windows, mean / (r[0].windows ? r[0].windows : 1));
     uint64_t pr[16];
     hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_enc_prof), sizeof pr);
-    const char* nm[8] = {"issue+wait", "compare", "chain walk", "emit", "advance", "(match ext)", "flush", "-"};
+    const char* nm[8] = {"M: produce", "P: compare", "P: chain walk", "P: emit", "M: barrier", "P: (match ext)", "P: barrier", "-"};
     for (int pass = 1; pass >= 0; pass--)
       for (int i = 0; i < 7; i++)
         printf("   %s %-12s %10.0f cycles/stream\n", pass ? "probe" : "main ", nm[i], pr[8 * pass + i] / (double)nblk);
