@@ -61,11 +61,16 @@ int compress_batch(const CompressPlan& plan, const uint8_t* d_src, int64_t src_s
 // tables are then sized from it (every block has a 4-byte bstart, every stream a 4-byte csize word)
 // and the call never waits on the host (a batch that exceeds the bounds fails per chunk with
 // BLOSC2_ERROR_MEMORY_ALLOC).  src_bound < 0: the tables are sized exactly, which costs one
-// synchronisation of `stream`.
+// synchronisation of `stream`.  `mode`: kDecRawStreams (decode the streams only) | kDecDeltaSelf
+// (every block un-deltas against itself, as blosc_d with dest_offset 0 does for getitem /
+// decompress_block) | kDecNoDict (the dictionary flag is not read: those entry points never parse
+// the dictionary section).  Errors are the reference's for the same chunk: its chunk-level checks in
+// order, then the first failure of its serial block walk (blosc/blosc2.c:2177-2225).
+enum { kDecRawStreams = 1, kDecDeltaSelf = 2, kDecNoDict = 4 };
 int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint8_t* const* d_dst,
                      const int32_t* d_dstsize, int32_t n, int64_t dst_bound, int32_t* d_status,
                      const uint8_t* d_maskout, hipStream_t stream, Workspace* ws = nullptr,
-                     int64_t src_bound = -1, int raw_streams = 0, int32_t mask_stride = 0);
+                     int64_t src_bound = -1, int mode = 0, int32_t mask_stride = 0);
 
 // Strided convenience form: chunk i at d_src + i*src_stride with cbytes d_cbytes[i], output at
 // d_dst + i*dst_stride with capacity dst_cap.
@@ -86,7 +91,7 @@ int unpack_chunks(const uint8_t* d_src, const int64_t* d_offsets, int32_t n, uin
 // Single-chunk stages of host-driven pipelines (chunks with user-registered filters / codecs):
 // one forward filter slot of P over the blocks of `pass` (0 all, 1 block 0, 2 blocks >= 1); the
 // built-in codec stage from an already-filtered image; one backward filter over a pass.  Device
-// buffers need >= 256 bytes of slack.  decompress_batch(..., raw_streams = 1) decodes the streams
+// buffers need >= 256 bytes of slack.  decompress_batch(..., kDecRawStreams) decodes the streams
 // only, leaving the backward filters to the caller.
 int forward_filter_chunk(const CompressPlan& P, int slot, int pass, const uint8_t* d_in, uint8_t* d_out,
                          const uint8_t* d_raw, hipStream_t stream);

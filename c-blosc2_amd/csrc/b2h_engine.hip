@@ -33,9 +33,12 @@ namespace b2h {
 
 // error codes (include/blosc2.h:453-492)
 enum {
-  E_FAILURE = -1, E_DATA = -3, E_MEMORY = -4, E_READ = -5, E_WRITE = -6, E_CODEC = -7, E_VERSION = -10,
-  E_HEADER = -11, E_PARAM = -12, E_RUNLEN = -17, E_FILTER = -18, E_MAXBUF = -35,
+  E_FAILURE = -1, E_DATA = -3, E_MEMORY = -4, E_READ = -5, E_WRITE = -6, E_CODEC = -7, E_DICT = -9,
+  E_VERSION = -10, E_HEADER = -11, E_PARAM = -12, E_RUNLEN = -17, E_FILTER = -18, E_MAXBUF = -35,
 };
+constexpr int32_t kMaxBlocksize = 536866816;   // BLOSC2_MAXBLOCKSIZE (include/blosc2.h:302)
+constexpr uint8_t kFlag2VL = 0x1;              // BLOSC2_VL_BLOCKS in blosc2_flags2 (include/blosc2.h:293)
+constexpr uint8_t kUseDict = 0x1;              // BLOSC2_USEDICT in blosc2_flags (include/blosc2.h:284)
 
 static thread_local char g_err[256];
 const char* last_error() { return g_err; }
@@ -1402,14 +1405,23 @@ __device__ __forceinline__ int32_t rd32(const uint8_t* p) {
 // backward is a plain copy (plugins/filters/int_trunc/int_trunc.c:116-125).
 __host__ __device__ __forceinline__ bool bwd_noop(uint8_t f) { return f == kNoFilter || f == kTruncPrec || f == kIntTrunc; }
 
-// read_chunk_header + initialize_context_decompression (blosc/blosc2.c:738-852, 2688-2909)
+// The chunk-level checks of a decompression, in the reference's order and with its codes:
+// read_chunk_header (blosc/blosc2.c:738-852), the destination check of
+// blosc_run_decompression_with_context (3921-3924), blosc2_initialize_context_from_header
+// (862-910) and initialize_context_decompression (2723-2906).  Block-level failures (bstarts,
+// stream sizes, decoding, the filter pipeline) are keyed by position in DChunk::errkey, so the
+// batch reports the error the reference's serial block walk meets first.
+// mode bit 0: raw streams (host-driven pipelines apply the filters); bit 1: every block
+// un-deltas against itself (blosc_d with dest_offset 0: getitem / decompress_block); bit 2: the
+// dictionary flag is not read (those two entry points never parse the section).
 __global__ void k_dplan_chunks(const uint8_t* const* __restrict__ srcs, const int32_t* __restrict__ srcsize,
                                const int32_t* __restrict__ dstsize, DChunk* __restrict__ ch, int32_t n,
-                               int raw_streams) {
+                               int mode) {
   const int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= n) return;
   DChunk d;
   memset(&d, 0, sizeof d);
+  d.errkey = kNoErr;
   const uint8_t* s = srcs[c];
   const int32_t ss = srcsize[c];
   auto fail = [&](int32_t code) { d.status = code; d.nstreams = 0; d.nblocks = 0; ch[c] = d; };
@@ -1418,68 +1430,105 @@ __global__ void k_dplan_chunks(const uint8_t* const* __restrict__ srcs, const in
   d.flags = s[2];
   d.typesize = s[3];
   d.nbytes = rd32(s + 4);
-  d.blocksize = rd32(s + 8);
+  int32_t bs = rd32(s + 8);
   const int32_t cb = rd32(s + 12);
-  if (cb < kHdrMin || d.blocksize <= 0 || d.blocksize > 536866816 || d.typesize == 0) return fail(E_HEADER);
+  if (cb < kHdrMin || bs <= 0 || bs > kMaxBlocksize || d.typesize == 0) return fail(E_HEADER);
   const bool ext = (d.flags & kFlagShuffle) && (d.flags & kFlagBitshuffle);
+  uint8_t flags2 = 0, bflags = 0;
   if (ext) {
-    if (cb < kHdrExt || ss < kHdrExt) return fail(ss < kHdrExt ? E_READ : E_HEADER);
+    if (cb < kHdrExt) return fail(E_HEADER);
+    if (ss < kHdrExt) return fail(E_READ);
     for (int i = 0; i < 6; i++) { d.filters[i] = s[16 + i]; d.filters_meta[i] = s[24 + i]; }
     d.codec = s[22];
-    const uint8_t flags2 = s[30], bflags = s[31];
-    if (flags2 != 0) return fail(E_VERSION);          // VL blocks: not on the device path
-    if (bflags & 0x08) return fail(E_PARAM);            // lazy chunks need a frame
-    if (bflags & 0x01) return fail(E_CODEC);            // dictionaries: LZ4/ZSTD only
+    flags2 = s[30];
+    bflags = s[31];
     d.special = (bflags >> 4) & 7;
+    if ((flags2 & kFlag2VL) && d.special != 0) return fail(E_HEADER);
+    if (d.special == kSpecialValue) {
+      const int32_t vts = cb - kHdrExt;
+      if (vts <= 0 || vts > kMaxBlocksize || vts > d.nbytes || d.nbytes % vts != 0) return fail(E_HEADER);
+    } else if (d.special != 0 && d.special != kSpecialZero && d.nbytes % d.typesize != 0) {
+      return fail(E_HEADER);
+    }
     if (d.version == 3) { d.filters[5] = 0; d.filters_meta[5] = 0; }
     d.overhead = kHdrExt;
   } else {
-    // flags_to_filters + get_filter_flags (blosc/blosc2.c:704-735)
-    if ((d.flags & kFlagShuffle) && d.typesize > 1) d.filters[5] = kShuffle;
+    // flags_to_filters (blosc/blosc2.c:704-735)
+    if (d.flags & kFlagShuffle) d.filters[5] = kShuffle;
     if (d.flags & kFlagBitshuffle) d.filters[5] = kBitshuffle;
     if (d.flags & kFlagDelta) d.filters[4] = kDelta;
     d.overhead = kHdrMin;
   }
-  // special-chunk header checks of read_chunk_header (blosc/blosc2.c:796-825)
-  if (d.special == kSpecialValue) {
-    const int32_t vts = cb - kHdrExt;
-    if (vts <= 0 || vts > 536866816 || vts > d.nbytes || d.nbytes % vts != 0) return fail(E_HEADER);
-  } else if (d.special != 0 && d.special != kSpecialZero && d.nbytes % d.typesize != 0) {
-    return fail(E_HEADER);
-  }
-  // set_nans handles float32 / float64 only (blosc/blosc2.c:1612-1636)
-  if (d.special == kSpecialNan && d.nbytes > 0 && d.typesize != 4 && d.typesize != 8) return fail(E_DATA);
-  if (d.nbytes > 0 && d.blocksize > d.nbytes) d.blocksize = d.nbytes;
-  if (cb > ss) return fail(E_HEADER);
-  if (d.nbytes > dstsize[c]) return fail(E_WRITE);
-  if (d.special > kSpecialUninit) return fail(E_DATA);
+  if (d.version > 6 && (flags2 & ~kFlag2VL)) return fail(E_VERSION);
+  const bool vl = flags2 & kFlag2VL;
   const bool memcpyed = d.flags & kFlagMemcpy;
+  if (vl && memcpyed) return fail(E_HEADER);
+  if (!vl && d.nbytes > 0 && bs > d.nbytes) bs = d.nbytes;
+  if (d.nbytes > dstsize[c]) return fail(E_WRITE);
+  // blosc2_calculate_blocks (854-860); VL chunks carry their block count in the blocksize field
+  int32_t nblocks = vl ? bs : d.nbytes / bs;
+  d.leftover = vl ? 0 : d.nbytes % bs;
+  if (d.leftover > 0) nblocks++;
+  d.blocksize = bs;
+  const bool lazy = ext && (bflags & 0x08);
+  if (!lazy && cb > ss) return fail(E_HEADER);
+  if (d.special > kSpecialUninit) return fail(E_DATA);
   if (memcpyed && cb != d.nbytes + d.overhead) return fail(E_DATA);
-  d.status = d.nbytes;
-  d.nblocks = d.nbytes / d.blocksize + (d.nbytes % d.blocksize ? 1 : 0);
-  d.leftover = d.nbytes % d.blocksize;
+  d.status = max(d.nbytes, 0);
+  if (d.nbytes == 0 && cb == d.overhead && !d.special) return fail(0);
+  int64_t bstarts_end = d.overhead;
+  if (!d.special && !memcpyed) {
+    bstarts_end += 4 * (int64_t)nblocks;
+    if (nblocks < 0 || bstarts_end > 0x7fffffff) return fail(E_HEADER);
+  }
+  if (ss < bstarts_end) return fail(E_READ);
+  if (vl && lazy && !d.special && !memcpyed && (int64_t)ss < bstarts_end + 12 + 4 * (int64_t)nblocks)
+    return fail(E_READ);
+  if ((bflags & kUseDict) && !lazy && !(mode & 4)) {
+    // the dictionary section after the bstarts: [int32 size | bytes] (2790-2825); BloscLZ and
+    // the LZ4 streams of these chunks reference nothing in it
+    const int64_t rem = ss - bstarts_end;
+    if (rem < 4) return fail(E_READ);
+    const int32_t dsz = rd32(s + bstarts_end);
+    if (dsz <= 0 || dsz > 32 * 1024) return fail(E_DICT);
+    if (rem - 4 < dsz) return fail(E_READ);
+  }
+  if (vl && !d.special && !memcpyed) return fail(E_VERSION);   // VL-block chunks: not on the device path
   d.dont_split = (d.flags >> 4) & 1;
-  if (d.nbytes == 0 || memcpyed || d.special) {
+  d.delta_self = (mode >> 1) & 1;
+  if (nblocks <= 0) return fail(d.status = 0);   // the block walk has nothing to do
+  if (lazy && !d.special) return fail(E_PARAM);   // lazy chunks need their frame (blosc_d 1757-1766)
+  if (memcpyed || d.special) {
+    // blosc_d's memcpyed path (1865-1935): set_nans / set_values need whole items in every block
+    const int32_t ts = d.special == kSpecialValue ? cb - kHdrExt : d.typesize;
+    const bool full_blocks = nblocks - (d.leftover ? 1 : 0) > 0;
+    if ((d.special == kSpecialNan || d.special == kSpecialValue) &&
+        ((full_blocks && bs % ts) || (d.leftover && d.leftover % ts)))
+      return fail(E_DATA);
+    if (d.special == kSpecialNan && ts != 4 && ts != 8) return fail(E_DATA);
     d.nblocks = 0;   // handled by k_dspecial, not by the block table
     d.nstreams = 0;
     ch[c] = d;
     return;
   }
-  if (ss < d.overhead + 4 * d.nblocks) return fail(E_READ);
+  d.nblocks = nblocks;
   const int32_t spb = d.dont_split ? 1 : d.typesize;
   d.nstreams = (d.nblocks - (d.leftover ? 1 : 0)) * spb + (d.leftover ? 1 : 0);
-  if (raw_streams) {   // the caller applies the filters itself (host-driven pipelines)
+  if (mode & 1) {   // the caller applies the filters itself (host-driven pipelines)
     d.nfilters_bwd = 0;
     ch[c] = d;
     return;
   }
-  // backward pipeline: active filters (not NOFILTER / TRUNC_PREC), applied high slot -> low
+  // backward pipeline (pipeline_backward, 1473-1609): active filters (not NOFILTER / TRUNC_PREC)
+  // from slot 5 down; an unknown id <= 31 fails the block with -1 after the pass, a filter id > 31
+  // other than the device plugins with FILTER_PIPELINE (user filters take the host path)
   int k = 0, K = 0;
   for (int i = 5; i >= 0; i--) if (!bwd_noop(d.filters[i])) K++;
   for (int i = 5; i >= 0; i--) {
     const uint8_t f = d.filters[i];
     if (bwd_noop(f)) continue;
-    if (f > kTruncPrec && f != kBytedelta) return fail(E_FILTER);   // other user filters: not on device
+    if (f > 31 && f != kBytedelta) d.ferr = (int8_t)E_FILTER;
+    else if (f > kTruncPrec && f <= 31 && d.ferr == 0) d.ferr = (int8_t)E_FAILURE;
     d.has_delta |= f == kDelta;
     d.fsrc[i] = (k % 2 == 0) ? 0 : 1;
     d.fdst[i] = (k == K - 1) ? 2 : ((k % 2 == 0) ? 1 : 0);
@@ -1578,10 +1627,18 @@ __device__ int32_t find_chunk(const DChunk* ch, int32_t n, int32_t idx) {
 // Pull order of the decoder: LZ / LZ4 streams (thousands of tokens each; on T one per block, ~90 %
 // of the decode wave-time) from the front, raw copies and runs (a 64 KiB memcpy / memset) from the
 // back, so the long streams start first and the short ones fill the end of the launch.
+__device__ __forceinline__ void rec_err(DChunk* ch, int32_t c, int32_t block, int32_t step, int32_t code) {
+  atomicMin(reinterpret_cast<unsigned long long*>(&ch[c].errkey), (unsigned long long)err_key(block, step, code));
+}
+
+// One block of the walk (blosc_d, blosc/blosc2.c:1734-2016): a masked block is skipped before any
+// check; then the bstart (1937-1940), the stream count (1982-1986) and each stream's size words
+// (2002-2015), every failure keyed by its position.
 __device__ void dplan_block(const uint8_t* const* __restrict__ srcs, const int32_t* __restrict__ srcsize,
                             DChunk* __restrict__ ch, int32_t n, DBlock* __restrict__ blocks,
                             DStream* __restrict__ streams, int32_t idx, int32_t* __restrict__ order,
-                            int32_t* __restrict__ octr, int32_t nstreams) {
+                            int32_t* __restrict__ octr, int32_t nstreams, const uint8_t* __restrict__ maskout,
+                            int32_t mask_stride) {
   const int32_t c = find_chunk(ch, n, idx);
   const DChunk d = ch[c];
   const int32_t b = idx - d.block_base;
@@ -1594,10 +1651,14 @@ __device__ void dplan_block(const uint8_t* const* __restrict__ srcs, const int32
   const int32_t ns = (!d.dont_split && !lo) ? d.typesize : 1;
   const int32_t neblock = bsize / ns;
   const int32_t sbase = d.stream_base + b * (d.dont_split ? 1 : d.typesize);
+  const bool masked = maskout && maskout[(int64_t)c * mask_stride + b];
   int32_t pos = rd32(s + d.overhead + 4 * b);
   int32_t err = 0;
-  if (pos <= 0 || pos >= ss) err = E_DATA;
-  if (neblock == 0) err = E_WRITE;
+  if (masked) err = 1;   // no stream is planned and nothing is recorded
+  else if (pos <= 0 || pos >= ss) err = E_DATA;
+  else if (neblock == 0) err = E_WRITE;
+  if (err < 0) rec_err(ch, c, b, 0, err);
+  else if (!masked && d.ferr) rec_err(ch, c, b, kStepFilters, d.ferr);
   for (int32_t j = 0; j < ns; j++) {
     DStream st;
     st.chunk = c;
@@ -1606,8 +1667,9 @@ __device__ void dplan_block(const uint8_t* const* __restrict__ srcs, const int32
     st.csize = 0;
     st.src = 0;
     if (!err) {
-      if (ss - pos < 4) { err = E_READ; }
-      else {
+      if (ss - pos < 4) {
+        err = E_READ;
+      } else {
         const int32_t cs = rd32(s + pos);
         pos += 4;
         int32_t payload = cs > 0 ? cs : (cs < 0 ? 1 : 0);
@@ -1616,6 +1678,7 @@ __device__ void dplan_block(const uint8_t* const* __restrict__ srcs, const int32
         st.src = pos;
         pos += payload;
       }
+      if (err) rec_err(ch, c, b, 1 + j, err);
     }
     if (err) st.neblock = -1;
     streams[sbase + j] = st;
@@ -1623,16 +1686,16 @@ __device__ void dplan_block(const uint8_t* const* __restrict__ srcs, const int32
     const int32_t slot = heavy ? atomicAdd(&octr[0], 1) : nstreams - 1 - atomicAdd(&octr[1], 1);
     order[slot] = sbase + j;
   }
-  if (err) atomicMin(&ch[c].status, err);
 }
 
 __global__ void k_dplan_blocks(const uint8_t* const* __restrict__ srcs, const int32_t* __restrict__ srcsize,
                                DChunk* __restrict__ ch, int32_t n, DBlock* __restrict__ blocks,
                                DStream* __restrict__ streams, const DTotals* __restrict__ tot,
-                               int32_t* __restrict__ order, int32_t* __restrict__ octr) {
+                               int32_t* __restrict__ order, int32_t* __restrict__ octr,
+                               const uint8_t* __restrict__ maskout, int32_t mask_stride) {
   const int32_t nb = tot->nblocks, ns = tot->nstreams;
   for (int32_t idx = blockIdx.x * blockDim.x + threadIdx.x; idx < nb; idx += gridDim.x * blockDim.x)
-    dplan_block(srcs, srcsize, ch, n, blocks, streams, idx, order, octr, ns);
+    dplan_block(srcs, srcsize, ch, n, blocks, streams, idx, order, octr, ns, maskout, mask_stride);
 }
 
 // Decoder: one wave per stream, persistent (as many single-wave workgroups as the LDS ring
@@ -1657,12 +1720,15 @@ __device__ __forceinline__ void decode_stream(const uint8_t* const* __restrict__
   gin_t in = (gin_t)(srcs[c] + st.src);
   gout_t out = (gout_t)((d.nfilters_bwd ? stage + d.stage_off : dsts[c]) + st.dst_off);
   const int32_t nb = st.neblock;
+  // the stream's place in the serial walk, for the error key
+  const int32_t blk = st.dst_off / d.blocksize;
+  const int32_t step = 1 + (st.dst_off - blk * d.blocksize) / nb;
   if (st.csize == 0) {
     wave_fill(out, 0, nb);
   } else if (st.csize < 0) {
     const uint8_t token = in[0];
     if (!(token & 1) || st.csize < -255) {
-      if (lane == 0) atomicMin(&ch[c].status, E_RUNLEN);
+      if (lane == 0) rec_err(ch, c, blk, step, E_RUNLEN);
     } else {
       wave_fill(out, (uint8_t)(-st.csize), nb);
       *kind_out = 1;
@@ -1672,13 +1738,13 @@ __device__ __forceinline__ void decode_stream(const uint8_t* const* __restrict__
     *kind_out = 2;
   } else if ((d.flags >> 5) == 1) {   // LZ4 (blosc/blosc2.c:2062-2067)
     const int32_t got = wave_lz4_decode_ring<RLOG>(in, st.csize, out, nb, ring);
-    if (got != nb && lane == 0) atomicMin(&ch[c].status, E_DATA);
+    if (got != nb && lane == 0) rec_err(ch, c, blk, step, E_DATA);
     *kind_out = 4;
   } else if ((d.flags >> 5) != 0) {
-    if (lane == 0) atomicMin(&ch[c].status, E_CODEC);
+    if (lane == 0) rec_err(ch, c, blk, step, E_CODEC);
   } else {
     const int32_t got = wave_lz_decode_par<RLOG>(in, st.csize, out, nb, ring);
-    if (got != nb && lane == 0) atomicMin(&ch[c].status, E_DATA);
+    if (got != nb && lane == 0) rec_err(ch, c, blk, step, E_DATA);
     *kind_out = 3;
   }
 }
@@ -1742,7 +1808,7 @@ __device__ __forceinline__ void dfilter_block(DChunk* __restrict__ ch, const DBl
   if (fused_delta_shuffle(d, bsize) && aligned16(bufs[0]) && aligned16(bufs[2]) && aligned16(dsts[bk.chunk])) {
     if (slot != 5) return;
     const int32_t ne = bsize / d.typesize;
-    if (bk.block == 0) {
+    if (bk.block == 0 || d.delta_self) {
       if (d.typesize == 4) unshuffle_scan_fast<4>(bufs[0], bufs[2], ne);
       else if (d.typesize == 8) unshuffle_scan_fast<8>(bufs[0], bufs[2], ne);
       else unshuffle_scan_fast<2>(bufs[0], bufs[2], ne);
@@ -1761,7 +1827,7 @@ __device__ __forceinline__ void dfilter_block(DChunk* __restrict__ ch, const DBl
     case kBitshuffle: block_bitunshuffle(s, o, bsize, d.typesize, d.version); break;
     case kBytedelta: block_bytedelta_decode(s, o, bsize, meta ? meta : d.typesize); break;
     case kDelta:
-      if (bk.block == 0) block_delta_decode_first(s, o, bsize, d.typesize);
+      if (bk.block == 0 || d.delta_self) block_delta_decode_first(s, o, bsize, d.typesize);
       else block_delta_decode_rest(s, dsts[bk.chunk], o, bsize, d.typesize);
       break;
     default: break;
@@ -1820,7 +1886,9 @@ __global__ void k_dspecial(const uint8_t* const* __restrict__ srcs, uint8_t* con
 
 __global__ void k_dstatus(const DChunk* __restrict__ ch, int32_t* __restrict__ status, int32_t n) {
   const int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < n) status[c] = ch[c].status;
+  if (c >= n) return;
+  const DChunk& d = ch[c];
+  status[c] = (d.status >= 0 && d.errkey != kNoErr) ? -(int32_t)(d.errkey & 0xff) : d.status;
 }
 
 static int dec_ring_log() {
@@ -1846,7 +1914,7 @@ static void launch_decode(const uint8_t* const* d_src, uint8_t* const* d_dst, DC
 static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const int32_t* d_srcsize,
                              uint8_t* const* d_dst, const int32_t* d_dstsize, int32_t n, int64_t dst_bound,
                              int32_t* d_status, const uint8_t* d_maskout, hipStream_t st, int64_t src_bound,
-                             int raw_streams = 0, int32_t mask_stride = 0) {
+                             int mode = 0, int32_t mask_stride = 0) {
   if (ws->dchunks.ensure(sizeof(DChunk) * (size_t)n) < 0 || ws->dtotals.ensure(sizeof(DTotals)) < 0) return E_MEMORY;
   DChunk* ch = ws->dchunks.as<DChunk>();
   DTotals* tot = ws->dtotals.as<DTotals>();
@@ -1858,7 +1926,7 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
     cap_blocks = cap_streams = src_bound / 4 + 1;
     cap_stage = std::max<int64_t>(dst_bound, 0);
   }
-  k_dplan_chunks<<<(n + 255) / 256, 256, 0, st>>>(d_src, d_srcsize, d_dstsize, ch, n, raw_streams);
+  k_dplan_chunks<<<(n + 255) / 256, 256, 0, st>>>(d_src, d_srcsize, d_dstsize, ch, n, mode);
   k_dscan<<<1, 1024, 0, st>>>(ch, n, tot, cap_blocks, cap_streams, cap_stage);
   HIPCHK(hipGetLastError());
   DTotals h{};
@@ -1889,7 +1957,8 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
     int32_t* next = ws->dqctr.as<int32_t>();   // [0]: the decoder's pull counter, [1..2]: the order's ends
     HIPCHK(hipMemsetAsync(next, 0, 4 * sizeof(int32_t), st));
     const int64_t pb_grid = std::max<int64_t>(1, std::min<int64_t>((h.nblocks + 255) / 256, 4096));
-    k_dplan_blocks<<<(uint32_t)pb_grid, 256, 0, st>>>(d_src, d_srcsize, ch, n, blocks, streams, tot, order, next + 1);
+    k_dplan_blocks<<<(uint32_t)pb_grid, 256, 0, st>>>(d_src, d_srcsize, ch, n, blocks, streams, tot, order, next + 1,
+                                                       d_maskout, mask_stride);
     ev_decode.start(st);
     {
       int64_t* dbg = nullptr;
@@ -1935,14 +2004,14 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
 
 int decompress_batch(const uint8_t* const* d_src, const int32_t* d_srcsize, uint8_t* const* d_dst,
                      const int32_t* d_dstsize, int32_t n, int64_t dst_bound, int32_t* d_status,
-                     const uint8_t* d_maskout, hipStream_t st, Workspace* wsx, int64_t src_bound, int raw_streams,
+                     const uint8_t* d_maskout, hipStream_t st, Workspace* wsx, int64_t src_bound, int mode,
                      int32_t mask_stride) {
   if (n <= 0) return 0;
   Workspace* ws = wsx ? wsx : ws_for_current_device();
   WsUse use(ws, st);
   if (use.rc) return use.rc;
   return decompress_locked(ws, d_src, d_srcsize, d_dst, d_dstsize, n, dst_bound, d_status, d_maskout, st, src_bound,
-                           raw_streams, mask_stride);
+                           mode, mask_stride);
 }
 
 __global__ void k_fill_ptrs(const uint8_t* src, int64_t src_stride, const int32_t* cbytes, uint8_t* dst, int64_t dst_stride,

@@ -43,7 +43,11 @@ struct StreamResult {
 // One chunk of a decompression batch after header parsing (device-side plan).
 struct DChunk {
   int64_t stage_off;     // offset of this chunk's staging area (sum of previous nbytes)
-  int32_t status;        // >= 0: nbytes; < 0: BLOSC2_ERROR_*
+  // First error of the block walk in the reference's serial order (blosc/blosc2.c:2177-2225):
+  // (block << 20 | step << 8 | -code), step 0 = the block's bstart / size checks, 1 + j = stream
+  // j, kStepFilters = the backward pipeline; atomicMin keeps the earliest.  kNoErr: none.
+  uint64_t errkey;
+  int32_t status;        // >= 0: nbytes; < 0: BLOSC2_ERROR_* (header-level checks)
   int32_t nbytes;
   int32_t blocksize;
   int32_t nblocks;
@@ -57,8 +61,16 @@ struct DChunk {
   uint8_t filters_meta[kMaxFilters];
   uint8_t fsrc[kMaxFilters];   // per backward slot: buffer the stage reads (0 stage,1 tmp,2 dst)
   uint8_t fdst[kMaxFilters];   // per backward slot: buffer the stage writes
-  uint8_t codec, pad0, pad1, pad2;
+  uint8_t codec, delta_self;   // delta_self: every block un-deltas against itself (dest_offset 0)
+  int8_t ferr;                 // backward-pipeline error of every decoded block (0, -1, -18)
+  uint8_t pad0;
 };
+
+constexpr uint64_t kNoErr = ~0ull;
+constexpr int32_t kStepFilters = 4095;
+constexpr uint64_t err_key(int32_t block, int32_t step, int32_t code) {
+  return ((uint64_t)(uint32_t)block << 20) | ((uint64_t)step << 8) | (uint64_t)(uint8_t)(-code);
+}
 
 // One LZ/raw/run stream of a decompression batch.
 struct DStream {

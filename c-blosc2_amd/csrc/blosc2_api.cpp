@@ -244,60 +244,116 @@ int compress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void* d
   return cb;
 }
 
-// Host-side mirror of read_chunk_header's size fields (blosc/blosc2.c:738-777), used for staging.
-int peek_header(const void* src, int32_t srcsize, int32_t* nbytes, int32_t* cbytes, int32_t* blocksize) {
+// Host mirror of read_chunk_header (blosc/blosc2.c:738-852, extended headers read) and
+// blosc2_initialize_context_from_header (862-910): the same checks, order and codes as the
+// reference and as the device planner (b2h_engine.hip k_dplan_chunks), for the entry points that
+// need the geometry on the host (staging sizes, masks, getitem, decompress_block).
+struct ChunkHdr {
+  int32_t nbytes, blocksize, cbytes;   // blocksize clamped to nbytes as the reference does
+  uint8_t version, flags, typesize, flags2, bflags, special;
+  bool ext, vl, memcpyed, lazy;
+  int32_t overhead, nblocks, leftover;
+};
+
+int read_header(const void* src, int32_t srcsize, ChunkHdr* h) {
+  memset(h, 0, sizeof *h);
   if (srcsize < BLOSC_MIN_HEADER_LENGTH) return BLOSC2_ERROR_READ_BUFFER;
   const uint8_t* s = static_cast<const uint8_t*>(src);
-  *nbytes = rd32(s + 4);
-  *blocksize = rd32(s + 8);
-  *cbytes = rd32(s + 12);
-  if (*cbytes < BLOSC_MIN_HEADER_LENGTH) return BLOSC2_ERROR_INVALID_HEADER;
-  if (*blocksize <= 0 || *blocksize > BLOSC2_MAXBLOCKSIZE || s[3] == 0) return BLOSC2_ERROR_INVALID_HEADER;
+  h->version = s[0];
+  h->flags = s[2];
+  h->typesize = s[3];
+  h->nbytes = rd32(s + 4);
+  h->blocksize = rd32(s + 8);
+  h->cbytes = rd32(s + 12);
+  if (h->cbytes < BLOSC_MIN_HEADER_LENGTH) return BLOSC2_ERROR_INVALID_HEADER;
+  if (h->blocksize <= 0 || h->blocksize > BLOSC2_MAXBLOCKSIZE) return BLOSC2_ERROR_INVALID_HEADER;
+  if (h->typesize == 0) return BLOSC2_ERROR_INVALID_HEADER;
+  h->ext = (h->flags & BLOSC_DOSHUFFLE) && (h->flags & BLOSC_DOBITSHUFFLE);
+  if (h->ext) {
+    if (h->cbytes < BLOSC_EXTENDED_HEADER_LENGTH) return BLOSC2_ERROR_INVALID_HEADER;
+    if (srcsize < BLOSC_EXTENDED_HEADER_LENGTH) return BLOSC2_ERROR_READ_BUFFER;
+    h->flags2 = s[BLOSC2_CHUNK_BLOSC2_FLAGS2];
+    h->bflags = s[BLOSC2_CHUNK_BLOSC2_FLAGS];
+    h->special = (h->bflags >> 4) & BLOSC2_SPECIAL_MASK;
+    if ((h->flags2 & BLOSC2_VL_BLOCKS) && h->special != 0) return BLOSC2_ERROR_INVALID_HEADER;
+    if (h->special == BLOSC2_SPECIAL_VALUE) {
+      const int32_t vts = h->cbytes - BLOSC_EXTENDED_HEADER_LENGTH;
+      if (vts <= 0 || vts > BLOSC2_MAXTYPESIZE || vts > h->nbytes || h->nbytes % vts != 0)
+        return BLOSC2_ERROR_INVALID_HEADER;
+    } else if (h->special != 0 && h->special != BLOSC2_SPECIAL_ZERO && h->nbytes % h->typesize != 0) {
+      return BLOSC2_ERROR_INVALID_HEADER;
+    }
+  }
+  if (h->version > BLOSC2_VERSION_FORMAT && (h->flags2 & (uint8_t)~BLOSC2_VL_BLOCKS) != 0)
+    return BLOSC2_ERROR_VERSION_SUPPORT;
+  h->vl = h->flags2 & BLOSC2_VL_BLOCKS;
+  h->memcpyed = h->flags & BLOSC_MEMCPYED;
+  if (h->vl && h->memcpyed) return BLOSC2_ERROR_INVALID_HEADER;
+  if (!h->vl && h->nbytes > 0 && h->blocksize > h->nbytes) h->blocksize = h->nbytes;
+  return 0;
+}
+
+int init_from_header(ChunkHdr* h, int32_t srcsize) {
+  if (h->vl) {
+    h->nblocks = h->blocksize;
+    h->leftover = 0;
+  } else {
+    h->nblocks = h->nbytes / h->blocksize;
+    h->leftover = h->nbytes % h->blocksize;
+    if (h->leftover > 0) h->nblocks++;
+  }
+  h->overhead = h->ext ? BLOSC_EXTENDED_HEADER_LENGTH : BLOSC_MIN_HEADER_LENGTH;
+  h->lazy = h->ext && (h->bflags & 0x08);
+  if (!h->lazy && h->cbytes > srcsize) return BLOSC2_ERROR_INVALID_HEADER;
   return 0;
 }
 
 // Decompress one host chunk through the engine.  With a block mask only unmasked blocks are
 // copied back so masked regions of `dest` keep the caller's bytes (blosc/blosc2.c:1734-1737).
+// `mode`: b2h::kDecDeltaSelf for the per-block entry points (getitem, decompress_block).
 int decompress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void* dest, int32_t destsize,
-                    const std::vector<uint8_t>* mask) {
-  int32_t nbytes, cbytes, bs;
-  int rc = peek_header(src, srcsize, &nbytes, &cbytes, &bs);
+                    const std::vector<uint8_t>* mask, int mode = 0) {
+  ChunkHdr H;
+  int rc = read_header(src, srcsize, &H);
   if (rc < 0) return rc;
-  if (nbytes > destsize) return BLOSC2_ERROR_WRITE_BUFFER;
-  if (cbytes > srcsize) return BLOSC2_ERROR_INVALID_HEADER;
-  if (nbytes > 0 && bs > nbytes) bs = nbytes;
-  const int32_t nblocks = nbytes > 0 ? nbytes / bs + (nbytes % bs ? 1 : 0) : 0;
+  if (H.nbytes > destsize) return BLOSC2_ERROR_WRITE_BUFFER;
+  if ((rc = init_from_header(&H, srcsize)) < 0) return rc;
+  const int32_t nbytes = H.nbytes, bs = H.blocksize, nblocks = H.nblocks;
   if (mask && (int32_t)mask->size() != nblocks) {
     TRACE_ERROR("The number of items in block_maskout (%zu) must match the number of blocks in chunk (%d).",
                 mask->size(), nblocks);
     return BLOSC2_ERROR_DATA;
   }
-  {
-    // user filters / codecs in an extended header (not memcpyed, not special) -> host callbacks
-    const uint8_t* s = static_cast<const uint8_t*>(src);
-    const bool ext = (s[2] & BLOSC_DOSHUFFLE) && (s[2] & BLOSC_DOBITSHUFFLE);
-    if (ext && srcsize >= BLOSC_EXTENDED_HEADER_LENGTH && !(s[2] & BLOSC_MEMCPYED) && ((s[31] >> 4) & 7) == 0 &&
-        nbytes > 0) {
-      uint8_t fl[6];
-      for (int i = 0; i < 6; i++) fl[i] = s[16 + i];
-      if (s[0] == BLOSC2_VERSION_FORMAT_ALPHA) fl[5] = 0;
-      if (needs_host_callbacks(fl, (s[2] >> 5) == BLOSC_UDCODEC_FORMAT ? 255 : 0))
-        return decompress_hybrid(ctx, src, srcsize, dest, destsize, mask);
+  const uint8_t* s = static_cast<const uint8_t*>(src);
+  // user filters / codecs in an extended header (not memcpyed, not special) -> host callbacks;
+  // unknown ids <= BLOSC2_DEFINED_FILTERS_STOP stay on the device, which fails them as
+  // pipeline_backward does (blosc/blosc2.c:1534-1539)
+  if (H.ext && !H.memcpyed && H.special == 0 && nbytes > 0) {
+    uint8_t fl[6];
+    for (int i = 0; i < 6; i++) {
+      fl[i] = s[16 + i];
+      if (fl[i] <= BLOSC2_DEFINED_FILTERS_STOP) fl[i] = 0;
     }
+    if (s[0] == BLOSC2_VERSION_FORMAT_ALPHA) fl[5] = 0;
+    if (needs_host_callbacks(fl, (s[2] >> 5) == BLOSC_UDCODEC_FORMAT ? 255 : 0))
+      return decompress_hybrid(ctx, src, srcsize, dest, destsize, mask);
   }
+  // The device reads what the reference may read: srcsize bytes (the blosc1 entry points pass
+  // INT32_MAX for "unknown": the chunk's own cbytes then).
+  const int32_t ss = srcsize == INT32_MAX ? std::max<int32_t>(H.cbytes, BLOSC_EXTENDED_HEADER_LENGTH) : srcsize;
   Device& d = ctx->dev;
   if (!d.init()) return BLOSC2_ERROR_FAILURE;
   const size_t mask_bytes = mask ? mask->size() : 0;
-  if (!d.in.ensure((size_t)cbytes) || !d.out.ensure((size_t)(nbytes > 0 ? nbytes : 1)) ||
+  if (!d.in.ensure((size_t)ss) || !d.out.ensure((size_t)(nbytes > 0 ? nbytes : 1)) ||
       !d.small.ensure(64 + mask_bytes))
     return BLOSC2_ERROR_MEMORY_ALLOC;
   struct Ptrs { const uint8_t* s; uint8_t* o; int32_t ss, ds, status, pad; } h;
   h.s = d.in.u8();
   h.o = d.out.u8();
-  h.ss = cbytes;
+  h.ss = ss;
   h.ds = destsize;
   uint8_t* sm = d.small.u8();
-  if (hipMemcpyAsync(d.in.p, src, (size_t)cbytes, hipMemcpyHostToDevice, d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+  if (hipMemcpyAsync(d.in.p, src, (size_t)ss, hipMemcpyHostToDevice, d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
   if (hipMemcpyAsync(sm, &h, sizeof h, hipMemcpyHostToDevice, d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
   const uint8_t* d_mask = nullptr;
   if (mask) {
@@ -306,9 +362,11 @@ int decompress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void*
     d_mask = sm + 64;
   }
   Ptrs* dp = reinterpret_cast<Ptrs*>(sm);
+  // exact tables (src_bound -1): a malformed chunk may claim more streams than its bytes hold and
+  // still be decoded by the reference (bstarts sharing stream data); one extra sync, host call
   rc = b2h::decompress_batch(reinterpret_cast<const uint8_t* const*>(&dp->s), &dp->ss,
-                             reinterpret_cast<uint8_t* const*>(&dp->o), &dp->ds, 1, nbytes, &dp->status, d_mask,
-                             d.stream, d.ws, cbytes);
+                             reinterpret_cast<uint8_t* const*>(&dp->o), &dp->ds, 1, std::max(nbytes, 0), &dp->status,
+                             d_mask, d.stream, d.ws, -1, mode);
   if (rc < 0) {
     TRACE_ERROR("device decompression failed: %s", b2h::last_error());
     return rc;
@@ -317,6 +375,7 @@ int decompress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void*
   if (hipMemcpyAsync(&status, &dp->status, 4, hipMemcpyDeviceToHost, d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
   if (hipStreamSynchronize(d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
   if (status <= 0) return status;
+  if (H.special == BLOSC2_SPECIAL_UNINIT) return status;   // nothing written (blosc/blosc2.c:1904-1906)
   if (!mask) {
     if (hipMemcpy(dest, d.out.p, (size_t)status, hipMemcpyDeviceToHost) != hipSuccess) return BLOSC2_ERROR_FAILURE;
   } else {
@@ -920,114 +979,141 @@ int blosc2_decompress_ctx(blosc2_context* context, const void* src, int32_t srcs
   return decompress_host(context, src, srcsize, dest, destsize, has_mask ? &mask : nullptr);
 }
 
+// A memcpyed or special chunk's items [off, off + len) as a stand-alone chunk of the same kind
+// (header with nbytes = blocksize = len, no dictionary / lazy / VL bits; the raw bytes, or the
+// repeated value), decoded by the device's memcpyed / special path.
+static void carve_items(const uint8_t* s, const ChunkHdr& H, int64_t off, int32_t len, std::vector<uint8_t>& one) {
+  auto put32 = [&](size_t at, int32_t v) { memcpy(one.data() + at, &v, 4); };
+  if (H.special) {
+    // the special kind decides, whatever the memcpyed bit and cbytes say (blosc_d 1865-1909)
+    one.assign(s, s + (H.special == BLOSC2_SPECIAL_VALUE ? H.cbytes : BLOSC_EXTENDED_HEADER_LENGTH));
+    one[2] &= (uint8_t)~BLOSC_MEMCPYED;
+    put32(12, (int32_t)one.size());
+  } else {
+    one.assign(s, s + H.overhead);
+    one.insert(one.end(), s + H.overhead + off, s + H.overhead + off + len);
+    put32(12, (int32_t)one.size());
+  }
+  put32(4, len);
+  put32(8, len);
+  if (H.ext) {
+    one[BLOSC2_CHUNK_BLOSC2_FLAGS2] = 0;
+    one[BLOSC2_CHUNK_BLOSC2_FLAGS] = (uint8_t)(H.special << 4);
+  }
+}
+
 // blosc2_decompress_block_ctx (blosc/blosc2.c:4580-4687; declared in blosc-private.h:29 and used
 // by the sparse reader, schunk.c:1858): block `nblock` of a chunk into dest, returning its size.
-// The block is carved out as a one-block chunk (header with nbytes = blocksize = the block's size,
-// one bstart, the block's streams) and decoded on the device.  Being block 0 of that chunk, a
-// DELTA pipeline decodes it against itself -- exactly the reference's serial result, where
-// blosc_d runs with dest_offset 0 (delta_decoder's offset == 0 branch, delta.c:96-100).  A
-// leftover last block is never split (blosc_d), so its carved header sets DONT_SPLIT.
+// Checks in the reference's order; then the chunk is decoded on the device with every other block
+// masked and the block un-deltaed against itself, as blosc_d with dest_offset 0 leaves it
+// (delta_decoder's offset == 0 branch, delta.c:96-100).  Memcpyed / special blocks are carved out
+// as stand-alone chunks of the same kind (blosc_d's memcpyed path, 1865-1935).
 int blosc2_decompress_block_ctx(blosc2_context* context, const void* src, int32_t srcsize, int32_t nblock, void* dest,
                                 int32_t destsize) {
   if (!context || !src) return BLOSC2_ERROR_NULL_POINTER;
-  int32_t nbytes, cbytes, bs;
-  int rc = peek_header(src, srcsize, &nbytes, &cbytes, &bs);
+  ChunkHdr H;
+  int rc = read_header(src, srcsize, &H);
   if (rc < 0) return rc;
-  const uint8_t* s = static_cast<const uint8_t*>(src);
-  const bool ext = (s[2] & BLOSC_DOSHUFFLE) && (s[2] & BLOSC_DOBITSHUFFLE);
-  const int32_t ovh = ext ? BLOSC_EXTENDED_HEADER_LENGTH : BLOSC_MIN_HEADER_LENGTH;
-  if (srcsize < ovh || cbytes > srcsize) return BLOSC2_ERROR_READ_BUFFER;
-  if (ext && (s[BLOSC2_CHUNK_BLOSC2_FLAGS2] & BLOSC2_VL_BLOCKS)) {
+  if (H.vl) {
     TRACE_ERROR("block decompression is not supported for VL-block chunks.");
     return BLOSC2_ERROR_INVALID_PARAM;
   }
-  const int special = ext ? (s[BLOSC2_CHUNK_BLOSC2_FLAGS] >> 4) & BLOSC2_SPECIAL_MASK : 0;
-  if (special > BLOSC2_SPECIAL_LASTID) {
-    TRACE_ERROR("Unknown special values ID (%d) ", special);
+  if ((rc = init_from_header(&H, srcsize)) < 0) return rc;
+  if (H.special > BLOSC2_SPECIAL_LASTID) {
+    TRACE_ERROR("Unknown special values ID (%d) ", H.special);
     return BLOSC2_ERROR_DATA;
   }
-  // blosc2_calculate_blocks: nblocks = ceil(nbytes / blocksize), leftover = nbytes % blocksize
-  const int32_t nblocks = nbytes / bs + (nbytes % bs ? 1 : 0);
-  if (nblock < 0 || nblock >= nblocks) {
+  if (nblock < 0 || nblock >= H.nblocks) {
     TRACE_ERROR("`nblock` out of bounds.");
     return BLOSC2_ERROR_INVALID_PARAM;
   }
-  const bool memcpyed = (s[2] & BLOSC_MEMCPYED) || special;
-  if (!memcpyed && (int64_t)ovh + 4 * (int64_t)nblocks > srcsize) {
+  if (!H.special && !H.memcpyed && (int64_t)H.overhead + 4 * (int64_t)H.nblocks > srcsize) {
     TRACE_ERROR("`bstarts` out of bounds.");
     return BLOSC2_ERROR_READ_BUFFER;
   }
-  const bool leftover = nblock == nblocks - 1 && nbytes % bs > 0;
-  const int32_t bsize = leftover ? nbytes % bs : bs;
+  const bool leftover = nblock == H.nblocks - 1 && H.leftover > 0;
+  const int32_t bsize = leftover ? H.leftover : H.blocksize;
   if (destsize < bsize) {
     TRACE_ERROR("Destination is too small for block.");
     return BLOSC2_ERROR_WRITE_BUFFER;
   }
-  std::vector<uint8_t> one;
-  auto put32 = [&](size_t at, int32_t v) { memcpy(one.data() + at, &v, 4); };
-  if (special) {                      // header (+ the repeated value) only
-    one.assign(s, s + cbytes);
-  } else if (s[2] & BLOSC_MEMCPYED) {   // the block's raw bytes
-    const int64_t at = (int64_t)ovh + (int64_t)nblock * bs;
-    if (at + bsize > cbytes) return BLOSC2_ERROR_READ_BUFFER;
-    one.assign(s, s + ovh);
-    one.insert(one.end(), s + at, s + at + bsize);
-  } else {                            // one bstart + the block's streams
-    const int32_t b0 = rd32(s + ovh + 4 * nblock);
-    if (b0 < ovh + 4 * nblocks || b0 >= cbytes) return BLOSC2_ERROR_READ_BUFFER;
-    int32_t b1 = cbytes;              // the next stored block (threaded writers store blocks out of order)
-    for (int32_t k = 0; k < nblocks; k++) {
-      const int32_t o = rd32(s + ovh + 4 * k);
-      if (o > b0 && o < b1) b1 = o;
-    }
-    one.assign(s, s + ovh);
-    one.resize((size_t)ovh + 4);
-    put32((size_t)ovh, ovh + 4);
-    one.insert(one.end(), s + b0, s + b1);
-    if (leftover) one[2] |= 0x10;   // dont_split, bit 4 of the flags (blosc/blosc2.c:1719)
-  }
-  put32(4, bsize);
-  put32(8, bsize);
-  if (!special) put32(12, (int32_t)one.size());
+  if (H.lazy && !H.special) return BLOSC2_ERROR_INVALID_PARAM;   // lazy chunks need their frame
+  const uint8_t* s = static_cast<const uint8_t*>(src);
   std::lock_guard<std::mutex> g(context->mu);
-  rc = decompress_host(context, one.data(), (int32_t)one.size(), dest, destsize, nullptr);
+  if (H.memcpyed || H.special) {
+    if (!H.special) {
+      if (H.nbytes + H.overhead != H.cbytes) return BLOSC2_ERROR_WRITE_BUFFER;
+      if (H.cbytes < H.overhead + (int64_t)nblock * H.blocksize + bsize) return BLOSC2_ERROR_READ_BUFFER;
+    }
+    const int32_t its = H.special == BLOSC2_SPECIAL_VALUE ? H.cbytes - H.overhead : H.typesize;
+    if ((H.special == BLOSC2_SPECIAL_VALUE || H.special == BLOSC2_SPECIAL_NAN) && bsize % its) return BLOSC2_ERROR_DATA;
+    if (H.special == BLOSC2_SPECIAL_NAN && its != 4 && its != 8) return BLOSC2_ERROR_DATA;
+    if (H.special == BLOSC2_SPECIAL_UNINIT) return bsize;
+    std::vector<uint8_t> one;
+    carve_items(s, H, (int64_t)nblock * H.blocksize, bsize, one);
+    rc = decompress_host(context, one.data(), (int32_t)one.size(), dest, destsize, nullptr);
+    return rc < 0 ? rc : bsize;
+  }
+  std::vector<uint8_t> mask((size_t)H.nblocks, 1);
+  mask[nblock] = 0;
+  std::vector<uint8_t> full((size_t)H.nbytes);
+  rc = decompress_host(context, src, srcsize, full.data(), H.nbytes, &mask, b2h::kDecDeltaSelf | b2h::kDecNoDict);
   if (rc < 0) return rc;
+  memcpy(dest, full.data() + (int64_t)nblock * H.blocksize, (size_t)bsize);
   return bsize;
 }
 
-// blosc/blosc2.c:4265-4474 / 4541-4550: decode only the blocks overlapping [start, start+nitems)
+// blosc/blosc2.c:4265-4474 / 4541-4550: the reference's checks in order, then the blocks
+// overlapping [start, start + nitems) decoded on the device (the rest masked), each un-deltaed
+// against itself as _blosc_getitem's blosc_d(dest_offset 0) leaves it; memcpyed / special chunks
+// through a carved stand-alone chunk (the reference's short-circuit, 4321-4383).
 int blosc2_getitem_ctx(blosc2_context* context, const void* src, int32_t srcsize, int start, int nitems, void* dest,
                        int32_t destsize) {
   if (!context) return BLOSC2_ERROR_NULL_POINTER;
-  int32_t nbytes, cbytes, bs;
-  int rc = peek_header(src, srcsize, &nbytes, &cbytes, &bs);
+  ChunkHdr H;
+  int rc = read_header(src, srcsize, &H);
   if (rc < 0) return rc;
-  const uint8_t* s = static_cast<const uint8_t*>(src);
-  const int64_t ts = s[3];
-  if ((s[2] & BLOSC_DOSHUFFLE) && (s[2] & BLOSC_DOBITSHUFFLE) && srcsize >= 32 && (s[30] & BLOSC2_VL_BLOCKS)) {
+  if (H.vl) {
     TRACE_ERROR("getitem is not supported for VL-block chunks.");
     return BLOSC2_ERROR_INVALID_PARAM;
   }
+  if ((rc = init_from_header(&H, srcsize)) < 0) return rc;
   if (nitems == 0) return 0;
   if (nitems < 0) return BLOSC2_ERROR_INVALID_PARAM;
+  const int64_t ts = H.typesize;
   const int64_t nib = (int64_t)nitems * ts;
   if (nib > INT32_MAX || nib > destsize) return BLOSC2_ERROR_WRITE_BUFFER;
   const int64_t sb = (int64_t)start * ts;
-  if (start < 0 || sb > nbytes) return BLOSC2_ERROR_INVALID_PARAM;
+  if (start < 0 || sb > H.nbytes) return BLOSC2_ERROR_INVALID_PARAM;
   const int64_t stop = (int64_t)start + nitems;
-  if (stop > INT32_MAX || stop * ts > nbytes) return BLOSC2_ERROR_INVALID_PARAM;
-  if (nbytes > 0 && bs > nbytes) bs = nbytes;
-  const int32_t nblocks = nbytes > 0 ? nbytes / bs + (nbytes % bs ? 1 : 0) : 0;
-  std::vector<uint8_t> mask((size_t)nblocks, 1);
-  const bool delta = (s[2] & BLOSC_DODELTA) != 0;
-  for (int32_t b = 0; b < nblocks; b++) {
-    const int64_t lo = (int64_t)b * bs, hi = lo + bs;
+  if (stop > INT32_MAX || stop * ts > H.nbytes) return BLOSC2_ERROR_INVALID_PARAM;
+  if (!H.special && !H.memcpyed && (int64_t)H.overhead + 4 * (int64_t)H.nblocks > srcsize) {
+    TRACE_ERROR("`bstarts` out of bounds.");
+    return BLOSC2_ERROR_READ_BUFFER;
+  }
+  const uint8_t* s = static_cast<const uint8_t*>(src);
+  const bool lazy = H.lazy && !H.special;
+  std::lock_guard<std::mutex> g(context->mu);
+  if ((H.memcpyed || H.special) && !lazy) {
+    if (H.special > BLOSC2_SPECIAL_LASTID) return BLOSC2_ERROR_SCHUNK_SPECIAL;
+    const int32_t its = H.special == BLOSC2_SPECIAL_VALUE ? H.cbytes - H.overhead : H.typesize;
+    if ((H.special == BLOSC2_SPECIAL_VALUE || H.special == BLOSC2_SPECIAL_NAN) && nib % its) return BLOSC2_ERROR_DATA;
+    if (H.special == BLOSC2_SPECIAL_NAN && its != 4 && its != 8) return BLOSC2_ERROR_DATA;
+    if (!H.special && H.overhead + sb + nib > srcsize) return BLOSC2_ERROR_READ_BUFFER;
+    if (H.special == BLOSC2_SPECIAL_UNINIT) return (int)nib;
+    std::vector<uint8_t> one;
+    carve_items(s, H, sb, (int32_t)nib, one);
+    rc = decompress_host(context, one.data(), (int32_t)one.size(), dest, destsize, nullptr);
+    return rc < 0 ? rc : (int)nib;
+  }
+  if (lazy) return BLOSC2_ERROR_INVALID_PARAM;   // lazy chunks need their frame (blosc_d 1757-1766)
+  std::vector<uint8_t> mask((size_t)H.nblocks, 1);
+  for (int32_t b = 0; b < H.nblocks; b++) {
+    const int64_t lo = (int64_t)b * H.blocksize, hi = lo + H.blocksize;
     if (hi > sb && lo < stop * ts) mask[b] = 0;
   }
-  if (delta && nblocks) mask[0] = 0;   // later blocks XOR against decoded block 0
-  std::vector<uint8_t> full((size_t)std::max(nbytes, 1));
-  std::lock_guard<std::mutex> g(context->mu);
-  rc = decompress_host(context, src, srcsize, full.data(), nbytes, &mask);
+  std::vector<uint8_t> full((size_t)H.nbytes);
+  rc = decompress_host(context, src, srcsize, full.data(), H.nbytes, &mask, b2h::kDecDeltaSelf | b2h::kDecNoDict);
   if (rc < 0) return rc;
   memcpy(dest, full.data() + sb, (size_t)nib);
   return (int)nib;
