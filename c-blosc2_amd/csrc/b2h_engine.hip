@@ -1485,13 +1485,15 @@ __global__ void k_dplan_chunks(const uint8_t* const* __restrict__ srcs, const in
   if (vl && lazy && !d.special && !memcpyed && (int64_t)ss < bstarts_end + 12 + 4 * (int64_t)nblocks)
     return fail(E_READ);
   if ((bflags & kUseDict) && !lazy && !(mode & 4)) {
-    // the dictionary section after the bstarts: [int32 size | bytes] (2790-2825); BloscLZ and
-    // the LZ4 streams of these chunks reference nothing in it
+    // the dictionary section after the bstarts: [int32 size | bytes] (2790-2825); LZ4 streams
+    // may match into it (LZ4_decompress_safe_usingDict, 504-508), BloscLZ ignores it
     const int64_t rem = ss - bstarts_end;
     if (rem < 4) return fail(E_READ);
     const int32_t dsz = rd32(s + bstarts_end);
     if (dsz <= 0 || dsz > 32 * 1024) return fail(E_DICT);
     if (rem - 4 < dsz) return fail(E_READ);
+    d.dict_off = (int32_t)bstarts_end + 4;
+    d.dict_size = dsz;
   }
   if (vl && !d.special && !memcpyed) return fail(E_VERSION);   // VL-block chunks: not on the device path
   d.dont_split = (d.flags >> 4) & 1;
@@ -1737,7 +1739,7 @@ __device__ __forceinline__ void decode_stream(const uint8_t* const* __restrict__
     wave_copy(out, in, nb);
     *kind_out = 2;
   } else if ((d.flags >> 5) == 1) {   // LZ4 (blosc/blosc2.c:2062-2067)
-    const int32_t got = wave_lz4_decode_ring<RLOG>(in, st.csize, out, nb, ring);
+    const int32_t got = wave_lz4_decode_ring<RLOG>(in, st.csize, out, nb, ring, (gin_t)(srcs[c] + d.dict_off), d.dict_size);
     if (got != nb && lane == 0) rec_err(ch, c, blk, step, E_DATA);
     *kind_out = 4;
   } else if ((d.flags >> 5) != 0) {

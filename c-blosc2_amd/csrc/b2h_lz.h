@@ -844,8 +844,11 @@ __host__ __device__ constexpr int32_t ring_piece(int rlog) { return (1 << rlog) 
 // made the token loop irreducible (the backend then wraps every token in a guard-variable
 // state machine, ~4x the instructions).  Called for copies longer than 64 bytes, sources older
 // than the ring, and ring flushes.  Returns the new flush frontier F.
+// A source before the stream start (src < 0, LZ4 with a dictionary) reads the dictionary's tail:
+// position y < 0 is dict[dsz + y] (LZ4_decompress_safe_usingDict's external dictionary).
 template <int RLOG>
-__device__ __noinline__ int32_t copy_general(B2H_LDS uint8_t* ring, gout_t out, int32_t op, int32_t src, int32_t len, int32_t dist, int32_t F) {
+__device__ __noinline__ int32_t copy_general(B2H_LDS uint8_t* ring, gout_t out, int32_t op, int32_t src, int32_t len, int32_t dist, int32_t F,
+                                             gin_t dict = nullptr, int32_t dsz = 0) {
   constexpr int32_t R = 1 << RLOG, RM = R - 1, PIECE = ring_piece(RLOG), STEP = 1024;
   const int lane = lane_id();
   const bool overlap = dist < len;
@@ -857,7 +860,7 @@ __device__ __noinline__ int32_t copy_general(B2H_LDS uint8_t* ring, gout_t out, 
     if (src < F) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     for (int32_t i = done + lane; i < done + n; i += 64) {
       const int32_t y = overlap ? src + r : src + i;
-      const uint8_t b = y >= F ? ring[y & RM] : out[y];
+      const uint8_t b = y >= F ? ring[y & RM] : (y >= 0 ? out[y] : dict[dsz + y]);
       ring[(op + i) & RM] = b;
       if (overlap) { r += step; if (r >= dist) r -= dist; }
     }
@@ -1002,9 +1005,11 @@ __device__ __noinline__ int32_t ring_put(B2H_LDS uint8_t* ring, gout_t out, int3
 // literals, LE16 offset, match; the last sequence is literals only.  Same LDS-ring machinery as
 // the BloscLZ decoder: token bytes by readlane from the register window, literal runs and matches
 // copied by 64 lanes through the ring.  Returns decoded bytes, or -1.
+// `dict` / `dsz`: the chunk's dictionary (BLOSC2_USEDICT, blosc/blosc2.c:504-508), matches may
+// reach dsz bytes before the output start.
 template <int RLOG>
 __device__ __forceinline__ int32_t wave_lz4_decode_ring(gin_t in, int32_t length, gout_t out, int32_t maxout,
-                                                        B2H_LDS uint8_t* ring) {
+                                                        B2H_LDS uint8_t* ring, gin_t dict = nullptr, int32_t dsz = 0) {
   constexpr int32_t R = 1 << RLOG, RM = R - 1;
   constexpr int32_t kMfLimit = 12, kLastLit = 5;
   const int lane = lane_id();
@@ -1041,7 +1046,7 @@ __device__ __forceinline__ int32_t wave_lz4_decode_ring(gin_t in, int32_t length
     if (last) break;
     const int32_t off = (int32_t)(inwin_byte(W, in, length, ip) | (inwin_byte(W, in, length, ip + 1) << 8));
     ip += 2;
-    if (off > op) return -1;
+    if (off > op + dsz) return -1;
     int32_t ml = (int32_t)(token & 15u);
     if (ml == 15) {
       uint32_t s;
@@ -1062,7 +1067,7 @@ __device__ __forceinline__ int32_t wave_lz4_decode_ring(gin_t in, int32_t length
         const int32_t yl = off < ml ? lane % off : lane;
         if (lane < ml) ring[(op + lane) & RM] = ring[(src + yl) & RM];
       } else {
-        F = copy_general<RLOG>(ring, out, op, src, ml, off, F);
+        F = copy_general<RLOG>(ring, out, op, src, ml, off, F, dict, dsz);
       }
     }
     op += ml;

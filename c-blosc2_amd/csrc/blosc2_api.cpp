@@ -206,6 +206,9 @@ int check_supported(const blosc2_context* c) {
 }
 
 bool needs_host_callbacks(const uint8_t* filters, int compcode);
+bool device_filter(uint8_t f);
+bool lookup_filter(uint8_t id, blosc2_filter* out);
+bool lookup_codec(int compcode, blosc2_codec* out);
 int compress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void* dest, int32_t destsize,
                     int32_t blocksize_in, bool sticky, bool extended);
 int decompress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void* dest, int32_t destsize,
@@ -335,8 +338,19 @@ int decompress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void*
       if (fl[i] <= BLOSC2_DEFINED_FILTERS_STOP) fl[i] = 0;
     }
     if (s[0] == BLOSC2_VERSION_FORMAT_ALPHA) fl[5] = 0;
-    if (needs_host_callbacks(fl, (s[2] >> 5) == BLOSC_UDCODEC_FORMAT ? 255 : 0))
-      return decompress_hybrid(ctx, src, srcsize, dest, destsize, mask);
+    const bool udcodec = (s[2] >> 5) == BLOSC_UDCODEC_FORMAT;
+    if (needs_host_callbacks(fl, udcodec ? 255 : 0)) {
+      // A plugin that is neither registered nor loadable fails where the reference's block walk
+      // meets it (the codec at its first stream, a filter after the block's streams): the device
+      // planner keys those failures in order, so such chunks stay on the device path.
+      bool found = true;
+      blosc2_filter fi;
+      blosc2_codec co;
+      for (int i = 0; i < 6; i++)
+        if (!device_filter(fl[i]) && !lookup_filter(fl[i], &fi)) found = false;
+      if (udcodec && !lookup_codec(s[22], &co)) found = false;
+      if (found) return decompress_hybrid(ctx, src, srcsize, dest, destsize, mask);
+    }
   }
   // The device reads what the reference may read: srcsize bytes (the blosc1 entry points pass
   // INT32_MAX for "unknown": the chunk's own cbytes then).

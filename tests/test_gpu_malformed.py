@@ -62,6 +62,10 @@ BASES = [
     ("zeros", np.zeros(50_000, np.uint8), dict(typesize=4, blocksize=16384, filters=(0, 0, 0, 0, 0, 1))),
     ("delta_shuffle", int64_ramp(3, 12_000).view(np.uint8),
      dict(typesize=8, blocksize=16384, filters=(0, 0, 0, 0, 2, 1))),
+    # LZ4 with a dictionary (the reference's use_dict: raw samples of the filtered blocks,
+    # blosc/blosc2.c:3195-3235): streams match into the dictionary section
+    ("lz4_dict", gen_f32(9, 60_000).view(np.uint8),
+     dict(typesize=4, blocksize=16384, filters=(0, 0, 0, 0, 0, 1), compcode=1, use_dict=1)),
 ]
 
 
@@ -164,6 +168,10 @@ def test_malformed_chunks_match_reference(libs, base):
     B, L, R = libs
     name, raw, kw = base
     good = _ref_chunk(R, raw, **kw)
+    if kw.get("use_dict"):
+        assert good[31] & 1, "the reference wrote no dictionary"
+    rc, got = _decomp(L, B.dparams, good, good.nbytes, raw.nbytes)
+    assert rc == raw.nbytes and np.array_equal(got[:rc], raw), name
     bad = []
     for label, chunk, srcsize, ddest in _variants(good):
         destsize = raw.nbytes + ddest
