@@ -82,7 +82,7 @@ struct Scratch {
 struct Workspace {
   Scratch t1, t2, work, sbuf, res, place, mode, qctr, gtab, porder;    // compress
   bool porder_init = false;
-  Scratch dchunks, dstreams, dblocks, dtotals, stage, stage2, ptrs, dqctr, ddbg, dorder;  // decompress
+  Scratch dchunks, dstreams, dblocks, dtotals, stage, stage2, ptrs, dqctr, ddbg, dorder, dbcnt;  // decompress
   std::mutex mu;
   hipEvent_t done = nullptr;       // recorded after the last kernel of the latest call
   hipStream_t last = nullptr;      // the stream that call ran on
@@ -101,7 +101,7 @@ struct Workspace {
   void free_all() {
     if (used && done) (void)hipEventSynchronize(done);
     for (Scratch* s : {&t1, &t2, &work, &sbuf, &res, &place, &mode, &qctr, &gtab, &porder, &dchunks, &dstreams,
-                       &dblocks, &dtotals, &stage, &stage2, &ptrs, &dqctr, &ddbg, &dorder})
+                       &dblocks, &dtotals, &stage, &stage2, &ptrs, &dqctr, &ddbg, &dorder, &dbcnt})
       s->release();
     if (done) (void)hipEventDestroy(done);
     done = nullptr;
@@ -1537,6 +1537,14 @@ __global__ void k_dplan_chunks(const uint8_t* const* __restrict__ srcs, const in
     k++;
   }
   d.nfilters_bwd = (uint8_t)K;
+  // a lone 4-byte SHUFFLE (the T pipeline) is undone inside the decode launch by the wave that
+  // completes each block (k_decode finish_block); k_dfilter skips these chunks
+  if (K == 1 && d.ferr == 0) {
+    int i = 5;
+    while (bwd_noop(d.filters[i])) i--;
+    const int32_t ts = d.filters_meta[i] ? d.filters_meta[i] : d.typesize;
+    d.fuse_unshuffle = d.filters[i] == kShuffle && ts == 4 && (mode & 8) == 0;
+  }
   ch[c] = d;
 }
 
@@ -1569,7 +1577,7 @@ __global__ __launch_bounds__(1024) void k_dscan(DChunk* __restrict__ ch, int32_t
     dl |= ch[i].has_delta ? 0x100 : 0;
     dl |= (ch[i].nstreams == 0 && ch[i].nbytes != 0) ? 0x200 : 0;   // k_dspecial's chunks
     for (int f = 0; f < 6; f++)
-      if (!bwd_noop(ch[i].filters[f])) dl |= 1 << f;
+      if (!bwd_noop(ch[i].filters[f]) && !ch[i].fuse_unshuffle) dl |= 1 << f;
     mf = max(mf, (int32_t)ch[i].nfilters_bwd);
   }
   sb[threadIdx.x] = a; sbk[threadIdx.x] = bk; sst[threadIdx.x] = st; sdl[threadIdx.x] = dl; smf[threadIdx.x] = mf;
@@ -1626,12 +1634,13 @@ __device__ int32_t find_chunk(const DChunk* ch, int32_t n, int32_t idx) {
   return lo;
 }
 
-// Pull order of the decoder: LZ / LZ4 streams (thousands of tokens each; on T one per block, ~90 %
-// of the decode wave-time) from the front, raw copies and runs (a 64 KiB memcpy / memset) from the
-// back, so the long streams start first and the short ones fill the end of the launch.
 __device__ __forceinline__ void rec_err(DChunk* ch, int32_t c, int32_t block, int32_t step, int32_t code) {
   atomicMin(reinterpret_cast<unsigned long long*>(&ch[c].errkey), (unsigned long long)err_key(block, step, code));
 }
+
+// Pull order of the decoder: LZ / LZ4 streams (thousands of tokens each; on T one per block, ~90 %
+// of the decode wave-time) from the front, raw copies and runs (a 64 KiB memcpy / memset) from the
+// back, so the long streams start first and the short ones fill the end of the launch.
 
 // One block of the walk (blosc_d, blosc/blosc2.c:1734-2016): a masked block is skipped before any
 // check; then the bstart (1937-1940), the stream count (1982-1986) and each stream's size words
@@ -1640,12 +1649,13 @@ __device__ void dplan_block(const uint8_t* const* __restrict__ srcs, const int32
                             DChunk* __restrict__ ch, int32_t n, DBlock* __restrict__ blocks,
                             DStream* __restrict__ streams, int32_t idx, int32_t* __restrict__ order,
                             int32_t* __restrict__ octr, int32_t nstreams, const uint8_t* __restrict__ maskout,
-                            int32_t mask_stride) {
+                            int32_t mask_stride, int32_t* __restrict__ bcnt) {
   const int32_t c = find_chunk(ch, n, idx);
   const DChunk d = ch[c];
   const int32_t b = idx - d.block_base;
   blocks[idx].chunk = c;
   blocks[idx].block = b;
+  if (bcnt) bcnt[idx] = 0;
   const uint8_t* s = srcs[c];
   const int32_t ss = srcsize[c];
   const bool lo = (b == d.nblocks - 1) && d.leftover;
@@ -1684,8 +1694,11 @@ __device__ void dplan_block(const uint8_t* const* __restrict__ srcs, const int32
     }
     if (err) st.neblock = -1;
     streams[sbase + j] = st;
+    // LZ streams first, except in chunks whose blocks are unshuffled by the wave that completes
+    // them: there raw / run streams go first, so a block's LZ stream finishes it while the other
+    // waves are still decoding and the un-filter overlaps them (it would all land in the tail)
     const bool heavy = st.neblock > 0 && st.csize > 0 && st.csize != st.neblock;
-    const int32_t slot = heavy ? atomicAdd(&octr[0], 1) : nstreams - 1 - atomicAdd(&octr[1], 1);
+    const int32_t slot = (heavy != (bool)d.fuse_unshuffle) ? atomicAdd(&octr[0], 1) : nstreams - 1 - atomicAdd(&octr[1], 1);
     order[slot] = sbase + j;
   }
 }
@@ -1694,10 +1707,10 @@ __global__ void k_dplan_blocks(const uint8_t* const* __restrict__ srcs, const in
                                DChunk* __restrict__ ch, int32_t n, DBlock* __restrict__ blocks,
                                DStream* __restrict__ streams, const DTotals* __restrict__ tot,
                                int32_t* __restrict__ order, int32_t* __restrict__ octr,
-                               const uint8_t* __restrict__ maskout, int32_t mask_stride) {
+                               const uint8_t* __restrict__ maskout, int32_t mask_stride, int32_t* __restrict__ bcnt) {
   const int32_t nb = tot->nblocks, ns = tot->nstreams;
   for (int32_t idx = blockIdx.x * blockDim.x + threadIdx.x; idx < nb; idx += gridDim.x * blockDim.x)
-    dplan_block(srcs, srcsize, ch, n, blocks, streams, idx, order, octr, ns, maskout, mask_stride);
+    dplan_block(srcs, srcsize, ch, n, blocks, streams, idx, order, octr, ns, maskout, mask_stride, bcnt);
 }
 
 // Decoder: one wave per stream, persistent (as many single-wave workgroups as the LDS ring
@@ -1709,16 +1722,17 @@ __global__ void k_dplan_blocks(const uint8_t* const* __restrict__ srcs, const in
 // picks it; default 13 (T decode: 15 -> 10.2 ms, 14 -> 6.3 ms, 13 -> 5.6 ms: the token loop is
 // latency-bound, and more resident waves beat keeping older match sources in LDS).
 
+// Returns whether the stream was decoded (false: skipped -- failed chunk, unplanned or masked).
 template <int RLOG>
-__device__ __forceinline__ void decode_stream(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
+__device__ __forceinline__ bool decode_stream(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
                                               DChunk* __restrict__ ch, const DStream& st, uint8_t* __restrict__ stage,
                                               const uint8_t* __restrict__ maskout, int32_t mask_stride,
                                               B2H_LDS uint8_t* ring, int32_t* kind_out) {
   const int lane = lane_id();
   const int32_t c = st.chunk;
   const DChunk d = ch[c];
-  if (d.status < 0 || st.neblock < 0) return;
-  if (maskout && maskout[(int64_t)c * mask_stride + st.dst_off / d.blocksize]) return;
+  if (d.status < 0 || st.neblock < 0) return false;
+  if (maskout && maskout[(int64_t)c * mask_stride + st.dst_off / d.blocksize]) return false;
   gin_t in = (gin_t)(srcs[c] + st.src);
   gout_t out = (gout_t)((d.nfilters_bwd ? stage + d.stage_off : dsts[c]) + st.dst_off);
   const int32_t nb = st.neblock;
@@ -1726,17 +1740,17 @@ __device__ __forceinline__ void decode_stream(const uint8_t* const* __restrict__
   const int32_t blk = st.dst_off / d.blocksize;
   const int32_t step = 1 + (st.dst_off - blk * d.blocksize) / nb;
   if (st.csize == 0) {
-    wave_fill(out, 0, nb);
+    wave_fill<true>(out, 0, nb);
   } else if (st.csize < 0) {
     const uint8_t token = in[0];
     if (!(token & 1) || st.csize < -255) {
       if (lane == 0) rec_err(ch, c, blk, step, E_RUNLEN);
     } else {
-      wave_fill(out, (uint8_t)(-st.csize), nb);
+      wave_fill<true>(out, (uint8_t)(-st.csize), nb);
       *kind_out = 1;
     }
   } else if (st.csize == nb) {
-    wave_copy(out, in, nb);
+    wave_copy<true>(out, in, nb);
     *kind_out = 2;
   } else if ((d.flags >> 5) == 1) {   // LZ4 (blosc/blosc2.c:2062-2067)
     const int32_t got = wave_lz4_decode_ring<RLOG>(in, st.csize, out, nb, ring, (gin_t)(srcs[c] + d.dict_off), d.dict_size);
@@ -1749,15 +1763,99 @@ __device__ __forceinline__ void decode_stream(const uint8_t* const* __restrict__
     if (got != nb && lane == 0) rec_err(ch, c, blk, step, E_DATA);
     *kind_out = 3;
   }
+  return true;
+}
+
+// SHUFFLE-only chunks (DChunk::fuse_unshuffle): the wave that decodes the last of a block's streams
+// unshuffles the block stage -> dst inside this launch, so the un-filter overlaps the latency-bound
+// LZ streams instead of running as its own bandwidth pass (k_dfilter).  Hand-off, after
+// MI355X_MICROARCH.md § inter-workgroup visibility R1: the decoders store their output write-
+// through (sc1) and drain it (vmcnt(0)) before lane 0 adds to the block's counter (agent scope,
+// relaxed); the wave whose add completes the count acquires (agent) before its plain loads.
+// One wave unshuffles a typesize-4 block on its own, so it must keep many bytes in flight: rows
+// of 1024 elements (1 KiB per plane) arrive by 16-byte lane-linear loads, the next row's loads
+// issued before this row is transposed through the idle LDS ring (4 KiB) and leaves by 16-byte
+// stores, each instruction 1 KiB contiguous.  The n % 256 remainder and the bsize % 4 tail
+// take the per-quad and byte paths.
+__device__ __forceinline__ void unshuffle4_wave_lds(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t bsize,
+                                                    B2H_LDS uint8_t* lds) {
+  const int lane = lane_id();
+  const int32_t n = bsize / 4;
+  if (!aligned16(src) || !aligned16(dst)) {
+    for (int32_t i = lane; i < n * 4; i += 64) dst[i] = src[(i & 3) * n + (i >> 2)];
+  } else {
+    const int32_t rows = (n % 4 == 0) ? n / 1024 : 0;   // 1024 elements = 1 KiB per plane
+    if (rows > 0) {
+      u32x4 v[4], v1[4];
+#pragma unroll
+      for (int p = 0; p < 4; p++) v[p] = *reinterpret_cast<const u32x4*>(src + (int64_t)p * n + 16 * lane);
+      if (rows > 1) {
+#pragma unroll
+        for (int p = 0; p < 4; p++) v1[p] = *reinterpret_cast<const u32x4*>(src + (int64_t)p * n + 1024 + 16 * lane);
+      }
+#pragma unroll 1
+      for (int32_t r = 0; r < rows; r++) {
+        // this row into LDS, then the loads two rows ahead in flight while this one is transposed
+#pragma unroll
+        for (int p = 0; p < 4; p++) *reinterpret_cast<B2H_LDS u32x4*>(lds + p * 1024 + 16 * lane) = v[p];
+#pragma unroll
+        for (int p = 0; p < 4; p++) v[p] = v1[p];
+        if (r + 2 < rows) {
+#pragma unroll
+          for (int p = 0; p < 4; p++)
+            v1[p] = *reinterpret_cast<const u32x4*>(src + (int64_t)p * n + (int64_t)(r + 2) * 1024 + 16 * lane);
+        }
+        uint8_t* row = dst + (int64_t)r * 4096;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int32_t q = k * 64 + lane;
+          uint32_t w[4];
+#pragma unroll
+          for (int p = 0; p < 4; p++) w[p] = *reinterpret_cast<const B2H_LDS uint32_t*>(lds + p * 1024 + 4 * q);
+          store_quad<4>(row, q, w);
+        }
+      }
+    }
+    for (int32_t q = rows * 256 + lane; q < n / 4; q += 64) {   // quads after the whole rows
+      uint32_t w[4];
+      load_planes<4>(src, q, n, w);
+      store_quad<4>(dst, q, w);
+    }
+    for (int32_t i = (n / 4) * 16 + lane; i < n * 4; i += 64) dst[i] = src[(i & 3) * n + (i >> 2)];
+  }
+  for (int32_t i = n * 4 + lane; i < bsize; i += 64) dst[i] = src[i];
+}
+
+__device__ __forceinline__ void finish_block(const DChunk* __restrict__ ch, const DStream* __restrict__ streams, int32_t s,
+                                             uint8_t* const* __restrict__ dsts, uint8_t* __restrict__ stage,
+                                             int32_t* __restrict__ bcnt, B2H_LDS uint8_t* ring) {
+  // re-read the plan words here: kept live across the decoder they cost it registers
+  asm volatile("" ::: "memory");
+  const DStream st = streams[s];
+  const DChunk& d = ch[st.chunk];
+  if (!d.fuse_unshuffle) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int32_t blk = st.dst_off / d.blocksize;
+  const bool lo = (blk == d.nblocks - 1) && d.leftover;
+  const int32_t ns = (!d.dont_split && !lo) ? d.typesize : 1;
+  int32_t old = 0;
+  if (lane_id() == 0)
+    old = __hip_atomic_fetch_add(bcnt + d.block_base + blk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __builtin_amdgcn_readfirstlane(old);
+  if (old != ns - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int64_t off = (int64_t)blk * d.blocksize;
+  unshuffle4_wave_lds(stage + d.stage_off + off, dsts[st.chunk] + off, lo ? d.leftover : d.blocksize, ring);
 }
 
 template <int RLOG>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RLOG == 12 ? 8 : 1, 8))) void k_decode(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RLOG == 12 ? 8 : RLOG == 13 ? 5 : 1, 8))) void k_decode(const uint8_t* const* __restrict__ srcs, uint8_t* const* __restrict__ dsts,
                                                DChunk* __restrict__ ch, const DStream* __restrict__ streams,
                                                uint8_t* __restrict__ stage, const DTotals* __restrict__ tot,
                                                const uint8_t* __restrict__ maskout, int32_t mask_stride,
                                                int32_t* __restrict__ next, const int32_t* __restrict__ order,
-                                               int64_t* __restrict__ dbg) {
+                                               int32_t* __restrict__ bcnt, int64_t* __restrict__ dbg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   B2H_LDS uint8_t* ring = (B2H_LDS uint8_t*)smem;
   const int32_t nstreams_total = __builtin_amdgcn_readfirstlane(tot->nstreams);
@@ -1768,7 +1866,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RLOG == 12 ?
     const int32_t s = __builtin_amdgcn_readfirstlane(order[i]);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     int32_t kind = 0;
-    decode_stream<RLOG>(srcs, dsts, ch, streams[s], stage, maskout, mask_stride, ring, &kind);
+    if (decode_stream<RLOG>(srcs, dsts, ch, streams[s], stage, maskout, mask_stride, ring, &kind))
+      finish_block(ch, streams, s, dsts, stage, bcnt, ring);
     if (dbg && lane_id() == 0) {
       dbg[2 * s] = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
       dbg[2 * s + 1] = kind;
@@ -1797,7 +1896,7 @@ __device__ __forceinline__ void dfilter_block(DChunk* __restrict__ ch, const DBl
   if (pass == 1 && bk.block != 0) return;
   if (pass == 2 && bk.block == 0) return;
   const DChunk d = ch[bk.chunk];
-  if (d.status < 0) return;
+  if (d.status < 0 || d.fuse_unshuffle) return;
   const uint8_t f = d.filters[slot];
   if (bwd_noop(f)) return;
   if (maskout && maskout[(int64_t)bk.chunk * mask_stride + bk.block]) return;
@@ -1905,12 +2004,13 @@ static int dec_ring_log() {
 template <int RLOG>
 static void launch_decode(const uint8_t* const* d_src, uint8_t* const* d_dst, DChunk* ch, const DStream* streams,
                           uint8_t* stage, const DTotals* tot, int64_t nstreams_bound, const uint8_t* d_maskout,
-                          int32_t mask_stride, int32_t* next, const int32_t* order, int64_t* dbg, hipStream_t st) {
+                          int32_t mask_stride, int32_t* next, const int32_t* order, int32_t* bcnt, int64_t* dbg,
+                          hipStream_t st) {
   const size_t lds = size_t(1) << RLOG;
   const int slots = resident_slots(reinterpret_cast<const void*>(&k_decode<RLOG>), lds);
   const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(nstreams_bound, slots));
   k_decode<RLOG><<<grid, 64, lds, st>>>(d_src, d_dst, ch, streams, stage, tot, d_maskout, mask_stride, next, order,
-                                        dbg);
+                                        bcnt, dbg);
 }
 
 static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const int32_t* d_srcsize,
@@ -1928,7 +2028,8 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
     cap_blocks = cap_streams = src_bound / 4 + 1;
     cap_stage = std::max<int64_t>(dst_bound, 0);
   }
-  k_dplan_chunks<<<(n + 255) / 256, 256, 0, st>>>(d_src, d_srcsize, d_dstsize, ch, n, mode);
+  static const int no_fuse = getenv("B2H_FUSE_UNSHUFFLE") && atoi(getenv("B2H_FUSE_UNSHUFFLE")) == 0 ? 8 : 0;
+  k_dplan_chunks<<<(n + 255) / 256, 256, 0, st>>>(d_src, d_srcsize, d_dstsize, ch, n, mode | no_fuse);
   k_dscan<<<1, 1024, 0, st>>>(ch, n, tot, cap_blocks, cap_streams, cap_stage);
   HIPCHK(hipGetLastError());
   DTotals h{};
@@ -1952,6 +2053,8 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
     if (h.max_filters >= 2) rc |= ws->stage2.ensure((size_t)h.stage_bytes);
     if (rc) return E_MEMORY;
     if (ws->dorder.ensure(sizeof(int32_t) * (size_t)h.nstreams)) return E_MEMORY;
+    if (ws->dbcnt.ensure(sizeof(int32_t) * (size_t)h.nblocks)) return E_MEMORY;
+    int32_t* bcnt = ws->dbcnt.as<int32_t>();   // per-block finished-stream counts, zeroed by the planner
     DBlock* blocks = ws->dblocks.as<DBlock>();
     DStream* streams = ws->dstreams.as<DStream>();
     int32_t* order = ws->dorder.as<int32_t>();
@@ -1960,7 +2063,7 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
     HIPCHK(hipMemsetAsync(next, 0, 4 * sizeof(int32_t), st));
     const int64_t pb_grid = std::max<int64_t>(1, std::min<int64_t>((h.nblocks + 255) / 256, 4096));
     k_dplan_blocks<<<(uint32_t)pb_grid, 256, 0, st>>>(d_src, d_srcsize, ch, n, blocks, streams, tot, order, next + 1,
-                                                       d_maskout, mask_stride);
+                                                       d_maskout, mask_stride, bcnt);
     ev_decode.start(st);
     {
       int64_t* dbg = nullptr;
@@ -1970,10 +2073,10 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
       }
       const int rlog = dec_ring_log();
       uint8_t* stage = ws->stage.as<uint8_t>();
-      if (rlog == 12) launch_decode<12>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, order, dbg, st);
-      else if (rlog == 13) launch_decode<13>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, order, dbg, st);
-      else if (rlog == 14) launch_decode<14>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, order, dbg, st);
-      else launch_decode<15>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, order, dbg, st);
+      if (rlog == 12) launch_decode<12>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, order, bcnt, dbg, st);
+      else if (rlog == 13) launch_decode<13>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, order, bcnt, dbg, st);
+      else if (rlog == 14) launch_decode<14>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, order, bcnt, dbg, st);
+      else launch_decode<15>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, order, bcnt, dbg, st);
     }
     ev_decode.stop(st);
     ev_unfilter.start(st);

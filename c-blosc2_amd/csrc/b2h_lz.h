@@ -699,33 +699,56 @@ __device__ __forceinline__ StreamResult encode_stream(gin_t in, int32_t n, int c
 }
 
 // ------------------------------------------------------------------ wave fills and copies ----
+// Output stores, plain or write-through (WT: `sc1` buffer stores, MI355X_MICROARCH.md
+// § inter-workgroup visibility, R1 payload).  The decoder writes its output write-through so the
+// wave that completes a block can hand the block's planes to its own unshuffle inside the launch:
+// every stream's bytes are in memory once its wave has drained them (vmcnt(0)), whichever XCD wrote
+// them.  The descriptor is built from the wave-uniform base (no waterfall loops).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(gout_t base) {
+  const uint64_t a = reinterpret_cast<uintptr_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+template <bool WT>
+__device__ __forceinline__ void st16(gout_t base, __amdgpu_buffer_rsrc_t r, int32_t off, u32x4 v) {
+  if constexpr (WT) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+  else *reinterpret_cast<B2H_GLB u32x4*>(base + off) = v;
+}
+template <bool WT>
+__device__ __forceinline__ void st8(gout_t base, __amdgpu_buffer_rsrc_t r, int32_t off, uint8_t v) {
+  if constexpr (WT) __builtin_amdgcn_raw_buffer_store_b8(v, r, off, 0, 16);
+  else base[off] = v;
+}
+
+template <bool WT = false>
 __device__ __forceinline__ void wave_fill(gout_t o, uint8_t v, int32_t n) {
   const int lane = lane_id();
+  const __amdgpu_buffer_rsrc_t r = wt_rsrc(o);
   const int32_t head = (int32_t)((16 - (reinterpret_cast<uintptr_t>(o) & 15)) & 15);
   const int32_t h = min(head, n);
-  if (lane < h) o[lane] = v;
+  if (lane < h) st8<WT>(o, r, lane, v);
   const uint32_t w = v * 0x01010101u;
-  B2H_GLB uint4* o16 = reinterpret_cast<B2H_GLB uint4*>(o + h);
+  const u32x4 w4 = {w, w, w, w};
   const int32_t n16 = (n - h) / 16;
-  for (int32_t i = lane; i < n16; i += 64) {
-    B2H_GLB uint32_t* q = reinterpret_cast<B2H_GLB uint32_t*>(o16 + i);
-    q[0] = w; q[1] = w; q[2] = w; q[3] = w;
-  }
-  for (int32_t i = h + n16 * 16 + lane; i < n; i += 64) o[i] = v;
+  for (int32_t i = lane; i < n16; i += 64) st16<WT>(o, r, h + 16 * i, w4);
+  for (int32_t i = h + n16 * 16 + lane; i < n; i += 64) st8<WT>(o, r, i, v);
 }
 
 // dst any alignment: 16-byte aligned stores of 16 funnel-shifted source bytes per lane, four
 // 1 KiB rows in flight per step (the source is read with aligned dwords: never past the last
 // dword that holds a source byte).
+template <bool WT = false>
 __device__ __forceinline__ void wave_copy(gout_t o, gin_t s, int32_t n) {
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const int lane = lane_id();
+  const __amdgpu_buffer_rsrc_t r = wt_rsrc(o);
   const int32_t head = (int32_t)((16 - (reinterpret_cast<uintptr_t>(o) & 15)) & 15);
   const int32_t h = min(head, n);
-  if (lane < h) o[lane] = s[lane];
+  if (lane < h) st8<WT>(o, r, lane, s[lane]);
   const int32_t n16 = (n - h) / 16;
   gin_t s1 = s + h;
-  B2H_GLB u32x4* o16 = reinterpret_cast<B2H_GLB u32x4*>(o + h);
   const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(s1) & 3);
   const B2H_GLB uint32_t* q0 = align4(s1);
   // the 5th dword of the last 16-byte piece exists only if the source is misaligned
@@ -746,7 +769,7 @@ __device__ __forceinline__ void wave_copy(gout_t o, gin_t s, int32_t n) {
       v.y = funnel(w[u][1], w[u][2], sh);
       v.z = funnel(w[u][2], w[u][3], sh);
       v.w = funnel(w[u][3], w[u][4], sh);
-      o16[i + 64 * u] = v;
+      st16<WT>(o, r, h + 16 * (i + 64 * u), v);
     }
   }
   for (; i < n16; i += 64) {
@@ -757,9 +780,9 @@ __device__ __forceinline__ void wave_copy(gout_t o, gin_t s, int32_t n) {
     v.y = funnel(b, c, sh);
     v.z = funnel(c, d, sh);
     v.w = funnel(d, e, sh);
-    o16[i] = v;
+    st16<WT>(o, r, h + 16 * i, v);
   }
-  for (int32_t j = h + n16 * 16 + lane; j < n; j += 64) o[j] = s[j];
+  for (int32_t j = h + n16 * 16 + lane; j < n; j += 64) st8<WT>(o, r, j, s[j]);
 }
 
 // ------------------------------------------------------------------------------- decoder ----
@@ -817,20 +840,24 @@ __device__ __forceinline__ uint32_t inwin_byte(InWin& W, gin_t in, int32_t lengt
 
 // Move output bytes [from, to) of the LDS ring to global memory (positions are stream offsets;
 // ring slot = position mod R).  16 B per lane when both sides are 16-byte aligned.
+// The decoders' output leaves write-through (see st16): 16 B per lane where out + x is 16-byte
+// aligned (whole 1 KiB rows, then the 16-byte groups of the last row), bytes elsewhere.
 template <int RLOG>
 __device__ __forceinline__ void ring_flush(const B2H_LDS uint8_t* ring, gout_t out, int32_t from, int32_t to) {
   constexpr int32_t RM = (1 << RLOG) - 1;
   const int lane = lane_id();
+  const __amdgpu_buffer_rsrc_t r = wt_rsrc(out);
   int32_t x = from;
   if (((reinterpret_cast<uintptr_t>(out + x) & 15) == 0) && ((x & 15) == 0)) {
     for (; x + 1024 <= to; x += 1024) {
       const int32_t y = x + lane * 16;
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      const u32x4 v = *reinterpret_cast<const B2H_LDS u32x4*>(ring + (y & RM));
-      *reinterpret_cast<B2H_GLB u32x4*>(out + y) = v;
+      st16<true>(out, r, y, *reinterpret_cast<const B2H_LDS u32x4*>(ring + (y & RM)));
     }
+    const int32_t y = x + lane * 16;
+    if (y + 16 <= to) st16<true>(out, r, y, *reinterpret_cast<const B2H_LDS u32x4*>(ring + (y & RM)));
+    x += ((to - x) >> 4) << 4;
   }
-  for (int32_t y = x + lane; y < to; y += 64) out[y] = ring[y & RM];
+  for (int32_t y = x + lane; y < to; y += 64) st8<true>(out, r, y, ring[y & RM]);
 }
 
 

@@ -239,6 +239,42 @@ def test_device_batch_matches_per_chunk(B):
             assert torch.equal(dout, dsrc)
 
 
+def test_fused_unshuffle_layouts(B):
+    """SHUFFLE ts=4 chunks are unshuffled inside the decode launch by the wave completing each
+    block (b2h_engine.hip finish_block): whole 1 KiB rows, remainder quads, blocks whose item count
+    is not a multiple of 4, a bsize % 4 tail, never-split blocks, and destinations at odd offsets
+    (the byte path) -- every chunk equal to its source after a strided batch decompress."""
+    import torch
+    cases = [dict(typesize=4, blocksize=4 * 3085, filters=(0, 0, 0, 0, 0, 1)),            # n % 4 == 1
+             dict(typesize=4, blocksize=4 * 1024 * 5 + 16, filters=(0, 0, 0, 0, 0, 1)),   # rows + quads
+             dict(typesize=4, blocksize=65536, filters=(0, 0, 0, 0, 0, 1), splitmode=2),  # never split
+             dict(typesize=4, blocksize=0, filters=(0, 0, 0, 0, 0, 1), clevel=9)]
+    nbytes = [300_001, 262_144 + 4 * 777, 1 << 20, 4 * 100_003 + 2]
+    for kw in cases:
+        for odd in (0, 3):
+            kwc = dict(kw)
+            clevel = kwc.pop("clevel", 5)
+            raws = [gen_f32(11 + i, (n + 3) // 4).view(np.uint8)[:n].copy() for i, n in enumerate(nbytes)]
+            chunks = [oracle_compress(r, clevel=clevel, **kwc) for r in raws]
+            stride = max(c.nbytes for c in chunks) + 64
+            cap = max(nbytes)
+            dstride = cap + odd
+            host = np.zeros(len(chunks) * stride, np.uint8)
+            for i, c in enumerate(chunks):
+                host[i * stride:i * stride + c.nbytes] = c
+            dsrc = torch.from_numpy(host).cuda()
+            dcb = torch.tensor([c.nbytes for c in chunks], dtype=torch.int32, device="cuda")
+            dout = torch.full((len(chunks) * dstride + 64,), 0xEE, dtype=torch.uint8, device="cuda")
+            dst = torch.zeros(len(chunks), dtype=torch.int32, device="cuda")
+            B.decompress_batch(dsrc.data_ptr(), stride, dcb.data_ptr(), len(chunks), dout.data_ptr(), dstride, cap,
+                               dst.data_ptr())
+            torch.cuda.synchronize()
+            assert list(dst.cpu().numpy()) == nbytes, (kw, odd)
+            out = dout.cpu().numpy()
+            for i, r in enumerate(raws):
+                assert np.array_equal(out[i * dstride:i * dstride + r.nbytes], r), (kw, odd, i)
+
+
 def test_ragged_batch_matches_oracle_without_host_wait(B):
     """b2h_compress_batch_sizes: a super-chunk's chunks with a short last one (ref
     blosc2_schunk_append_buffer, blosc/schunk.c:1459-1477: destsize nbytes + 32 per chunk) ride in
