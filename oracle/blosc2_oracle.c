@@ -21,7 +21,7 @@ enum {
   FLT_NONE = 0, FLT_SHUFFLE = 1, FLT_BITSHUFFLE = 2, FLT_DELTA = 3, FLT_TRUNC = 4,
   FLT_BYTEDELTA = 35, FLT_INT_TRUNC = 36,     /* include/blosc2/filters-registry.h:27-28 */
   SPLIT_ALWAYS = 1, SPLIT_NEVER = 2, SPLIT_AUTO = 3, SPLIT_FWD = 4,
-  SPECIAL_ZERO = 1, SPECIAL_NAN = 2, SPECIAL_VALUE = 3, SPECIAL_UNINIT = 4,
+  SPECIAL_ZERO = 1, SPECIAL_NAN = 2, SPECIAL_VALUE = 3, SPECIAL_UNINIT = 4, USEDICT = 1,
   ERR_DATA = -3, ERR_READ = -5, ERR_WRITE = -6, ERR_PARAM = -12, ERR_CODEC = -7,
   ERR_RUNLEN = -17, ERR_FILTER = -18, ERR_HEADER = -11,
 };
@@ -577,10 +577,160 @@ fail:
   return rc;
 }
 
+/* LZ4_loadDict + LZ4_compress_fast_continue in external-dictionary mode (lz4 1.9.3), the call
+ * sequence of lz4_wrap_compress with a dictionary (blosc/blosc2.c:455-465).  Restated from the
+ * published algorithm and pinned against liblz4 through the reference build
+ * (tests/test_oracle.py::test_lz4_dict_chunks_match_reference).  Positions are 32-bit indices:
+ * loadDict starts the stream at currentOffset = 64 KiB, so the dictionary's last byte is index
+ * 65535 and the input starts at startIndex = 65536; the dictionary's positions 0, 3, 6, ... (up to
+ * its last 8 bytes) are pre-inserted in the byU32 table (hash5, log 12).  Candidates below
+ * startIndex - dictSize are empty slots (dictSmall), farther than 65535 are too far; a match that
+ * starts in the dictionary may run on into the input (LZ4_count up to the dictionary's end, then
+ * from the input's start); offsets are index differences. */
+int or_lz4_compress_dict(int accel, const uint8_t *in, int length, uint8_t *out, int maxout,
+                         const uint8_t *dict, int dsz) {
+  if (accel < 1) accel = 1;
+  if (accel > 65537) accel = 65537;
+  if (length < 0 || length > 0x7E000000) return 0;
+  if (length == 0) { if (maxout <= 0) return 0; out[0] = 0; return 1; }
+  if (dsz < 8) return or_lz4_compress(accel, in, length, out, maxout);   /* loadDict keeps no dictionary */
+  if (dsz > 65536) { dict += dsz - 65536; dsz = 65536; }
+  uint32_t *tab = (uint32_t *)calloc(1u << 12, sizeof(uint32_t));
+  if (!tab) return -1;
+  const uint32_t start = 65536, dict0 = start - (uint32_t)dsz;   /* index of dict[0] */
+  for (int32_t p = 0; p <= dsz - 8; p += 3) tab[lz4_hash_at(dict + p, 0)] = dict0 + (uint32_t)p;
+  const uint32_t prefix_lim = dict0;   /* dictSmall: startIndex - dictSize */
+  const int32_t iend = length, mflimit1 = length - LZ4_MFLIMIT + 1, matchlimit = length - LZ4_LASTLIT;
+  int32_t ip = 0, anchor = 0, op = 0;
+  int rc = 0;
+  /* the match: in the dictionary (mdict, at dict[mpos]) or in the input (at in[mpos]) */
+  int mdict = 0;
+  int32_t mpos = 0;
+  uint32_t offset = 0;
+#define LZ4D_BYTE(isd, q) ((isd) ? dict[(q)] : in[(q)])
+  if (length < LZ4_MFLIMIT + 1) goto last_literals;
+  tab[lz4_hash_at(in, 0)] = start;
+  ip = 1;
+  uint32_t fwdh = lz4_hash_at(in + ip, 0);
+  for (;;) {
+    int32_t fwd = ip, step = 1, nb = accel << LZ4_SKIP;
+    for (;;) {
+      uint32_t h = fwdh;
+      uint32_t cur = start + (uint32_t)fwd;
+      uint32_t mi = tab[h];
+      ip = fwd;
+      fwd += step;
+      step = nb++ >> LZ4_SKIP;
+      if (fwd > mflimit1) goto last_literals;
+      mdict = mi < start;
+      mpos = mdict ? (int32_t)(mi - dict0) : (int32_t)(mi - start);
+      fwdh = lz4_hash_at(in + fwd, 0);
+      tab[h] = cur;
+      if (mi < prefix_lim) continue;                 /* outside the valid area */
+      if (mi + LZ4_DMAX < cur) continue;             /* too far */
+      if (ld32(mdict ? dict + mpos : in + mpos) == ld32(in + ip)) { offset = cur - mi; break; }
+    }
+    /* catch up, not below the match's segment start (lowLimit) */
+    while (ip > anchor && mpos > 0 && in[ip - 1] == LZ4D_BYTE(mdict, mpos - 1)) { ip--; mpos--; }
+    int32_t token;
+    {
+      int32_t lit = ip - anchor;
+      token = op++;
+      if (op + lit + (2 + 1 + LZ4_LASTLIT) + lit / 255 > maxout) goto fail;
+      if (lit >= LZ4_RUN_MASK) {
+        int32_t len = lit - LZ4_RUN_MASK;
+        out[token] = LZ4_RUN_MASK << 4;
+        for (; len >= 255; len -= 255) out[op++] = 255;
+        out[op++] = (uint8_t)len;
+      } else {
+        out[token] = (uint8_t)(lit << 4);
+      }
+      memcpy(out + op, in + anchor, (size_t)lit);
+      op += lit;
+    }
+    for (;;) {   /* _next_match */
+      out[op] = (uint8_t)offset; out[op + 1] = (uint8_t)(offset >> 8);
+      op += 2;
+      int32_t mc;
+      if (mdict) {
+        int32_t limit = ip + (dsz - mpos);
+        if (limit > matchlimit) limit = matchlimit;
+        mc = 0;
+        while (ip + LZ4_MINMATCH + mc < limit && in[ip + LZ4_MINMATCH + mc] == dict[mpos + LZ4_MINMATCH + mc]) mc++;
+        ip += mc + LZ4_MINMATCH;
+        if (ip == limit) {   /* the match runs on from the dictionary's end into the input */
+          int32_t more = 0;
+          while (limit + more < matchlimit && in[limit + more] == in[more]) more++;
+          mc += more;
+          ip += more;
+        }
+      } else {
+        mc = lz4_count(in, ip + LZ4_MINMATCH, mpos + LZ4_MINMATCH, matchlimit);
+        ip += mc + LZ4_MINMATCH;
+      }
+      if (op + (1 + LZ4_LASTLIT) + (mc + 240) / 255 > maxout) goto fail;
+      if (mc >= LZ4_ML_MASK) {
+        out[token] += LZ4_ML_MASK;
+        mc -= LZ4_ML_MASK;
+        for (; mc >= 255; mc -= 255) out[op++] = 255;
+        out[op++] = (uint8_t)mc;
+      } else {
+        out[token] += (uint8_t)mc;
+      }
+      anchor = ip;
+      if (ip >= mflimit1) goto last_literals;
+      tab[lz4_hash_at(in + ip - 2, 0)] = start + (uint32_t)(ip - 2);
+      /* test the next position for an immediate match */
+      uint32_t h = lz4_hash_at(in + ip, 0);
+      uint32_t cur = start + (uint32_t)ip;
+      uint32_t mi = tab[h];
+      mdict = mi < start;
+      mpos = mdict ? (int32_t)(mi - dict0) : (int32_t)(mi - start);
+      tab[h] = cur;
+      if (mi >= prefix_lim && mi + LZ4_DMAX >= cur &&
+          ld32(mdict ? dict + mpos : in + mpos) == ld32(in + ip)) {
+        token = op++;
+        out[token] = 0;
+        offset = cur - mi;
+        continue;
+      }
+      break;
+    }
+    fwdh = lz4_hash_at(in + ++ip, 0);
+  }
+last_literals:
+  {
+    int32_t last = iend - anchor;
+    if (op + last + 1 + (last + 255 - LZ4_RUN_MASK) / 255 > maxout) goto fail;
+    if (last >= LZ4_RUN_MASK) {
+      int32_t acc = last - LZ4_RUN_MASK;
+      out[op++] = LZ4_RUN_MASK << 4;
+      for (; acc >= 255; acc -= 255) out[op++] = 255;
+      out[op++] = (uint8_t)acc;
+    } else {
+      out[op++] = (uint8_t)(last << 4);
+    }
+    memcpy(out + op, in + anchor, (size_t)last);
+    op += last;
+  }
+  rc = op;
+fail:
+#undef LZ4D_BYTE
+  free(tab);
+  return rc;
+}
+
 /* LZ4_decompress_safe: the decoded size, or < 0 for a malformed stream.  Rejections: truncated
  * input, output overflow, a reference before the output start, a match reaching into the last
  * LASTLITERALS bytes of the output, a stream that does not end on a literal run. */
 int or_lz4_decompress(const uint8_t *in, int length, uint8_t *out, int maxout) {
+  return or_lz4_decompress_dict(in, length, out, maxout, NULL, 0);
+}
+
+/* LZ4_decompress_safe_usingDict (lz4_wrap_decompress with a dictionary, blosc/blosc2.c:504-508):
+ * a match may reach dsz bytes before the output start, into the dictionary's tail. */
+int or_lz4_decompress_dict(const uint8_t *in, int length, uint8_t *out, int maxout, const uint8_t *dict,
+                           int dsz) {
   if (length <= 0) return -1;
   if (maxout == 0) return (length == 1 && in[0] == 0) ? 0 : -1;
   int32_t ip = 0, op = 0;
@@ -607,7 +757,7 @@ int or_lz4_decompress(const uint8_t *in, int length, uint8_t *out, int maxout) {
     op += lit; ip += lit;
     int32_t off = in[ip] | (in[ip + 1] << 8);
     ip += 2;
-    if (off > op) return -1;   /* offset 0 is accepted by liblz4 1.9.3 (it copies zeros) */
+    if (off > op + dsz) return -1;   /* offset 0 is accepted by liblz4 1.9.3 (it copies zeros) */
     int32_t ml = (int32_t)(token & 15u);
     if (ml == LZ4_ML_MASK) {
       uint32_t s;
@@ -621,7 +771,11 @@ int or_lz4_decompress(const uint8_t *in, int length, uint8_t *out, int maxout) {
     ml += LZ4_MINMATCH;
     if (op + ml > maxout - LZ4_LASTLIT) return -1;
     if (off == 0) memset(out + op, 0, (size_t)ml);
-    else for (int32_t i = 0; i < ml; i++) out[op + i] = out[op - off + i];
+    else
+      for (int32_t i = 0; i < ml; i++) {
+        const int32_t q = op - off + i;
+        out[op + i] = q >= 0 ? out[q] : dict[dsz + q];
+      }
     op += ml;
   }
 }
@@ -725,7 +879,8 @@ static void flags_to_filter_list(uint8_t flags, uint8_t *filters) {
  * (>0), 0 when the chunk does not fit, <0 on error. */
 static int32_t compress_block(const or_cparams *cp, int32_t ts, int split, uint8_t *chunk,
                               int32_t offset, int32_t bsize, int leftover, uint8_t *dest,
-                              int32_t ntbytes, int32_t destsize, uint8_t *t1, uint8_t *t2) {
+                              int32_t ntbytes, int32_t destsize, uint8_t *t1, uint8_t *t2,
+                              const uint8_t *dict, int dsz) {
   const uint8_t *blk = pipe_forward(cp, ts, chunk, offset, bsize, t1, t2);
   if (!blk) return ERR_FILTER;
   int32_t nstreams = (split && !leftover) ? ts : 1;
@@ -751,8 +906,10 @@ static int32_t compress_block(const or_cparams *cp, int32_t ts, int split, uint8
       if (maxout <= 0) return 0;
     }
     /* the codec call (blosc/blosc2.c:1357-1366); LZ4's acceleration is 10 - clevel (get_accel 619-629) */
-    int32_t cb = cp->compcode == 1 ? or_lz4_compress(10 - cp->clevel, s, neblock, dest + written, maxout)
-                                   : or_blosclz_compress(cp->clevel, s, neblock, dest + written, maxout);
+    int32_t cb = cp->compcode == 1
+                     ? (dict ? or_lz4_compress_dict(10 - cp->clevel, s, neblock, dest + written, maxout, dict, dsz)
+                             : or_lz4_compress(10 - cp->clevel, s, neblock, dest + written, maxout))
+                     : or_blosclz_compress(cp->clevel, s, neblock, dest + written, maxout);
     if (cb < 0) return ERR_DATA;
     if (cb == 0) cb = neblock;
     if (cb == neblock) {
@@ -780,6 +937,9 @@ int or_compress_chunk(const or_cparams *cp, const void *src_, int32_t srcsize, v
   int32_t nblocks = bs ? srcsize / bs : 0, leftover = bs ? srcsize % bs : 0;
   if (leftover) nblocks++;
 
+  /* dictionaries: LZ4 only (blosc/blosc2.c:2514-2521); clevel 0 drops them (2916-2919) */
+  if (cp->use_dict && cp->compcode != 1) return -8;
+  const int use_dict = cp->use_dict && cp->clevel > 0 && srcsize >= MIN_BUF;
   uint8_t flags = F_SHUF | F_BITSHUF;   /* extended-header marker */
   int memcpyed = cp->clevel == 0 || srcsize < MIN_BUF;
   int32_t out = HDR_EXT + (memcpyed ? 0 : 4 * nblocks);
@@ -807,6 +967,7 @@ int or_compress_chunk(const or_cparams *cp, const void *src_, int32_t srcsize, v
   st32(dest + 8, (srcsize > 0 && hb > srcsize) ? srcsize : hb);
   for (int i = 0; i < 6; i++) { dest[16 + i] = cp->filters[i]; dest[24 + i] = cp->filters_meta[i]; }
   dest[22] = (uint8_t)cp->compcode;
+  if (use_dict) dest[31] |= USEDICT;   /* blosc2_initialize_header_from_context, 1037-1039 */
 
   int32_t ntbytes = 0;
   /* private copy of the input: the reference may rewrite it (see pipe_forward), and a later
@@ -814,23 +975,69 @@ int or_compress_chunk(const or_cparams *cp, const void *src_, int32_t srcsize, v
   uint8_t *work = (uint8_t *)malloc((size_t)srcsize + 64);
   if (!work) return -1;
   memcpy(work, src, (size_t)srcsize);
+  uint8_t *dict = NULL;
+  int32_t dsz = 0;
+  if (use_dict) {
+    /* blosc2_compress_ctx with use_dict (blosc/blosc2.c:3140-3235): a training pass runs the
+     * filters over every block and stores the filtered blocks in order (blosc_c with
+     * dict_training: one stream per block, no csize words, 1270-1356); when they do not fit the
+     * chunk is given up (the memcpy bit stays set, 3036-3052, and the second pass returns 0).
+     * The dictionary is the first bytes of that image: min(nblocks' * (nbytes / nblocks' / 16),
+     * min(32 KiB, nbytes / 20)), nblocks' = nblocks * typesize when split, at least 8; below
+     * 256 bytes (or a zero sample) the chunk is compressed without one (the flag cleared). */
+    if ((int64_t)srcsize + HDR_EXT > destsize) { free(work); memset(dest, 0, HDR_EXT); return 0; }
+    uint8_t *img = (uint8_t *)malloc((size_t)srcsize + 64);
+    uint8_t *t1 = (uint8_t *)malloc((size_t)bs + 64), *t2 = (uint8_t *)malloc((size_t)bs + 64);
+    if (!img || !t1 || !t2) { free(img); free(t1); free(t2); free(work); return -1; }
+    for (int32_t j = 0; j < nblocks; j++) {
+      int lo = (j == nblocks - 1) && leftover;
+      int32_t bsize = lo ? leftover : bs;
+      const uint8_t *blk = pipe_forward(cp, ts, work, j * bs, bsize, t1, t2);
+      if (!blk) { free(img); free(t1); free(t2); free(work); return ERR_FILTER; }
+      memcpy(img + (int64_t)j * bs, blk, (size_t)bsize);
+    }
+    free(t1); free(t2);
+    int32_t nbe = split ? nblocks * ts : nblocks;
+    if (nbe < 8) nbe = 8;
+    const int32_t sample = srcsize / nbe / 16;
+    int32_t dmax = srcsize / 20 < 32 * 1024 ? srcsize / 20 : 32 * 1024;
+    if (dmax < 256 || sample == 0) {
+      dest[31] &= (uint8_t)~USEDICT;
+      free(img);
+    } else {
+      dsz = nbe * sample < dmax ? nbe * sample : dmax;
+      dict = img;   /* its first dsz bytes ... */
+      /* ... as they lie in the output when they are moved behind the size word: the samples start
+       * at the bstarts (dest + 32) and the size word is stored at dest + 32 + 4 * nblocks before the
+       * move (3205-3210), so it replaces those four sample bytes */
+      for (int32_t k = 0; k < 4; k++)
+        if (4 * nblocks + k < dsz) dict[4 * nblocks + k] = (uint8_t)((uint32_t)dsz >> (8 * k));
+    }
+  }
   if (!memcpyed) {
     uint8_t *t1 = (uint8_t *)malloc((size_t)bs + 64), *t2 = (uint8_t *)malloc((size_t)bs + 64);
-    if (!t1 || !t2) { free(t1); free(t2); free(work); return -1; }
+    if (!t1 || !t2) { free(t1); free(t2); free(work); free(dict); return -1; }
     ntbytes = out;
+    if (dict) {   /* [int32 dsz | dictionary] after the bstarts (3202-3221) */
+      st32(dest + ntbytes, dsz);
+      memcpy(dest + ntbytes + 4, dict, (size_t)dsz);
+      ntbytes += 4 + dsz;
+    }
     for (int32_t j = 0; j < nblocks; j++) {
       st32(dest + HDR_EXT + 4 * j, ntbytes);
       int lo = (j == nblocks - 1) && leftover;
       int32_t bsize = lo ? leftover : bs;
       int32_t cb = compress_block(cp, ts, split, work, j * bs, bsize, lo, dest + ntbytes, ntbytes,
-                                  destsize, t1, t2);
-      if (cb < 0) { free(t1); free(t2); free(work); return cb; }
+                                  destsize, t1, t2, dict, dsz);
+      if (cb < 0) { free(t1); free(t2); free(work); free(dict); return cb; }
       if (cb == 0) { ntbytes = 0; break; }
       ntbytes += cb;
     }
     free(t1); free(t2);
     if (ntbytes == 0) memcpyed = 2;   /* fall back to a plain copy (blosc/blosc2.c:3017-3051) */
   }
+  const int dict_used = dict != NULL;
+  free(dict);
   if (memcpyed) {
     if (srcsize + HDR_EXT > destsize) {
       ntbytes = 0;
@@ -839,7 +1046,7 @@ int or_compress_chunk(const or_cparams *cp, const void *src_, int32_t srcsize, v
       ntbytes = HDR_EXT + srcsize;
       dest[2] = flags | F_MEMCPY;
     }
-  } else {
+  } else if (!dict_used) {
     /* all streams zero runs -> SPECIAL_ZERO chunk (blosc/blosc2.c:3054-3063) */
     int32_t nstreams = nblocks;
     if (split) nstreams = leftover ? (nblocks - 1) * ts + 1 : nblocks * ts;
@@ -854,7 +1061,7 @@ int or_compress_chunk(const or_cparams *cp, const void *src_, int32_t srcsize, v
 }
 
 /* read_chunk_header + initialize_context_decompression (blosc/blosc2.c:738-852, 2688-2909),
- * restricted to non-VL, non-lazy, dictionary-free chunks. */
+ * restricted to non-VL, non-lazy chunks. */
 static int parse_header(const uint8_t *src, int32_t srcsize, or_hdr *h) {
   memset(h, 0, sizeof *h);
   if (srcsize < HDR_MIN) return ERR_READ;
@@ -929,6 +1136,14 @@ int or_decompress_chunk(const void *src_, int32_t srcsize, void *dest_, int32_t 
   int memcpyed = (h.flags & F_MEMCPY) != 0;
   if (memcpyed && h.cbytes != h.nbytes + h.overhead) return ERR_DATA;
   if (h.nbytes == 0 && h.cbytes == h.overhead && !special) return 0;
+  if ((h.bflags & USEDICT) && (special || memcpyed)) {
+    /* the dictionary section is looked for right after the header (no bstarts), as the reference
+     * does (blosc/blosc2.c:2754-2809): its own memcpyed fallback chunks with the flag set fail */
+    if (srcsize - h.overhead < 4) return ERR_READ;
+    const int32_t dsz = (int32_t)ld32(src + h.overhead);
+    if (dsz <= 0 || dsz > 32 * 1024) return -9;
+    if (srcsize - h.overhead - 4 < dsz) return ERR_READ;
+  }
   if (special) {
     /* blosc_d special fills (blosc/blosc2.c:1865-1935): set_values 1644-1700 repeats the typesize
        bytes stored after the 32-byte header; set_nans 1612-1641 writes quiet NaNs (ts 4/8 only). */
@@ -953,6 +1168,15 @@ int or_decompress_chunk(const void *src_, int32_t srcsize, void *dest_, int32_t 
   if (compformat > 1) return ERR_CODEC;   /* BloscLZ and LZ4 */
   int32_t bstarts_end = h.overhead + 4 * h.nblocks;
   if (srcsize < bstarts_end) return ERR_READ;
+  const uint8_t *dict = NULL;
+  int32_t dsz = 0;
+  if (h.bflags & USEDICT) {   /* [int32 size | bytes] after the bstarts (blosc/blosc2.c:2790-2825) */
+    if (srcsize - bstarts_end < 4) return ERR_READ;
+    dsz = (int32_t)ld32(src + bstarts_end);
+    if (dsz <= 0 || dsz > 32 * 1024) return -9;
+    if (srcsize - bstarts_end - 4 < dsz) return ERR_READ;
+    dict = src + bstarts_end + 4;
+  }
   int dont_split = (h.flags >> 4) & 1;
   int32_t bs = h.blocksize;
   uint8_t *t0 = (uint8_t *)malloc((size_t)bs + 64), *t1 = (uint8_t *)malloc((size_t)bs + 64),
@@ -990,7 +1214,7 @@ int or_decompress_chunk(const void *src_, int32_t srcsize, void *dest_, int32_t 
         if (avail < cb) { rc = ERR_READ; break; }
         if (cb == neblock) {
           memcpy(d, p, (size_t)neblock);
-        } else if ((compformat == 1 ? or_lz4_decompress(p, cb, d, neblock)
+        } else if ((compformat == 1 ? or_lz4_decompress_dict(p, cb, d, neblock, dict, dsz)
                                     : or_blosclz_decompress(p, cb, d, neblock)) != neblock) {
           rc = ERR_DATA; break;
         }

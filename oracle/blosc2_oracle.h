@@ -46,7 +46,13 @@ int or_blosclz_decompress(const uint8_t *in, int length, uint8_t *out, int maxou
 /* LZ4 block codec, compformat 1 (blosc/blosc2.c:450-519 -> lz4 1.9.3 LZ4_compress_fast /
  * LZ4_decompress_safe).  compress returns 0 when the output does not fit in maxout. */
 int or_lz4_compress(int accel, const uint8_t *in, int length, uint8_t *out, int maxout);
+/* LZ4_loadDict(dict, dsz) + LZ4_compress_fast_continue (external-dictionary mode), as
+ * lz4_wrap_compress does per stream when the context has a dictionary (blosc2.c:455-465). */
+int or_lz4_compress_dict(int accel, const uint8_t *in, int length, uint8_t *out, int maxout,
+                         const uint8_t *dict, int dsz);
 int or_lz4_decompress(const uint8_t *in, int length, uint8_t *out, int maxout);
+int or_lz4_decompress_dict(const uint8_t *in, int length, uint8_t *out, int maxout, const uint8_t *dict,
+                           int dsz);
 
 /* Chunk engine, serial (nthreads == 1) layout, BloscLZ codec only.
  * cparams mirror blosc2_cparams (include/blosc2.h of the reference, 1173-1211). */
@@ -58,6 +64,7 @@ typedef struct {
   int splitmode;       /* BLOSC_ALWAYS_SPLIT=1, NEVER=2, AUTO=3, FORWARD_COMPAT=4 */
   uint8_t filters[6];
   uint8_t filters_meta[6];
+  int use_dict;        /* LZ4 only: a dictionary from the filtered chunk (blosc2.c:3151-3235) */
 } or_cparams;
 
 /* Automatic blocksize (reference: blosc/stune.c:47-165 + split_block 186-215). */

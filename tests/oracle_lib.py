@@ -15,7 +15,7 @@ _ref = None
 class OrCParams(C.Structure):
     _fields_ = [("compcode", C.c_int), ("clevel", C.c_int), ("typesize", C.c_int),
                 ("blocksize", C.c_int), ("splitmode", C.c_int),
-                ("filters", C.c_uint8 * 6), ("filters_meta", C.c_uint8 * 6)]
+                ("filters", C.c_uint8 * 6), ("filters_meta", C.c_uint8 * 6), ("use_dict", C.c_int)]
 
 
 def oracle():
@@ -71,9 +71,10 @@ def ref():
 
 
 def or_cparams(clevel=5, typesize=4, filters=(0, 0, 0, 0, 0, 1), filters_meta=(0,) * 6,
-               blocksize=0, splitmode=4, compcode=0):
+               blocksize=0, splitmode=4, compcode=0, use_dict=0):
     p = OrCParams()
     p.compcode, p.clevel, p.typesize, p.blocksize, p.splitmode = compcode, clevel, typesize, blocksize, splitmode
+    p.use_dict = use_dict
     for i in range(6):
         p.filters[i], p.filters_meta[i] = filters[i], filters_meta[i] & 0xFF
     return p
@@ -104,7 +105,7 @@ def ref_compress(src: np.ndarray, **kw):
                  filters=kw.get("filters", (0, 0, 0, 0, 0, 1)),
                  filters_meta=kw.get("filters_meta", (0,) * 6),
                  blocksize=kw.get("blocksize", 0), splitmode=kw.get("splitmode", 4),
-                 compcode=kw.get("compcode", 0))
+                 compcode=kw.get("compcode", 0), use_dict=kw.get("use_dict", 0))
     ctx = R.blosc2_create_cctx(cp)
     raw = src.view(np.uint8).reshape(-1).copy()   # the reference may rewrite its input
     out = np.zeros(raw.nbytes + 64, np.uint8)
