@@ -39,9 +39,10 @@ class DParams(C.Structure):
 
 
 def cparams(clevel=5, typesize=8, filters=(0, 0, 0, 0, 0, SHUFFLE), filters_meta=(0,) * 6,
-            blocksize=0, splitmode=FORWARD_COMPAT_SPLIT, compcode=0, nthreads=1):
+            blocksize=0, splitmode=FORWARD_COMPAT_SPLIT, compcode=0, nthreads=1, use_dict=0):
     p = CParams()
     p.compcode, p.clevel, p.typesize, p.nthreads = compcode, clevel, typesize, nthreads
+    p.use_dict = use_dict
     p.blocksize, p.splitmode = blocksize, splitmode
     for i in range(MAX_FILTERS):
         p.filters[i] = filters[i]

@@ -34,6 +34,8 @@ struct CompressPlan {
   uint8_t filters_meta[6];
   uint8_t header[32];      // header template (cbytes patched per chunk)
   int32_t compcode;        // BLOSC_BLOSCLZ (0) or BLOSC_LZ4 (1)
+  bool use_dict;           // LZ4 with a dictionary requested and in force (clevel > 0, not memcpyed)
+  int32_t dict_size;       // its size (0: the reference falls back to no dictionary)
 };
 
 // Fill the plan from cparams-level values the way blosc2_compress_ctx does (initialize_context_
@@ -44,7 +46,7 @@ struct CompressPlan {
 int make_compress_plan(CompressPlan* p, int32_t nbytes, int32_t destsize, int clevel, int32_t typesize,
                        int32_t ctx_blocksize, int32_t splitmode, const uint8_t* filters,
                        const uint8_t* filters_meta, int32_t* computed_blocksize, bool extended = true,
-                       int compcode = 0, int compcode_meta = 0, int user_version = 1);
+                       int compcode = 0, int compcode_meta = 0, int user_version = 1, int use_dict = 0);
 
 // Compress `nchunks` chunks: chunk i is d_src + i*src_stride, its output goes to
 // d_dst + i*dst_stride (capacity plan.destsize), its cbytes (>0, 0 = does not fit) to d_cbytes[i].

@@ -231,6 +231,7 @@ static EvPair ev_filter, ev_encode, ev_final, ev_decode, ev_unfilter;
 // ================================================================ compression: geometry ====
 struct CGeom {
   int32_t nbytes, bs, nblocks, leftover, spb, nsc, neblock, ts, destsize, clevel, overhead, compcode;
+  int32_t dict_size;   // LZ4 dictionary section [int32 size | bytes] after the bstarts (0: none)
   int32_t front;   // encoder pull schedule (pull_to_stream), 0 = stream order
   int64_t src_stride, wstride, dst_stride;
 };
@@ -591,6 +592,27 @@ __device__ __forceinline__ int32_t wave_common_back(gin_t in, int32_t a, int32_t
   }
   return lim;
 }
+// the same over two sequences a[..] and b[..] (an LZ4 match whose source is the dictionary)
+__device__ __forceinline__ int32_t wave_common_fwd2(gin_t a, gin_t b, int32_t lim) {
+  const int lane = lane_id();
+  for (int32_t x = 0; x < lim; x += 64) {
+    const int32_t i = x + lane;
+    const bool diff = i < lim && a[i] != b[i];
+    const uint64_t m = __ballot(diff);
+    if (m) return x + __builtin_ctzll(m);
+  }
+  return lim;
+}
+__device__ __forceinline__ int32_t wave_common_back2(gin_t a, gin_t b, int32_t lim) {   // a[-1-i] vs b[-1-i]
+  const int lane = lane_id();
+  for (int32_t x = 0; x < lim; x += 64) {
+    const int32_t i = x + lane;
+    const bool diff = i < lim && a[-1 - i] != b[-1 - i];
+    const uint64_t m = __ballot(diff);
+    if (m) return x + __builtin_ctzll(m);
+  }
+  return lim;
+}
 __device__ __forceinline__ void wave_bytes(B2H_GLB uint8_t* o, gin_t s, int32_t n) {
   for (int32_t i = lane_id(); i < n; i += 64) o[i] = s[i];
 }
@@ -748,9 +770,208 @@ __device__ int32_t lz4_encode_wave(gin_t in, int32_t n, int accel, B2H_GLB uint8
   return fail ? 0 : op;
 }
 
+// LZ4_loadDict(dict, dsz) + LZ4_compress_fast_continue, external-dictionary mode (lz4 1.9.3; the
+// call sequence of lz4_wrap_compress with a dictionary, blosc/blosc2.c:455-465; restated in
+// oracle/blosc2_oracle.c or_lz4_compress_dict and pinned to the reference there).  The same
+// window search as lz4_encode_wave (byU32 table, hash5), on 32-bit indices: the dictionary's byte
+// d is index 65536 - dsz + d, the stream's byte i is 65536 + i; the dictionary's positions 0, 3,
+// 6, ... are inserted first (lanes of one store apply in lane order: the later position wins, as
+// serially); candidates below 65536 - dsz (empty slots) or farther than 65535 are skipped; a
+// match found in the dictionary extends to its end and then on from the stream's start.
+__device__ int32_t lz4_encode_wave_dict(gin_t in, int32_t n, int accel, B2H_GLB uint8_t* out, Lz4Lds<false> tab,
+                                        B2H_LDS uint32_t* bits, int32_t* peak_out, gin_t dict, int32_t dsz) {
+  constexpr int32_t kMfLimit = 12, kLastLit = 5, kRunMask = 15, kDMax = 65535;
+  constexpr uint32_t kStart = 65536;
+  const int lane = lane_id();
+  const uint32_t dict0 = kStart - (uint32_t)dsz;   // index of dict[0]; below it: empty slots
+  const int32_t mflimit1 = n - kMfLimit + 1, matchlimit = n - kLastLit;
+  int32_t anchor = 0, op = 0, peak = 0;
+  bool fail = false;
+  auto need = [&](int32_t v) { peak = max(peak, v); return v <= n; };
+  auto at = [&](uint32_t idx) -> gin_t { return idx < kStart ? dict + (idx - dict0) : in + (idx - kStart); };
+  {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    B2H_LDS u32x4* t = (B2H_LDS u32x4*)tab.base;
+    for (int i = lane; i < kLz4TabBytes / 16; i += 64) t[i] = u32x4{0, 0, 0, 0};
+    for (int i = lane; i < kLz4BitsBytes / 4; i += 64) bits[i] = 0u;
+    for (int32_t base = 0; 3 * base <= dsz - 8; base += 64) {   // LZ4_loadDict
+      // an atomic exchange per lane: the lanes of one LDS atomic apply in lane order, so of two
+      // positions with one bucket the later (higher lane) stays, as in the serial insert loop
+      const int32_t p = 3 * (base + lane);
+      if (p <= dsz - 8)
+        (void)__hip_atomic_exchange(&((B2H_LDS uint32_t*)tab.base)[lz4_hash_at(dict + p, false)], dict0 + (uint32_t)p,
+                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  if (n >= kMfLimit + 1) {
+    if (lane == 0) tab.put(lz4_hash_at(in, false), (int32_t)kStart);
+    int32_t ip = 1;
+    for (;;) {
+      int32_t pos = ip, k0 = 0;
+      uint32_t midx = 0;
+      bool last = false;
+      for (;;) {
+        const int32_t k = k0 + lane;
+        const int32_t stp = k == 0 ? 1 : ((accel << 6) + k - 1) >> 6;
+        const int32_t incl = wave_scan_add(stp);
+        const int32_t p = pos + incl - stp;
+        const bool valid = p + stp <= mflimit1;
+        const uint64_t vmask = __ballot(valid);
+        const int32_t E = vmask == ~0ull ? 64 : __builtin_ctzll(~vmask);
+        uint32_t seq = 0, h = 0;
+        if (valid) {
+          seq = ldu32(in + p);
+          h = lz4_hash_seq(seq, ldu32(in + p + 4), false);
+        }
+        const uint32_t cand = valid ? (uint32_t)tab.get(h) : 0u;
+        uint32_t old = 0;
+        if (valid) {
+          old = __hip_atomic_fetch_or(&bits[h >> 5], 1u << (h & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          bits[h >> 5] = 0u;
+        }
+        const uint64_t dup = __ballot(valid && ((old >> (h & 31)) & 1u));
+        const int32_t W = min(E, dup ? __builtin_ctzll(dup) : 64);
+        const uint32_t cur = kStart + (uint32_t)p;
+        bool ok = false;
+        if (lane < W && cand >= dict0 && cand + kDMax >= cur) ok = ldu32(at(cand)) == seq;
+        const uint64_t om = __ballot(ok);
+        const int32_t f = om ? __builtin_ctzll(om) : W;
+        if (lane < W && lane <= f) tab.put(h, (int32_t)cur);
+        if (om) {
+          ip = __builtin_amdgcn_readlane(p, f);
+          midx = (uint32_t)__builtin_amdgcn_readlane((int32_t)cand, f);
+          break;
+        }
+        if (W >= E && E < 64) { last = true; break; }
+        pos = __builtin_amdgcn_readlane(p, W - 1) + __builtin_amdgcn_readlane(stp, W - 1);
+        k0 += W;
+      }
+      if (last) break;
+      {   // catch up, not below the start of the match's segment
+        const bool md = midx < kStart;
+        const int32_t mpos = md ? (int32_t)(midx - dict0) : (int32_t)(midx - kStart);
+        const int32_t back = wave_common_back2(in + ip, (md ? dict : in) + mpos, min(ip - anchor, mpos));
+        ip -= back;
+        midx -= (uint32_t)back;
+      }
+      int32_t token = op++;
+      uint32_t tokv;
+      {
+        const int32_t lit = ip - anchor;
+        if (!need(op + lit + (2 + 1 + kLastLit) + lit / 255)) { fail = true; break; }
+        if (lit >= kRunMask) {
+          const int32_t len = lit - kRunMask;
+          tokv = kRunMask << 4;
+          wave_fill255(out + op, len / 255);
+          op += len / 255;
+          if (lane == 0) out[op] = (uint8_t)(len % 255);
+          op++;
+        } else {
+          tokv = (uint32_t)lit << 4;
+        }
+        if (lit > 64) wave_copy(out + op, in + anchor, lit);
+        else wave_bytes(out + op, in + anchor, lit);
+        op += lit;
+      }
+      bool done = false;
+      for (;;) {   // _next_match
+        const uint32_t d = kStart + (uint32_t)ip - midx;
+        if (lane == 0) { out[op] = (uint8_t)d; out[op + 1] = (uint8_t)(d >> 8); }
+        op += 2;
+        int32_t mc;
+        if (midx < kStart) {   // in the dictionary: up to its end, then on from the stream's start
+          const int32_t mpos = (int32_t)(midx - dict0);
+          const int32_t limit = min(ip + (dsz - mpos), matchlimit);
+          mc = wave_common_fwd2(in + ip + 4, dict + mpos + 4, max(0, limit - (ip + 4)));
+          ip += mc + 4;
+          if (ip == limit) {
+            const int32_t more = wave_common_fwd2(in + limit, in, max(0, matchlimit - limit));
+            mc += more;
+            ip += more;
+          }
+        } else {
+          const int32_t mpos = (int32_t)(midx - kStart);
+          mc = wave_common_fwd(in, ip + 4, mpos + 4, max(0, matchlimit - (ip + 4)));
+          ip += mc + 4;
+        }
+        if (!need(op + (1 + kLastLit) + (mc + 240) / 255)) { fail = true; break; }
+        if (mc >= 15) {
+          tokv += 15;
+          mc -= 15;
+          wave_fill255(out + op, mc / 255);
+          op += mc / 255;
+          if (lane == 0) out[op] = (uint8_t)(mc % 255);
+          op++;
+        } else {
+          tokv += (uint32_t)mc;
+        }
+        if (lane == 0) out[token] = (uint8_t)tokv;
+        anchor = ip;
+        if (ip >= mflimit1) { done = true; break; }
+        if (lane == 0) tab.put(lz4_hash_at(in + ip - 2, false), (int32_t)(kStart + (uint32_t)(ip - 2)));
+        const uint32_t h = lz4_hash_at(in + ip, false);
+        const uint32_t mi = (uint32_t)tab.get(h);
+        const uint32_t cur = kStart + (uint32_t)ip;
+        if (lane == 0) tab.put(h, (int32_t)cur);
+        if (mi >= dict0 && mi + kDMax >= cur && ldu32(at(mi)) == ldu32(in + ip)) {
+          midx = mi;
+          token = op++;
+          tokv = 0;
+          continue;
+        }
+        break;
+      }
+      if (fail || done) break;
+      ip++;
+    }
+  }
+  if (!fail) {
+    const int32_t last = n - anchor;
+    if (!need(op + last + 1 + (last + 255 - kRunMask) / 255)) {
+      fail = true;
+    } else {
+      if (last >= kRunMask) {
+        const int32_t acc = last - kRunMask;
+        if (lane == 0) out[op] = kRunMask << 4;
+        op++;
+        wave_fill255(out + op, acc / 255);
+        op += acc / 255;
+        if (lane == 0) out[op] = (uint8_t)(acc % 255);
+        op++;
+      } else {
+        if (lane == 0) out[op] = (uint8_t)(last << 4);
+        op++;
+      }
+      if (last > 64) wave_copy(out + op, in + anchor, last);
+      else wave_bytes(out + op, in + anchor, last);
+      op += last;
+    }
+  }
+  *peak_out = peak;
+  return fail ? 0 : op;
+}
+
+// The dictionary section of a chunk's output ([int32 size | bytes] after the bstarts, blosc/blosc2.c:
+// 3202-3221): the first dict_size bytes of the training pass's image -- the filtered blocks in
+// order, which is the filtered image -- as they lie once the size word has been stored over four of
+// them (the samples start at the bstarts and are moved behind the size word, 3205-3210).
+__global__ void k_put_dict(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restrict__ dst) {
+  const int32_t c = blockIdx.x;
+  uint8_t* d = dst + (int64_t)c * g.dst_stride + g.overhead + 4 * g.nblocks;
+  const uint8_t* f = filt + (int64_t)c * g.wstride;
+  const int32_t dsz = g.dict_size, w = 4 * g.nblocks;
+  for (int32_t i = threadIdx.x; i < dsz + 4; i += blockDim.x) {
+    uint8_t v;
+    if (i < 4) v = (uint8_t)((uint32_t)dsz >> (8 * i));
+    else if (i - 4 >= w && i - 4 < w + 4) v = (uint8_t)((uint32_t)dsz >> (8 * (i - 4 - w)));
+    else v = f[i - 4];
+    d[i] = v;
+  }
+}
+
 __global__ __launch_bounds__(64) void k_encode_lz4(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
                                                    StreamResult* __restrict__ res, int32_t nstreams_total,
-                                                   int32_t* __restrict__ next) {
+                                                   int32_t* __restrict__ next, const uint8_t* __restrict__ dst) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   B2H_LDS uint8_t* lds = (B2H_LDS uint8_t*)smem;
   B2H_LDS uint32_t* bits = (B2H_LDS uint32_t*)(lds + kLz4TabBytes);
@@ -775,7 +996,11 @@ __global__ __launch_bounds__(64) void k_encode_lz4(CGeom g, const uint8_t* __res
     } else {
       int32_t peak = 0;
       int32_t cb;
-      if (len < 65536 + 11) {
+      if (g.dict_size > 0) {   // LZ4_compress_fast_continue: byU32 whatever the length
+        Lz4Lds<false> t{lds};
+        gin_t dict = (gin_t)(dst + (int64_t)c * g.dst_stride + g.overhead + 4 * g.nblocks + 4);
+        cb = lz4_encode_wave_dict(in, len, accel, out, t, bits, &peak, dict, g.dict_size);
+      } else if (len < 65536 + 11) {
         Lz4Lds<true> t{lds};
         cb = lz4_encode_wave<true>(in, len, accel, out, t, bits, &peak);
       } else {
@@ -791,7 +1016,7 @@ __global__ __launch_bounds__(64) void k_encode_lz4(CGeom g, const uint8_t* __res
 }
 
 static int launch_encode_lz4(Workspace* ws, const CGeom& g, const uint8_t* filt, StreamResult* res, int64_t ntot,
-                             int32_t* next, hipStream_t st) {
+                             int32_t* next, hipStream_t st, uint8_t* d_dst) {
   (void)ws;
   const size_t lds = kLz4TabBytes + kLz4BitsBytes;
   int dev = 0, ncu = 0, per_cu = 0;
@@ -801,7 +1026,7 @@ static int launch_encode_lz4(Workspace* ws, const CGeom& g, const uint8_t* filt,
       hipSuccess) per_cu = 1;
   const int64_t slots = (int64_t)std::max(1, per_cu) * std::max(1, ncu);
   const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(ntot, slots));
-  k_encode_lz4<<<grid, 64, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next);
+  k_encode_lz4<<<grid, 64, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, d_dst);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -822,7 +1047,7 @@ __global__ void k_finalize(CGeom g, const StreamResult* __restrict__ res, Place*
   const StreamResult* r = res + (int64_t)c * g.nsc;
   Place* pl = place + (int64_t)c * g.nsc;
   const int32_t ovh = g.overhead;
-  int32_t ntbytes = ovh + 4 * g.nblocks;
+  int32_t ntbytes = ovh + 4 * g.nblocks + (g.dict_size ? 4 + g.dict_size : 0);
   const int32_t destsize = g.destsize;
   bool ok = true, all_zero = true;
   int32_t l = 0;
@@ -868,7 +1093,7 @@ __global__ void k_finalize(CGeom g, const StreamResult* __restrict__ res, Place*
   int32_t m, cb;
   if (ok) {
     const int32_t nstreams = g.nsc;
-    if (all_zero && ntbytes == ovh + 4 * g.nblocks + 4 * nstreams) {
+    if (all_zero && !g.dict_size && ntbytes == ovh + 4 * g.nblocks + 4 * nstreams) {
       m = 2;
       cb = ovh;
       d[31] |= (uint8_t)(kSpecialZero << 4);
@@ -973,7 +1198,7 @@ static int32_t split_block(int32_t splitmode, int compcode, const uint8_t* filte
 int make_compress_plan(CompressPlan* p, int32_t nbytes, int32_t destsize, int clevel, int32_t typesize,
                        int32_t ctx_blocksize, int32_t splitmode, const uint8_t* filters,
                        const uint8_t* filters_meta, int32_t* computed_blocksize, bool extended, int compcode,
-                       int compcode_meta, int user_version) {
+                       int compcode_meta, int user_version, int use_dict) {
   memset(p, 0, sizeof *p);
   // BloscLZ and LZ4 on the device; user codecs (> BLOSC2_DEFINED_CODECS_STOP) through host callbacks
   if (compcode != 0 && compcode != 1 && compcode <= 31) return -7;   // BLOSC2_ERROR_CODEC_SUPPORT
@@ -1020,7 +1245,9 @@ int make_compress_plan(CompressPlan* p, int32_t nbytes, int32_t destsize, int cl
   // write_compression_header (blosc/blosc2.c:2911-3001)
   uint8_t flags = extended ? (kFlagShuffle | kFlagBitshuffle) : 0;
   bool memcpyed = clevel == 0 || nbytes < kMinBuffer;
-  if (!memcpyed && p->overhead + 4 * nblocks > destsize) memcpyed = true;
+  // a dictionary's training pass writes no bstarts: only the header must fit (2940-2942, 2960)
+  const bool dict_training = use_dict && compcode == 1 && extended;
+  if (!memcpyed && p->overhead + (dict_training ? 0 : 4 * nblocks) > destsize) memcpyed = true;
   if (memcpyed) {
     flags |= kFlagMemcpy;
   } else {
@@ -1046,6 +1273,20 @@ int make_compress_plan(CompressPlan* p, int32_t nbytes, int32_t destsize, int cl
   for (int i = 0; i < 6; i++) { h[16 + i] = filters[i]; h[24 + i] = filters_meta[i]; }
   h[22] = (uint8_t)compcode;   // udcompcode = the codec (blosc/blosc2.c:1030)
   h[23] = (uint8_t)compcode_meta;
+  // LZ4 dictionaries (blosc/blosc2.c:3151-3235): the size the reference derives from the chunk
+  // geometry; below BLOSC2_MINUSEFULDICT (or a zero sample) it compresses without one
+  p->use_dict = use_dict && compcode == 1 && !memcpyed;
+  p->dict_size = 0;
+  if (p->use_dict) {
+    int32_t nbe = p->split ? nblocks * ts : nblocks;
+    if (nbe < 8) nbe = 8;
+    const int32_t sample = nbytes / nbe / 16;
+    const int32_t dmax = std::min(32 * 1024, nbytes / 20);
+    if (dmax >= 256 && sample > 0) {
+      p->dict_size = (int32_t)std::min<int64_t>((int64_t)nbe * sample, dmax);
+      h[31] |= 0x01;   // BLOSC2_USEDICT (blosc2_initialize_header_from_context, 1037-1039)
+    }
+  }
   return 0;
 }
 
@@ -1135,6 +1376,7 @@ static CGeom make_geom(const CompressPlan& P, int64_t src_stride, int64_t dst_st
   g.destsize = P.destsize;
   g.overhead = P.overhead;
   g.compcode = P.compcode;
+  g.dict_size = P.use_dict ? P.dict_size : 0;
   g.src_stride = src_stride;
   g.dst_stride = dst_stride;
   g.wstride = ((int64_t)n + 255) / 256 * 256 + 256;
@@ -1198,6 +1440,33 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
   uint8_t* htpl = ws->mode.as<uint8_t>() + sizeof(int32_t) * (size_t)nchunks;
   htpl = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(htpl) + 15) & ~uintptr_t(15));
   HIPCHK(hipMemcpyAsync(htpl, P.header, 32, hipMemcpyHostToDevice, st));
+  if (P.use_dict && (int64_t)P.nbytes + P.overhead > P.destsize) {
+    // The reference's training pass stores the filtered blocks uncompressed (blosc_c with
+    // dict_training, blosc/blosc2.c:1343-1356), each after its filters ran: a filter error first;
+    // then the first block that does not fit gives up the chunk when no room is left at all (the
+    // memcpy bit stays set and both passes give up, 3036-3052: cbytes 0), and is an overrun
+    // otherwise (cbytes > maxout, 1417-1420).
+    for (int k = 0; k < nact; k++) {
+      const uint8_t f = P.filters[act[k]], meta = P.filters_meta[act[k]];
+      int zeroed = 0;
+      if (f == kTruncPrec && !hostside_trunc_ok((int8_t)meta, g.ts, &zeroed)) return E_FILTER;
+      if (f == kIntTrunc && !hostside_int_trunc_ok((int8_t)meta, P.typesize, &zeroed)) return E_FILTER;
+    }
+    const int64_t room = (int64_t)P.destsize - P.overhead;
+    if (room > 0 && room % g.bs != 0) {
+      snprintf(g_err, sizeof g_err, "dictionary training block overruns the destination");
+      return E_WRITE;
+    }
+    k_memcpy_chunks<<<dim3(1, nchunks), 256, 0, st>>>(d_src, src_stride, d_dst, dst_stride, n, nullptr, htpl,
+                                                      d_cbytes, P.overhead, P.destsize);
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
+  if (g.dict_size > 0 && (int64_t)P.overhead + 4 * g.nblocks + 4 + g.dict_size > P.destsize) {
+    // only with blocks of a few bytes: the reference then stores the dictionary past destsize
+    snprintf(g_err, sizeof g_err, "bstarts + dictionary section exceed destsize");
+    return E_PARAM;
+  }
 
   const uint8_t* raw = d_src;
   int64_t raw_stride = src_stride;
@@ -1218,34 +1487,36 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
   const bool fuse_ds = nact == 2 && P.filters[act[0]] == kDelta && P.filters[act[1]] == kShuffle &&
                        (P.filters_meta[act[1]] == 0 || P.filters_meta[act[1]] == g.ts) &&
                        (g.ts == 2 || g.ts == 4 || g.ts == 8);
-  if (fuse_ds) {   // output where the two-launch loop leaves it: ring[1], stride wstride
-    dim3 grid(g.nblocks, nchunks);
-    k_ffilter_ds<<<grid, kBlockThreads, 0, st>>>(g, raw, raw_stride, ring[0], ring[1], g.wstride);
-    filt = ring[1];
-    filt_stride = g.wstride;
-  }
-  for (int pass = two_pass ? 1 : 0; pass <= (two_pass ? 2 : 0) && !fuse_ds; pass++) {
-    const uint8_t* cur = raw;
-    int64_t cur_stride = raw_stride;
-    for (int k = 0; k < nact; k++) {
-      const uint8_t f = P.filters[act[k]], meta = P.filters_meta[act[k]];
-      int zeroed = 0;
-      if (f == kTruncPrec && !hostside_trunc_ok((int8_t)meta, g.ts, &zeroed)) return E_FILTER;
-      if (f == kIntTrunc && !hostside_int_trunc_ok((int8_t)meta, P.typesize, &zeroed)) return E_FILTER;
-      // bytedelta's channel count is its meta; 0 means the super-chunk's typesize (bytedelta.c:90-98),
-      // which a caller without a super-chunk resolves before this point -- the chunk's own here
-      const uint8_t kmeta = (f == kBytedelta && meta == 0) ? (uint8_t)g.ts : meta;
-      uint8_t* outb = ring[k % 3];
-      const int64_t out_stride = (k % 3 == 2) ? g.wstride : g.wstride;
-      dim3 grid(pass == 1 ? 1 : (pass == 2 ? g.nblocks - 1 : g.nblocks), nchunks);
-      k_ffilter<<<grid, kBlockThreads, 0, st>>>(g, pass, f, kmeta, cur, cur_stride, outb, out_stride, raw, raw_stride, zeroed);
-      cur = outb;
-      cur_stride = out_stride;
+  auto run_filters = [&]() -> int {
+    if (fuse_ds) {   // output where the two-launch loop leaves it: ring[1], stride wstride
+      dim3 grid(g.nblocks, nchunks);
+      k_ffilter_ds<<<grid, kBlockThreads, 0, st>>>(g, raw, raw_stride, ring[0], ring[1], g.wstride);
+      filt = ring[1];
+      filt_stride = g.wstride;
     }
-    filt = cur;
-    filt_stride = cur_stride;
-  }
-  ev_filter.stop(st);
+    for (int pass = two_pass ? 1 : 0; pass <= (two_pass ? 2 : 0) && !fuse_ds; pass++) {
+      const uint8_t* cur = raw;
+      int64_t cur_stride = raw_stride;
+      for (int k = 0; k < nact; k++) {
+        const uint8_t f = P.filters[act[k]], meta = P.filters_meta[act[k]];
+        int zeroed = 0;
+        if (f == kTruncPrec && !hostside_trunc_ok((int8_t)meta, g.ts, &zeroed)) return E_FILTER;
+        if (f == kIntTrunc && !hostside_int_trunc_ok((int8_t)meta, P.typesize, &zeroed)) return E_FILTER;
+        // bytedelta's channel count is its meta; 0 means the super-chunk's typesize (bytedelta.c:90-98),
+        // which a caller without a super-chunk resolves before this point -- the chunk's own here
+        const uint8_t kmeta = (f == kBytedelta && meta == 0) ? (uint8_t)g.ts : meta;
+        uint8_t* outb = ring[k % 3];
+        dim3 grid(pass == 1 ? 1 : (pass == 2 ? g.nblocks - 1 : g.nblocks), nchunks);
+        k_ffilter<<<grid, kBlockThreads, 0, st>>>(g, pass, f, kmeta, cur, cur_stride, outb, g.wstride, raw, raw_stride, zeroed);
+        cur = outb;
+        cur_stride = g.wstride;
+      }
+      filt = cur;
+      filt_stride = cur_stride;
+    }
+    return 0;
+  };
+  if ((rc = run_filters())) return rc;
   if (nact > 0 && filt_stride != g.wstride) return E_FAILURE;
   // encoder reads the filtered streams at c*wstride: if no filter ran, stage the input there
   if (nact == 0) {
@@ -1255,6 +1526,14 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
     k_copy_work<<<grid, 256, 0, st>>>(raw, raw_stride, ws->t1.as<uint8_t>(), g.wstride, n);
     filt = ws->t1.as<uint8_t>();
   }
+  if (g.dict_size > 0) {
+    // the dictionary section comes from the training pass's image (blosc/blosc2.c:3146-3221)
+    k_put_dict<<<nchunks, 256, 0, st>>>(g, filt, d_dst);
+    // with >= 3 filters that pass rewrote the input (pipeline_forward's buffer cycle, 1048-1180): the real pass
+    // filters the rewritten input again
+    if (clobber && (rc = run_filters())) return rc;
+  }
+  ev_filter.stop(st);
   HIPCHK(hipGetLastError());
   return encode_stage(ws, P, g, filt, raw, raw_stride, d_dst, dst_stride, d_cbytes, nchunks, htpl, ntot, st);
 }
@@ -1276,7 +1555,7 @@ static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const ui
   int32_t* next = ws->qctr.as<int32_t>();
   HIPCHK(hipMemsetAsync(next, 0, sizeof(int32_t), st));
   if (g.compcode == 1) {
-    rc = launch_encode_lz4(ws, g, filt, res, ntot, next, st);
+    rc = launch_encode_lz4(ws, g, filt, res, ntot, next, st, d_dst);
     if (rc) return rc;
   } else {
     static const int front = [] { const char* e = getenv("B2H_ENC_FRONT"); return e ? std::max(0, atoi(e)) : 2; }();

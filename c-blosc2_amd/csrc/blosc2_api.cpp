@@ -185,7 +185,8 @@ int check_supported(const blosc2_context* c) {
     TRACE_ERROR("codec %d is not implemented by the MI355X engine (BloscLZ, LZ4 and user codecs)", c->compcode);
     return BLOSC2_ERROR_CODEC_SUPPORT;
   }
-  if (c->use_dict) {
+  // blosc/blosc2.c:2514-2521 (ZSTD and LZ4HC are refused above as codecs)
+  if (c->use_dict && c->compcode != BLOSC_LZ4) {
     TRACE_ERROR("`use_dict` is only supported for ZSTD, LZ4, and LZ4HC codecs.");
     return BLOSC2_ERROR_CODEC_PARAM;
   }
@@ -224,7 +225,7 @@ int compress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void* d
   int32_t computed = 0;
   int rc = b2h::make_compress_plan(&plan, srcsize, destsize, ctx->clevel, ctx->typesize, blocksize_in, ctx->splitmode,
                                    ctx->filters, ctx->filters_meta, &computed, extended, ctx->compcode,
-                                   ctx->compcode_meta);
+                                   ctx->compcode_meta, 1, ctx->use_dict);
   if (rc < 0) return rc;
   if (sticky) ctx->blocksize = computed;
   if ((rc = check_supported(ctx)) < 0) return rc;
@@ -545,6 +546,12 @@ int compress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void*
   if (rc < 0) return rc;
   if (sticky) ctx->blocksize = computed;
   if ((rc = check_supported(ctx)) < 0) return rc;
+  if (P.use_dict) {
+    // the dictionary's training pass is a device-pipeline feature (compress_batch); host-callback
+    // pipelines (user filters) do not run it
+    TRACE_ERROR("`use_dict` with user-registered filters is not supported by the MI355X engine");
+    return BLOSC2_ERROR_CODEC_PARAM;
+  }
   Device& d = ctx->dev;
   if (!d.init()) return BLOSC2_ERROR_FAILURE;
   const int32_t n = srcsize, ovh = P.overhead;
@@ -1494,7 +1501,8 @@ int b2h_compress_batch(const blosc2_cparams* cp, const void* d_src, int32_t chun
   b2h::CompressPlan plan;
   int32_t computed = 0;
   rc = b2h::make_compress_plan(&plan, chunk_nbytes, dst_capacity, cp->clevel, cp->typesize, cp->blocksize,
-                               cp->splitmode, cp->filters, cp->filters_meta, &computed, true, cp->compcode, cp->compcode_meta);
+                               cp->splitmode, cp->filters, cp->filters_meta, &computed, true, cp->compcode, cp->compcode_meta,
+                               1, cp->use_dict);
   if (rc < 0) return rc;
   return b2h::compress_batch(plan, static_cast<const uint8_t*>(d_src), src_stride, nchunks,
                              static_cast<uint8_t*>(d_dst), dst_stride, d_cbytes, static_cast<hipStream_t>(stream));

@@ -929,8 +929,9 @@ int or_compress_chunk(const or_cparams *cp, const void *src_, int32_t srcsize, v
   const uint8_t *src = (const uint8_t *)src_;
   uint8_t *dest = (uint8_t *)dest_;
   if (cp->compcode != 0 && cp->compcode != 1) return ERR_CODEC;   /* BloscLZ, LZ4 */
-  if (srcsize > 0x7fffffff - 32) return -9;
-  if (destsize < 32) return -9;
+  /* buffer size limits (blosc/blosc2.c:2492-2504): BLOSC2_ERROR_MAX_BUFSIZE_EXCEEDED */
+  if (srcsize > 0x7fffffff - 32) return -35;
+  if (destsize < 32) return -35;
   if (cp->clevel < 0 || cp->clevel > 9) return -10;
   int32_t ts = eff_typesize(cp);
   int32_t bs = or_compute_blocksize(cp, srcsize);
@@ -943,7 +944,8 @@ int or_compress_chunk(const or_cparams *cp, const void *src_, int32_t srcsize, v
   uint8_t flags = F_SHUF | F_BITSHUF;   /* extended-header marker */
   int memcpyed = cp->clevel == 0 || srcsize < MIN_BUF;
   int32_t out = HDR_EXT + (memcpyed ? 0 : 4 * nblocks);
-  if (!memcpyed && out > destsize) { memcpyed = 1; out = HDR_EXT; }
+  /* a dictionary's training pass writes no bstarts: only the header must fit (2940-2942, 2960) */
+  if (!memcpyed && (use_dict ? HDR_EXT : out) > destsize) { memcpyed = 1; out = HDR_EXT; }
   int split = 0;
   if (memcpyed) {
     flags |= F_MEMCPY;
@@ -984,8 +986,11 @@ int or_compress_chunk(const or_cparams *cp, const void *src_, int32_t srcsize, v
      * chunk is given up (the memcpy bit stays set, 3036-3052, and the second pass returns 0).
      * The dictionary is the first bytes of that image: min(nblocks' * (nbytes / nblocks' / 16),
      * min(32 KiB, nbytes / 20)), nblocks' = nblocks * typesize when split, at least 8; below
-     * 256 bytes (or a zero sample) the chunk is compressed without one (the flag cleared). */
-    if ((int64_t)srcsize + HDR_EXT > destsize) { free(work); memset(dest, 0, HDR_EXT); return 0; }
+     * 256 bytes (or a zero sample) the chunk is compressed without one (the flag cleared).
+     * A training block that does not fit: with no room left at all the pass gives up (0, and the
+     * chunk is 0); with some room, the block is stored anyway and blosc_c reports a codec overrun
+     * (BLOSC2_ERROR_WRITE_BUFFER, 1343-1356 and 1417-1420). */
+    if (HDR_EXT > destsize) { free(work); memset(dest, 0, HDR_EXT); return 0; }
     uint8_t *img = (uint8_t *)malloc((size_t)srcsize + 64);
     uint8_t *t1 = (uint8_t *)malloc((size_t)bs + 64), *t2 = (uint8_t *)malloc((size_t)bs + 64);
     if (!img || !t1 || !t2) { free(img); free(t1); free(t2); free(work); return -1; }
@@ -994,6 +999,12 @@ int or_compress_chunk(const or_cparams *cp, const void *src_, int32_t srcsize, v
       int32_t bsize = lo ? leftover : bs;
       const uint8_t *blk = pipe_forward(cp, ts, work, j * bs, bsize, t1, t2);
       if (!blk) { free(img); free(t1); free(t2); free(work); return ERR_FILTER; }
+      const int64_t at = (int64_t)HDR_EXT + (int64_t)j * bs;
+      if (at + bsize > destsize) {
+        free(img); free(t1); free(t2); free(work);
+        if (destsize - at <= 0) { memset(dest, 0, HDR_EXT); return 0; }
+        return ERR_WRITE;
+      }
       memcpy(img + (int64_t)j * bs, blk, (size_t)bsize);
     }
     free(t1); free(t2);

@@ -328,6 +328,48 @@ def test_lz4_dict_chunks_match_reference(clevel, filters):
         assert np.array_equal(back, raw), name
 
 
+def _ref_chunk(src, destsize, **kw):
+    from b2ctypes import cparams
+    R = ref()
+    ctx = R.blosc2_create_cctx(cparams(**kw))
+    raw = src.view(np.uint8).reshape(-1).copy()
+    out = np.zeros(raw.nbytes + (1 << 18), np.uint8)   # the training pass may store past destsize
+    n = R.blosc2_compress_ctx(ctx, p(raw), raw.nbytes, p(out), destsize)
+    R.blosc2_free_ctx(ctx)
+    return out[:n] if n > 0 else n
+
+
+def _oracle_chunk(src, destsize, **kw):
+    from oracle_lib import or_cparams
+    raw = src.view(np.uint8).reshape(-1)
+    out = np.zeros(max(destsize, raw.nbytes + 32) + 64, np.uint8)
+    n = oracle().or_compress_chunk(C.byref(or_cparams(**kw)), p(raw), raw.nbytes, p(out), destsize)
+    return out[:n] if n > 0 else n
+
+
+@needs_ref
+def test_lz4_dict_destsize_sweep():
+    """use_dict under tight destsizes: the training pass needs only the header to fit, gives the
+    chunk up (0) when a block finds no room at all, and reports BLOSC2_ERROR_WRITE_BUFFER when a
+    block finds some (blosc/blosc2.c:1343-1356, 1417-1420, 2940-2965, 3036-3052)."""
+    for src, ts in ((mixed_bytes(11, 40_000), 1), (gen_f32(3, 10_000), 4)):
+        for bs in (0, 64, 256, 4096):
+            for ds in list(range(28, 80, 3)) + [100, 300, 1000, 4128, 4129, 8000, 39999, 40031, 40032, 40033]:
+                kw = dict(clevel=5, typesize=ts, compcode=1, use_dict=1, blocksize=bs)
+                a, b = _oracle_chunk(src, ds, **kw), _ref_chunk(src, ds, **kw)
+                assert (a == b) if isinstance(b, int) else _bytes_equal(a, b), (ts, bs, ds, b)
+
+
+@needs_ref
+@pytest.mark.parametrize("filters,meta", [((0, 0, 0, 3, 1, 2), (0,) * 6), ((0, 0, 0, 4, 3, 1), (0, 0, 0, 16, 0, 0))])
+def test_lz4_dict_three_filters_vs_ref(filters, meta):
+    """Three filters rewrite the input during the training pass; the real pass filters it again."""
+    src = gen_f32(7, 300_000)
+    for clevel in (1, 5, 9):
+        kw = dict(clevel=clevel, typesize=4, filters=filters, filters_meta=meta, compcode=1, use_dict=1)
+        assert _bytes_equal(oracle_compress(src, **kw), ref_compress(src, **kw)), kw
+
+
 LZ4_KATS = ["blosc-lz4-3.0.0.cdata", "blosc-1.11.1-lz4.cdata", "blosc-1.14.0-lz4.cdata",
             "blosc-1.17.1-lz4-bitshuffle4-memcpy.cdata", "blosc-1.17.1-lz4-bitshuffle8-nomemcpy.cdata",
             "blosc-1.18.0-lz4-bitshuffle4-memcpy.cdata", "blosc-1.18.0-lz4-bitshuffle8-nomemcpy.cdata"]
