@@ -454,7 +454,11 @@ def run(args):
         t_c, t_d = head["t_c"], head["t_d"]
         lz_name = "fast" if modes[-1] == 1 else "exact"
         # the encoder kernel of the headline mode (rocprof names: k_encode_fast / k_encode)
-        dominant = ("k_encode_fast" if lz_name == "fast" else "k_encode") if enc >= dec else "k_decode"
+        # fast mode runs shuffle + encode + finalize + scatter as ONE launch, k_encode_fast_fused
+        # (B2H_FUSE, c-blosc2_amd/csrc/b2h_engine.hip); B2H_FUSE=0 restores the separate launches
+        fused = lz_name == "fast" and int(os.environ.get("B2H_FUSE", "19")) & 1
+        enc_name = ("k_encode_fast_fused" if fused else "k_encode_fast") if lz_name == "fast" else "k_encode"
+        dominant = enc_name if enc >= dec else "k_decode"
         kms = enc if enc >= dec else dec
         achieved = (N + Cb) / (kms * 1e-3) / 1e9     # algorithmic bytes of one launch: N + C
         traffic, traffic_src, traffic_corr = pmc_traffic(dominant, workload + f" [{lz_name}]")

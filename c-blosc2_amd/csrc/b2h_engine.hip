@@ -22,6 +22,7 @@
 #include <mutex>
 #include <type_traits>
 #include <vector>
+#include <unistd.h>
 
 #include "b2h_engine.h"
 #include "b2h_filters.h"
@@ -80,7 +81,7 @@ struct Scratch {
 };
 
 struct Workspace {
-  Scratch t1, t2, work, sbuf, res, place, mode, qctr, gtab, porder;    // compress
+  Scratch t1, t2, work, sbuf, res, place, mode, qctr, gtab, porder, fsync;    // compress
   bool porder_init = false;
   Scratch dchunks, dstreams, dblocks, dtotals, stage, stage2, ptrs, dqctr, ddbg, dorder, dbcnt;  // decompress
   std::mutex mu;
@@ -100,7 +101,7 @@ struct Workspace {
   }
   void free_all() {
     if (used && done) (void)hipEventSynchronize(done);
-    for (Scratch* s : {&t1, &t2, &work, &sbuf, &res, &place, &mode, &qctr, &gtab, &porder, &dchunks, &dstreams,
+    for (Scratch* s : {&t1, &t2, &work, &sbuf, &res, &place, &mode, &qctr, &gtab, &porder, &fsync, &dchunks, &dstreams,
                        &dblocks, &dtotals, &stage, &stage2, &ptrs, &dqctr, &ddbg, &dorder, &dbcnt})
       s->release();
     if (done) (void)hipEventDestroy(done);
@@ -1038,14 +1039,12 @@ struct Place {
 
 // Serial reference bookkeeping per chunk (blosc/blosc2.c:1277-1466, 2161-2228, 3004-3107).
 // mode: 0 compressed, 1 memcpy fallback, 2 special zero, 3 does not fit.
-__global__ void k_finalize(CGeom g, const StreamResult* __restrict__ res, Place* __restrict__ place,
-                           int32_t* __restrict__ mode, uint8_t* __restrict__ dst, int32_t* __restrict__ cbytes,
-                           int32_t nchunks, const uint8_t* __restrict__ header_template) {
-  const int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= nchunks) return;
-  uint8_t* d = dst + (int64_t)c * g.dst_stride;
-  const StreamResult* r = res + (int64_t)c * g.nsc;
-  Place* pl = place + (int64_t)c * g.nsc;
+// One lane: `ld(l)` gives stream l's StreamResult (kind, size, peak), `put(l, off, csize)` takes its
+// placement; writes the header and bstarts of chunk output `d`; returns the mode, *cb_out = cbytes.
+template <typename LD, typename PUT>
+__device__ __forceinline__ int32_t finalize_chunk(const CGeom& g, uint8_t* __restrict__ d,
+                                                  const uint8_t* __restrict__ header_template, LD ld, PUT put,
+                                                  int32_t* cb_out) {
   const int32_t ovh = g.overhead;
   int32_t ntbytes = ovh + 4 * g.nblocks + (g.dict_size ? 4 + g.dict_size : 0);
   const int32_t destsize = g.destsize;
@@ -1059,12 +1058,11 @@ __global__ void k_finalize(CGeom g, const StreamResult* __restrict__ res, Place*
     uint8_t* bs = d + ovh + 4 * b;
     bs[0] = (uint8_t)bstart; bs[1] = (uint8_t)(bstart >> 8); bs[2] = (uint8_t)(bstart >> 16); bs[3] = (uint8_t)(bstart >> 24);
     for (int32_t j = 0; j < ns; j++, l++) {
-      const StreamResult sr = r[l];
+      const StreamResult sr = ld(l);
       ntbytes += 4;
       if (sr.kind == kStreamZeroRun || sr.kind == kStreamByteRun) {
         if (ntbytes > destsize) { ok = false; break; }
-        pl[l].off = ntbytes;
-        pl[l].csize = -sr.size;
+        put(l, ntbytes, -sr.size);
         if (sr.size) {
           all_zero = false;
           ntbytes += 1;
@@ -1083,8 +1081,7 @@ __global__ void k_finalize(CGeom g, const StreamResult* __restrict__ res, Place*
       int32_t cb = (sr.kind == kStreamLz && (g.compcode == 1 || maxout >= 66) && sr.peak <= maxout) ? sr.size : 0;
       if (cb == 0) cb = nl;
       if (cb == nl && ntbytes + nl > destsize) { ok = false; break; }
-      pl[l].off = ntbytes;
-      pl[l].csize = cb;   // == nl means raw copy
+      put(l, ntbytes, cb);   // cb == nl means raw copy
       ntbytes += cb;
     }
   }
@@ -1110,7 +1107,21 @@ __global__ void k_finalize(CGeom g, const StreamResult* __restrict__ res, Place*
     cb = 0;
   }
   d[12] = (uint8_t)cb; d[13] = (uint8_t)(cb >> 8); d[14] = (uint8_t)(cb >> 16); d[15] = (uint8_t)(cb >> 24);
-  mode[c] = m;
+  *cb_out = cb;
+  return m;
+}
+
+__global__ void k_finalize(CGeom g, const StreamResult* __restrict__ res, Place* __restrict__ place,
+                           int32_t* __restrict__ mode, uint8_t* __restrict__ dst, int32_t* __restrict__ cbytes,
+                           int32_t nchunks, const uint8_t* __restrict__ header_template) {
+  const int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nchunks) return;
+  const StreamResult* r = res + (int64_t)c * g.nsc;
+  Place* pl = place + (int64_t)c * g.nsc;
+  int32_t cb = 0;
+  mode[c] = finalize_chunk(
+      g, dst + (int64_t)c * g.dst_stride, header_template, [&](int32_t l) { return r[l]; },
+      [&](int32_t l, int32_t off, int32_t csize) { pl[l].off = off; pl[l].csize = csize; }, &cb);
   cbytes[c] = cb;
 }
 
@@ -1183,6 +1194,395 @@ __global__ void k_memcpy_chunks(const uint8_t* __restrict__ src, int64_t src_str
   if (!fits) return;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nbytes; i += (int64_t)gridDim.x * blockDim.x)
     d[overhead + i] = s[i];
+}
+
+// ------------------------------------- fast mode, one launch: shuffle -> encode -> finalize/scatter ----
+// k_encode_fast with the passes on either side of it moved inside the launch, so that their HBM
+// traffic runs in the shadow of the latency-bound encoder instead of as launches of their own:
+//   * SHUFFLE jobs (f.raw != null; the lone filter is a typesize-4 byte shuffle, whole 64-byte
+//     groups): before encoding a stream the workgroup makes sure every block up to the stream's own
+//     + f.lead has been claimed (one atomic counter, blocks in chunk-major order), shuffles the
+//     blocks it claimed, then waits for its stream's block;
+//   * FINALIZE: the workgroup whose stream completes a chunk (per-chunk counter) runs the serial
+//     layout bookkeeping of k_finalize for it and publishes the chunk in a ready list;
+//   * SCATTER items (one per stream of a published chunk): claimed between streams while
+//     available, and by every workgroup once the stream queue is empty (k_scatter's work).
+// Hand-offs follow MI355X_MICROARCH.md § inter-workgroup visibility: every handed-off byte is stored
+// write-through (sc1: the shuffled planes, the encoder's ring flushes, the placement words), each
+// storing wave drains (vmcnt 0) before the workgroup barrier behind which one lane signals with an
+// agent-scope atomic; consumers poll relaxed; the encoder reads its block with plain loads behind an
+// agent acquire, the scatter reads its payload with sc1 loads.  Every wait is bounded (1 s; a
+// timeout sets sync[4], reported as E_FAILURE by the host at its next synchronisation).
+struct EncFuse {
+  const uint8_t* raw;      // SHUFFLE source (null: `filt` is already filtered)
+  int64_t raw_stride;
+  uint8_t* filt;           // shuffle output = the encoder's input, stride g.wstride
+  int32_t* sync;           // zeroed per launch: kFuseHdr words, blk_ready[nblk], chunk_cnt[nchunks], ready[nchunks]
+  int32_t* fin;            // per stream: kind, size, peak (sc1)
+  Place* place;
+  int32_t* mode;
+  uint8_t* dst;
+  int32_t* cbytes;
+  const uint8_t* htpl;
+  int32_t nchunks, lead;
+  int32_t* trace;          // debug (B2H_FUSE_TRACE): per workgroup, the phase it is in (host memory)
+  int32_t mode_bits;       // 1: finalize + scatter fused, 2: shuffle fused
+};
+constexpr int32_t kFuseHdr = 16;   // [0] shuffle claims [1] scatter claims [2] ready slots [3] published items [4] timeouts
+constexpr int32_t kFuseSpi = 8;    // streams per scatter item
+
+typedef B2H_GLB int32_t* gi32_t;
+__device__ __forceinline__ void st_agent(int32_t* p, int32_t v) {
+  __hip_atomic_store((gi32_t)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int32_t add_agent(int32_t* p, int32_t v) {
+  return __hip_atomic_fetch_add((gi32_t)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// counters and flags are read with an atomic read-modify-write (performed where the atomics are),
+// never with a load that a cache might serve
+__device__ __forceinline__ int32_t rd_agent(int32_t* p) { return add_agent(p, 0); }
+// one lane: poll *p until non-zero, bounded (~1 s or 2^21 polls); 0 on timeout (flagged in *tmo)
+__device__ int32_t wait_nonzero(int32_t* p, int32_t* tmo) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (int32_t it = 0; it < (1 << 21); it++) {
+    const int32_t v = rd_agent(p);
+    if (v) return v;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) break;   // 100 MHz clock
+    __builtin_amdgcn_s_sleep(8);
+  }
+  st_agent(tmo, 1);
+  return 0;
+}
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+#define FUSE_TRACE(code, v)                                                                                  \
+  do {                                                                                                     \
+    if (f.trace && threadIdx.x == 0)                                                                        \
+      __hip_atomic_store(f.trace + blockIdx.x, (int32_t)((code) | ((v) << 4)), __ATOMIC_RELAXED,            \
+                         __HIP_MEMORY_SCOPE_SYSTEM);                                                        \
+  } while (0)
+
+// Typesize-4 byte shuffle of one block by the workgroup (bsize % 64 == 0, s and d 16-aligned):
+// 16 elements per lane step, 4 x 16 B loads, a 4x4 byte transpose per 4 elements (v_perm), one
+// 16 B write-through store per plane.
+__device__ __forceinline__ void tr4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t (&o)[4]) {
+  const uint32_t t0 = __builtin_amdgcn_perm(b, a, 0x06020400u), t1 = __builtin_amdgcn_perm(b, a, 0x07030501u);
+  const uint32_t t2 = __builtin_amdgcn_perm(d, c, 0x06020400u), t3 = __builtin_amdgcn_perm(d, c, 0x07030501u);
+  o[0] = __builtin_amdgcn_perm(t2, t0, 0x05040100u);
+  o[2] = __builtin_amdgcn_perm(t2, t0, 0x07060302u);
+  o[1] = __builtin_amdgcn_perm(t3, t1, 0x05040100u);
+  o[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
+}
+__device__ void shuffle4_block_wt(const uint8_t* __restrict__ s, uint8_t* __restrict__ d, int32_t bsize) {
+  const int32_t n = bsize / 4, groups = n / 16;
+  const __amdgpu_buffer_rsrc_t r = wt_rsrc((gout_t)d);
+  const uint4* s4 = reinterpret_cast<const uint4*>(s);
+  constexpr int U = 2;
+  for (int32_t g0 = threadIdx.x; g0 < groups; g0 += U * blockDim.x) {
+    uint4 w[U][4];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int32_t gi = g0 + u * blockDim.x;
+#pragma unroll
+      for (int k = 0; k < 4; k++) w[u][k] = gi < groups ? s4[4 * gi + k] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int32_t gi = g0 + u * blockDim.x;
+      if (gi >= groups) break;
+      uint32_t o[4][4];   // [element quad k][plane]
+#pragma unroll
+      for (int k = 0; k < 4; k++) tr4(w[u][k].x, w[u][k].y, w[u][k].z, w[u][k].w, o[k]);
+#pragma unroll
+      for (int p = 0; p < 4; p++) {
+        const u32x4 v = {o[0][p], o[1][p], o[2][p], o[3][p]};
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, p * n + 16 * gi, 0, 16);
+      }
+    }
+  }
+}
+
+template <typename POS>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4, 8)))   // as k_encode_fast
+void k_encode_fast_fused(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
+                         StreamResult* __restrict__ res, int32_t nstreams_total, int32_t* __restrict__ next, int tablog,
+                         const int32_t* __restrict__ porder, EncFuse f) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  B2H_LDS uint8_t* tab = (B2H_LDS uint8_t*)smem;
+  B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + (sizeof(POS) << tablog));
+  B2H_LDS FastShared* sh = (B2H_LDS FastShared*)(smem + (sizeof(POS) << tablog) + kOutRing);
+  const bool matcher = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
+  const int32_t nblk = f.nchunks * g.nblocks;
+  int32_t* blk_ready = f.sync + kFuseHdr;
+  int32_t* chunk_cnt = blk_ready + nblk;
+  int32_t* ready = chunk_cnt + f.nchunks;
+  int32_t* tmo = f.sync + 4;
+  // lane 0 of the workgroup computes v, everyone gets it
+  auto bcast = [&](int32_t v) -> int32_t {
+    if (threadIdx.x == 0) sh->bcast = v;
+    __syncthreads();
+    const int32_t r = __builtin_amdgcn_readfirstlane(sh->bcast);
+    __syncthreads();
+    return r;
+  };
+  // scatter item k: streams [j0, j0 + kFuseSpi) of the chunk in ready slot k / ipc (the publish
+  // poll, ONE agent acquire for the item, then plain loads of the placements and payloads)
+  const int32_t ipc = (g.nsc + kFuseSpi - 1) / kFuseSpi;   // items per chunk
+  const int32_t nitems = f.nchunks * ipc;
+  auto scatter_item = [&](int32_t k) {
+    const int32_t slot = k / ipc, j0 = (k - slot * ipc) * kFuseSpi;
+    int32_t v = 0;
+    FUSE_TRACE(1, k);
+    if (threadIdx.x == 0) {
+      v = wait_nonzero(ready + slot, tmo);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      drain_stores();
+    }
+    v = bcast(v);
+    if (v <= 0) return;
+    const int32_t c = v - 1;
+    if (__builtin_amdgcn_readfirstlane(f.mode[c]) != 0) return;
+    uint8_t* d = f.dst + (int64_t)c * g.dst_stride;
+    const int32_t wv = threadIdx.x >> 6;
+    for (int32_t l = j0; l < min(j0 + kFuseSpi, g.nsc); l++) {
+      const int32_t s = c * g.nsc + l;
+      Place pl;
+      pl.off = __builtin_amdgcn_readfirstlane(f.place[s].off);
+      pl.csize = __builtin_amdgcn_readfirstlane(f.place[s].csize);
+      int32_t off, len, blk;
+      stream_locate(g, l, &off, &len, &blk);
+      if (threadIdx.x == 0) {
+        const uint32_t w = (uint32_t)pl.csize;
+        uint8_t* q = d + pl.off - 4;
+        q[0] = (uint8_t)w; q[1] = (uint8_t)(w >> 8); q[2] = (uint8_t)(w >> 16); q[3] = (uint8_t)(w >> 24);
+        if (pl.csize < 0) d[pl.off] = 0x1;   // run-length token
+      }
+      if (pl.csize <= 0) continue;
+      const uint8_t* src = (pl.csize == len ? filt : sbuf) + (int64_t)c * g.wstride + off;
+      const int32_t q = ((pl.csize + 1) / 2 + 15) & ~15;
+      const int32_t a = min(pl.csize, wv * q), b = min(pl.csize, a + q);
+      if (b > a) {
+        if (f.mode_bits & 32) wave_copy<false, true>((gout_t)(d + pl.off + a), (gin_t)(src + a), b - a);
+        else wave_copy((gout_t)(d + pl.off + a), (gin_t)(src + a), b - a);
+      }
+    }
+  };
+  // published scatter items, claimed with a CAS (never past the published count), a few tries.
+  // Every loop below that holds a barrier is `while (uniform)` with its broadcast last in the body:
+  // a `break` after lane-0-only code lets the compiler structurize the loop as divergent, and its
+  // waves then meet different barriers (seen: a workgroup re-shuffling one block forever).
+  auto try_claim_item = [&]() -> int32_t {   // lane 0
+    const int32_t pub = rd_agent(f.sync + 3);
+    int32_t cur = rd_agent(f.sync + 1);
+    for (int tries = 0; tries < 8 && cur < pub; tries++) {
+      const int32_t want = cur;
+      if (__hip_atomic_compare_exchange_strong((gi32_t)(f.sync + 1), &cur, want + 1, __ATOMIC_RELAXED,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        return want;
+    }
+    return -1;
+  };
+  auto scatter_available = [&](int max_items) {
+    int32_t k = bcast(threadIdx.x == 0 ? try_claim_item() : 0);
+    int it = 1;
+    while (k >= 0) {
+      scatter_item(k);
+      k = it < max_items ? bcast(threadIdx.x == 0 ? try_claim_item() : 0) : -1;
+      it++;
+    }
+  };
+  // lane 0: claim the next block to shuffle while the claims are behind `target`, else -1
+  auto claim_block = [&](int32_t target) -> int32_t {
+    return rd_agent(f.sync) < target ? add_agent(f.sync, 1) : -1;
+  };
+  int32_t i = bcast(threadIdx.x == 0 ? atomicAdd(next, 1) : 0);
+  while (i < nstreams_total) {
+    FUSE_TRACE(3, i);
+    const int32_t s = __builtin_amdgcn_readfirstlane(pull_to_stream(g, porder, g.front, i, nstreams_total));
+    const int32_t c = s / g.nsc, l = s - c * g.nsc;
+    int32_t off, len, blk;
+    stream_locate(g, l, &off, &len, &blk);
+    if (f.raw) {
+      const int32_t gb = c * g.nblocks + blk, target = min(gb + 1 + f.lead, nblk);
+      int32_t k = bcast(threadIdx.x == 0 ? claim_block(target) : -1);
+      while (k >= 0 && k < nblk) {   // keep the shuffle claims ahead of the streams
+        FUSE_TRACE(4, k);
+        const int32_t cc = k / g.nblocks, b = k - cc * g.nblocks;
+        const int32_t bsize = (b == g.nblocks - 1 && g.leftover) ? g.leftover : g.bs;
+        shuffle4_block_wt(f.raw + (int64_t)cc * f.raw_stride + (int64_t)b * g.bs,
+                          f.filt + (int64_t)cc * g.wstride + (int64_t)b * g.bs, bsize);
+        drain_stores();
+        __syncthreads();
+        int32_t nk = -1;
+        if (threadIdx.x == 0) {
+          st_agent(blk_ready + k, 1);
+          nk = claim_block(target);
+        }
+        k = bcast(nk);
+      }
+      FUSE_TRACE(5, gb);
+      if (threadIdx.x == 0) {
+        (void)wait_nonzero(blk_ready + gb, tmo);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        drain_stores();
+      }
+      __syncthreads();
+    }
+    gin_t in = (gin_t)(filt + (int64_t)c * g.wstride + off);
+    gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
+    FUSE_TRACE(6, s);
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+    StreamResult r = encode_stream_fast<POS, true>(in, len, g.clevel, out, tab, tablog, oring, sh,
+                                                   g.overhead == kHdrExt, matcher);
+    r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
+    r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
+    if (!matcher && lane_id() == 0) {
+      res[s] = r;
+      st_agent(f.fin + 3 * s, r.kind);
+      st_agent(f.fin + 3 * s + 1, r.size);
+      st_agent(f.fin + 3 * s + 2, r.peak);
+    }
+    FUSE_TRACE(7, s);
+    drain_stores();
+    __syncthreads();
+    const int32_t done = bcast(threadIdx.x == 0 ? add_agent(chunk_cnt + c, 1) : 0);
+    if (done == g.nsc - 1) {   // last stream of chunk c: finalize it (its stream results -> LDS)
+      B2H_LDS int32_t* fl = (B2H_LDS int32_t*)tab;
+      FUSE_TRACE(8, c);
+      if (threadIdx.x == 0) {   // the counter add returned: ONE acquire, then plain loads
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        drain_stores();
+      }
+      __syncthreads();
+      for (int32_t j = threadIdx.x; j < 3 * g.nsc; j += blockDim.x) fl[j] = f.fin[3 * c * g.nsc + j];
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        Place* pl = f.place + (int64_t)c * g.nsc;
+        int32_t cb = 0;
+        const int32_t m = finalize_chunk(
+            g, f.dst + (int64_t)c * g.dst_stride, f.htpl,
+            [&](int32_t j) {
+              StreamResult x;
+              x.kind = fl[3 * j];
+              x.size = fl[3 * j + 1];
+              x.peak = fl[3 * j + 2];
+              return x;
+            },
+            [&](int32_t j, int32_t o, int32_t cs) { st_agent(&pl[j].off, o); st_agent(&pl[j].csize, cs); }, &cb);
+        st_agent(f.mode + c, m);
+        f.cbytes[c] = cb;
+        drain_stores();
+        const int32_t slot = add_agent(f.sync + 2, 1);
+        st_agent(ready + slot, c + 1);
+        drain_stores();
+        add_agent(f.sync + 3, ipc);
+      }
+      __syncthreads();
+    }
+    FUSE_TRACE(2, 0);
+    if (!(f.mode_bits & 16)) scatter_available(2);
+    i = bcast(threadIdx.x == 0 ? atomicAdd(next, 1) : 0);
+  }
+  // stream queue empty: every remaining scatter item
+  FUSE_TRACE(9, 0);
+  int32_t k = bcast(threadIdx.x == 0 ? add_agent(f.sync + 1, 1) : 0);
+  while (k < nitems) {
+    scatter_item(k);
+    k = bcast(threadIdx.x == 0 ? add_agent(f.sync + 1, 1) : 0);
+  }
+  FUSE_TRACE(15, 0);
+}
+
+
+// A timed-out hand-off wait inside k_encode_fast_fused fails every chunk of the batch.
+__global__ void k_fuse_check(const int32_t* __restrict__ sync, int32_t* __restrict__ cbytes, int32_t nchunks) {
+  const int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < nchunks && sync[4]) cbytes[c] = E_FAILURE;
+}
+
+// B2H_FUSE (A/B runs, tests): 0 separate launches; bit 1 finalize + scatter inside the encode launch,
+// bit 2 + the byte shuffle, bit 16 scatter items only once the stream queue is empty, bit 32
+// non-temporal scatter copies.  Default 19.  Measured on T (tools/fuse_prof.py, profiles/r2_v5_*):
+// separate 1.54 + 16.55 + 1.10 ms; 19: 17.79 ms; scatter items claimed between streams (3) slow
+// the concurrent encoders' short planes ~2x (22.5 ms), with non-temporal copies too (35).
+static int fuse_bits() {
+  const char* e = getenv("B2H_FUSE");
+  return e ? atoi(e) : 19;
+}
+static bool fuse_enabled() { return (fuse_bits() & 1) != 0; }
+static int fuse_lead() {
+  static const int v = [] { const char* e = getenv("B2H_SHUF_LEAD"); return e ? std::max(1, atoi(e)) : 512; }();
+  return v;
+}
+
+// Sync words + per-stream results of the fused launch (f.raw / f.filt set by the caller).
+template <typename POS>
+static int launch_encode_fast_fused_t(Workspace* ws, const CGeom& g, const uint8_t* filt, StreamResult* res,
+                                      int64_t ntot, int32_t* next, const int32_t* porder, EncFuse f, hipStream_t st) {
+  const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
+  const int tablog = std::min(fast_tablog(), hashlog);
+  const size_t lds = fast_lds(sizeof(POS), tablog);
+  const void* fn = reinterpret_cast<const void*>(&k_encode_fast_fused<POS>);
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  const int slots = resident_slots(fn, lds, 128);
+  const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(ntot, slots));
+  const size_t sync_words = kFuseHdr + (size_t)f.nchunks * g.nblocks + 2 * (size_t)f.nchunks;
+  const size_t sync_bytes = (sync_words * 4 + 15) & ~size_t(15);
+  if (ws->fsync.ensure(sync_bytes + 12 * (size_t)ntot)) return E_MEMORY;
+  f.sync = ws->fsync.as<int32_t>();
+  f.fin = reinterpret_cast<int32_t*>(ws->fsync.as<uint8_t>() + sync_bytes);
+  f.lead = fuse_lead();
+  f.mode_bits = fuse_bits();
+  HIPCHK(hipMemsetAsync(f.sync, 0, sync_bytes, st));
+  static int32_t* trace = nullptr;
+  static const bool tr = getenv("B2H_FUSE_TRACE") != nullptr;
+  if (tr && !trace) HIPCHK(hipHostMalloc(&trace, 4 << 20, hipHostMallocCoherent));
+  f.trace = tr ? trace : nullptr;
+  if (tr) memset(trace, 0xff, 4 * (size_t)grid);
+  k_encode_fast_fused<POS><<<grid, 128, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog,
+                                                   porder, f);
+  HIPCHK(hipGetLastError());
+  if (tr) {   // debug watchdog: report where the workgroups are if the launch has not ended after 5 s
+    for (int ms = 0; ms < 5000 && hipStreamQuery(st) == hipErrorNotReady; ms++) usleep(1000);
+    if (hipStreamQuery(st) == hipErrorNotReady) {
+      int hist[16][2] = {};
+      for (uint32_t b = 0; b < grid; b++) {
+        const int32_t v = __atomic_load_n(trace + b, __ATOMIC_RELAXED);
+        if (v == -1) continue;
+        hist[v & 15][0]++;
+        hist[v & 15][1] = v >> 4;
+      }
+      fprintf(stderr, "k_encode_fast_fused stuck after 5 s (grid %u, ntot %lld):\n", grid, (long long)ntot);
+      for (int k = 0; k < 16; k++)
+        if (hist[k][0]) fprintf(stderr, "  phase %d: %d workgroups (e.g. value %d)\n", k, hist[k][0], hist[k][1]);
+      fflush(stderr);
+      abort();
+    }
+  }
+  k_fuse_check<<<(f.nchunks + 255) / 256, 256, 0, st>>>(f.sync, f.cbytes, f.nchunks);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// The fused launch applies to BloscLZ fast mode without a dictionary when the chunk's stream
+// results fit the LDS table (the finalizing workgroup stages them there).
+static bool fused_encode_ok(const CGeom& g) {
+  if (!fuse_enabled() || lz_mode() != 1 || g.compcode != 0 || g.dict_size) return false;
+  const bool small = std::max(g.neblock, g.leftover) <= 65536;
+  const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
+  const int tablog = std::min(fast_tablog(), hashlog);
+  return (size_t)12 * g.nsc <= ((small ? 2u : 4u) << tablog);
+}
+static int launch_encode_fast_fused(Workspace* ws, const CGeom& g, const uint8_t* filt, StreamResult* res,
+                                    int64_t ntot, int32_t* next, const int32_t* porder, const EncFuse& f,
+                                    hipStream_t st) {
+  if (std::max(g.neblock, g.leftover) <= 65536)
+    return launch_encode_fast_fused_t<uint16_t>(ws, g, filt, res, ntot, next, porder, f, st);
+  return launch_encode_fast_fused_t<uint32_t>(ws, g, filt, res, ntot, next, porder, f, st);
 }
 
 // ============================================================ compression: host driver ====
@@ -1393,7 +1793,7 @@ static CGeom make_geom(const CompressPlan& P, int64_t src_stride, int64_t dst_st
 
 static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const uint8_t* filt, const uint8_t* raw,
                         int64_t raw_stride, uint8_t* d_dst, int64_t dst_stride, int32_t* d_cbytes, int32_t nchunks,
-                        const uint8_t* htpl, int64_t ntot, hipStream_t st);
+                        const uint8_t* htpl, int64_t ntot, hipStream_t st, const uint8_t* fuse_raw = nullptr);
 
 int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stride, int32_t nchunks, uint8_t* d_dst,
                    int64_t dst_stride, int32_t* d_cbytes, hipStream_t st, Workspace* wsx) {
@@ -1516,7 +1916,18 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
     }
     return 0;
   };
-  if ((rc = run_filters())) return rc;
+  // the lone typesize-4 byte shuffle of a fast-mode batch runs inside the encode launch
+  const uint8_t meta0 = nact == 1 ? P.filters_meta[act[0]] : 0;
+  const bool fuse_shuffle = nact == 1 && P.filters[act[0]] == kShuffle && (meta0 == 0 || meta0 == 4) && g.ts == 4 &&
+                            g.bs % 64 == 0 && g.leftover % 64 == 0 && !clobber && g.dict_size == 0 &&
+                            (reinterpret_cast<uintptr_t>(raw) & 15) == 0 && raw_stride % 16 == 0 &&
+                            (fuse_bits() & 2) && fused_encode_ok(g);
+  if (fuse_shuffle) {
+    filt = ring[0];
+    filt_stride = g.wstride;
+  } else if ((rc = run_filters())) {
+    return rc;
+  }
   if (nact > 0 && filt_stride != g.wstride) return E_FAILURE;
   // encoder reads the filtered streams at c*wstride: if no filter ran, stage the input there
   if (nact == 0) {
@@ -1535,14 +1946,15 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
   }
   ev_filter.stop(st);
   HIPCHK(hipGetLastError());
-  return encode_stage(ws, P, g, filt, raw, raw_stride, d_dst, dst_stride, d_cbytes, nchunks, htpl, ntot, st);
+  return encode_stage(ws, P, g, filt, raw, raw_stride, d_dst, dst_stride, d_cbytes, nchunks, htpl, ntot, st,
+                      fuse_shuffle ? raw : nullptr);
 }
 
 // The codec stage of a batch whose filtered images sit at filt + c * g.wstride: encode every stream,
 // then the serial-layout finalisation, the payload scatter and the memcpy fallbacks (from raw).
 static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const uint8_t* filt, const uint8_t* raw,
                         int64_t raw_stride, uint8_t* d_dst, int64_t dst_stride, int32_t* d_cbytes, int32_t nchunks,
-                        const uint8_t* htpl, int64_t ntot, hipStream_t st) {
+                        const uint8_t* htpl, int64_t ntot, hipStream_t st, const uint8_t* fuse_raw) {
   const int32_t n = P.nbytes;
   int rc = 0;
   // encode
@@ -1550,6 +1962,8 @@ static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const ui
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
   const bool small = std::max(g.neblock, g.leftover) <= 65536;
   StreamResult* res = ws->res.as<StreamResult>();
+  const bool fused = fused_encode_ok(g);   // finalize + scatter (and fuse_raw's shuffle) inside the encode launch
+  if (fuse_raw && !fused) return E_FAILURE;
   rc = ws->qctr.ensure(16);
   if (rc) return rc;
   int32_t* next = ws->qctr.as<int32_t>();
@@ -1566,7 +1980,19 @@ static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const ui
       HIPCHK(hipMemsetAsync(porder, 0, 32 * sizeof(int32_t), st));
       ws->porder_init = true;
     }
-    if (lz_mode() == 1) rc = launch_encode_fast(ws, g, filt, res, ntot, next, porder, st);
+    if (fused) {
+      EncFuse f{};
+      f.raw = fuse_raw;
+      f.raw_stride = raw_stride;
+      f.filt = const_cast<uint8_t*>(filt);
+      f.place = ws->place.as<Place>();
+      f.mode = ws->mode.as<int32_t>();
+      f.dst = d_dst;
+      f.cbytes = d_cbytes;
+      f.htpl = htpl;
+      f.nchunks = nchunks;
+      rc = launch_encode_fast_fused(ws, g, filt, res, ntot, next, porder, f, st);
+    } else if (lz_mode() == 1) rc = launch_encode_fast(ws, g, filt, res, ntot, next, porder, st);
     else rc = small ? launch_encode<uint16_t>(ws, g, hashlog, filt, res, ntot, next, porder, st)
                     : launch_encode<uint32_t>(ws, g, hashlog, filt, res, ntot, next, porder, st);
     if (rc) return rc;
@@ -1578,8 +2004,11 @@ static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const ui
   ev_final.start(st);
   Place* place = ws->place.as<Place>();
   int32_t* mode = ws->mode.as<int32_t>();
-  k_finalize<<<(nchunks + 63) / 64, 64, 0, st>>>(g, res, place, mode, d_dst, d_cbytes, nchunks, htpl);
-  k_scatter<<<(uint32_t)ntot, kBlockThreads, 0, st>>>(g, place, mode, res, filt, ws->sbuf.as<uint8_t>(), d_dst, (int32_t)ntot);
+  if (!fused) {
+    k_finalize<<<(nchunks + 63) / 64, 64, 0, st>>>(g, res, place, mode, d_dst, d_cbytes, nchunks, htpl);
+    k_scatter<<<(uint32_t)ntot, kBlockThreads, 0, st>>>(g, place, mode, res, filt, ws->sbuf.as<uint8_t>(), d_dst,
+                                                        (int32_t)ntot);
+  }
   {
     dim3 grid(std::max(1, std::min(64, n / (256 * 16) + 1)), nchunks);
     k_memcpy_chunks<<<grid, 256, 0, st>>>(raw, raw_stride, d_dst, dst_stride, n, mode, htpl, d_cbytes,

@@ -740,7 +740,9 @@ __device__ __forceinline__ void wave_fill(gout_t o, uint8_t v, int32_t n) {
 // dst any alignment: 16-byte aligned stores of 16 funnel-shifted source bytes per lane, four
 // 1 KiB rows in flight per step (the source is read with aligned dwords: never past the last
 // dword that holds a source byte).
-template <bool WT = false>
+// NT: non-temporal loads and stores (a copy running beside latency-bound kernels: keeps their L2
+// lines)
+template <bool WT = false, bool NT = false>
 __device__ __forceinline__ void wave_copy(gout_t o, gin_t s, int32_t n) {
   const int lane = lane_id();
   const __amdgpu_buffer_rsrc_t r = wt_rsrc(o);
@@ -759,8 +761,8 @@ __device__ __forceinline__ void wave_copy(gout_t o, gin_t s, int32_t n) {
     for (int u = 0; u < 4; u++) {
       const B2H_GLB uint32_t* q = q0 + 4 * (i + 64 * u);
 #pragma unroll
-      for (int k = 0; k < 4; k++) w[u][k] = q[k];
-      w[u][4] = sh ? q[4] : 0u;
+      for (int k = 0; k < 4; k++) w[u][k] = NT ? __builtin_nontemporal_load(q + k) : q[k];
+      w[u][4] = sh ? (NT ? __builtin_nontemporal_load(q + 4) : q[4]) : 0u;
     }
 #pragma unroll
     for (int u = 0; u < 4; u++) {
@@ -769,7 +771,8 @@ __device__ __forceinline__ void wave_copy(gout_t o, gin_t s, int32_t n) {
       v.y = funnel(w[u][1], w[u][2], sh);
       v.z = funnel(w[u][2], w[u][3], sh);
       v.w = funnel(w[u][3], w[u][4], sh);
-      st16<WT>(o, r, h + 16 * (i + 64 * u), v);
+      if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<B2H_GLB u32x4*>(o + h + 16 * (i + 64 * u)));
+      else st16<WT>(o, r, h + 16 * (i + 64 * u), v);
     }
   }
   for (; i < n16; i += 64) {

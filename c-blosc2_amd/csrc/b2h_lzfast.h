@@ -76,6 +76,26 @@ __device__ __forceinline__ void rawc_load(gin_t p, RawCmp& r) {
 }
 __device__ __forceinline__ uint32_t rawc_word(const RawCmp& r, int i) { return funnel(r.d[i], r.d[i + 1], r.sh); }
 
+// Output ring -> global bytes [F, to) of `out` (one wave).  16-byte stores (the ring index of a
+// byte is its output offset mod kOutRing, so a 16-aligned output offset is a 16-aligned ring
+// offset when `out` is 16-aligned), bytes at the ends; WT: write-through (`sc1`) stores, for
+// streams another workgroup copies inside the same launch (k_encode_fast_fused).
+template <bool WT>
+__device__ __forceinline__ void ring_flush(gout_t out, const B2H_LDS uint8_t* oring, int32_t F, int32_t to) {
+  constexpr int32_t ORM = kOutRing - 1;
+  const int lane = lane_id();
+  const __amdgpu_buffer_rsrc_t r = wt_rsrc(out);
+  if ((reinterpret_cast<uintptr_t>(out) & 15) != 0 || to - F < 32) {
+    for (int32_t y = F + lane; y < to; y += 64) st8<WT>(out, r, y, oring[y & ORM]);
+    return;
+  }
+  const int32_t a = (F + 15) & ~15, b = to & ~15;
+  if (lane < a - F) st8<WT>(out, r, F + lane, oring[(F + lane) & ORM]);
+  if (lane < to - b) st8<WT>(out, r, b + lane, oring[(b + lane) & ORM]);
+  for (int32_t y = a + 16 * lane; y < b; y += 1024)
+    st16<WT>(out, r, y, *reinterpret_cast<const B2H_LDS u32x4*>(oring + (y & ORM)));
+}
+
 // ============================================================ matcher / parser workgroup ====
 // One stream per workgroup of two waves (k_encode_fast):
 //   wave 0, the MATCHER: tile exchanges, candidate loads and 60-byte compares -- for each lane of a
@@ -91,9 +111,10 @@ struct FastShared {          // per workgroup, after the table and the output ri
   int32_t ctrl[2];           // parser -> matcher: next tile, or -1 (stop); by iteration parity
   int32_t decide[2];         // the stream's probe decision / run verdict (parser -> both)
   int32_t pull;              // the stream index the workgroup pulled
+  int32_t bcast;             // k_encode_fast_fused: claims and hand-off words, lane 0 -> workgroup
 };
 
-template <bool PROBE, typename POS>
+template <bool PROBE, typename POS, bool WT>
 __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int probe_hashlog, int tablog, gout_t out,
                                                    int32_t maxout, B2H_LDS uint8_t* tab, B2H_LDS uint8_t* oring,
                                                    B2H_LDS FastShared* sh, int clevel, bool matcher) {
@@ -116,7 +137,7 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
   int32_t windows = 0;
   int32_t F = 0;   // parser: output [0, F) already in `out`
   auto flush = [&](int32_t to) {
-    for (int32_t y = F + lane; y < to; y += 64) out[y] = oring[y & ORM];
+    ring_flush<WT>(out, oring, F, to);
     F = to;
   };
   int32_t o = 5, lit = 4, pos = PROBE ? 0 : 4;
@@ -422,7 +443,7 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
       } else {
         flush(o);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) out[0] = (uint8_t)(byte0 | 0x20u);
+        if (lane == 0) st8<WT>(out, wt_rsrc(out), 0, (uint8_t)(byte0 | 0x20u));
       }
     }
   }
@@ -438,7 +459,7 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
 
 // Two-wave fast-mode stream encode: both waves run this; the parser's StreamResult is the one
 // to keep.  The run test is split between the waves; decisions travel through sh->decide.
-template <typename POS>
+template <typename POS, bool WT = false>
 __device__ __forceinline__ StreamResult encode_stream_fast(gin_t in, int32_t n, int clevel, gout_t out,
                                                             B2H_LDS uint8_t* tab, int tablog, B2H_LDS uint8_t* oring,
                                                             B2H_LDS FastShared* sh, bool allow_runs, bool matcher) {
@@ -468,7 +489,7 @@ __device__ __forceinline__ StreamResult encode_stream_fast(gin_t in, int32_t n, 
   if (clevel < 2) maxlen /= 8;
   else if (clevel < 4) maxlen /= 4;
   else if (clevel < 7) maxlen /= 2;
-  const LzPassOut pr = lz_pass_fast<true, POS>(in + (n - maxlen), maxlen, hashlog, tl, out, 0, tab, oring, sh, clevel,
+  const LzPassOut pr = lz_pass_fast<true, POS, WT>(in + (n - maxlen), maxlen, hashlog, tl, out, 0, tab, oring, sh, clevel,
                                                 matcher);
   res.windows = pr.windows;
   const double ratio = (double)pr.pos / (double)pr.o;
@@ -478,7 +499,7 @@ __device__ __forceinline__ StreamResult encode_stream_fast(gin_t in, int32_t n, 
   const bool go = sh->decide[0] != 0;
   __syncthreads();
   if (!go) return res;
-  const LzPassOut em = lz_pass_fast<false, POS>(in, n, hashlog, tl, out, n, tab, oring, sh, clevel, matcher);
+  const LzPassOut em = lz_pass_fast<false, POS, WT>(in, n, hashlog, tl, out, n, tab, oring, sh, clevel, matcher);
   res.windows += em.windows;
   if (em.fail) return res;
   res.kind = kStreamLz;

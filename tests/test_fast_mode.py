@@ -265,3 +265,42 @@ def test_gpu_fast_ratio_T(fast):
         sizes[mode] = int(cb.to(torch.int64).sum())
     L.b2h_set_blosclz_mode(1)
     assert sizes[1] <= sizes[0] * 1.001, sizes
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["T", "leftover", "clevel9_ts8"])
+def test_gpu_fused_launch_matches_separate_launches(fast, shape, monkeypatch):
+    """The one-launch fast-mode encode (byte shuffle, finalize and payload scatter inside the
+    encoder launch, k_encode_fast_fused) writes the same chunks as the separate launches
+    (B2H_FUSE=0; 19 is the default, 3 also claims scatter items between streams), on T's shape (4 MiB chunks: fused shuffle) and on shapes where only the
+    finalize/scatter is fused (a leftover block not of whole 64-byte groups, typesize 8)."""
+    import torch
+    B = fast
+    dev = torch.device("cuda")
+    if shape == "T":
+        chunk, n, kw = 4 << 20, 24, dict(clevel=5, typesize=4)
+    elif shape == "leftover":
+        chunk, n, kw = (1 << 20) + 4 * 37, 12, dict(clevel=5, typesize=4, blocksize=1 << 18)
+    else:
+        chunk, n, kw = 1 << 20, 12, dict(clevel=9, typesize=8)
+    src = torch.from_numpy(gen_f32(3, n * chunk // 4).view(np.uint8)).to(dev)
+    cap = chunk + 64
+    stride = (cap + 255) // 256 * 256
+    cp = B.cparams(**kw)
+    got = {}
+    for fuse in ("19", "3", "0"):
+        monkeypatch.setenv("B2H_FUSE", fuse)
+        comp = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
+        cb = torch.zeros(n, dtype=torch.int32, device=dev)
+        B.compress_batch(cp, src.data_ptr(), chunk, n, chunk, comp.data_ptr(), stride, cap, cb.data_ptr(), 0)
+        torch.cuda.synchronize()
+        cbh = cb.cpu().numpy()
+        assert (cbh > 0).all(), cbh
+        compb = comp.cpu().numpy().reshape(n, stride)
+        got[fuse] = [compb[i, :cbh[i]].copy() for i in range(n)]
+    for fz in ("19", "3"):
+        for a, b in zip(got[fz], got["0"]):
+            assert np.array_equal(a, b), fz
+    raw = src.cpu().numpy()
+    for i in range(0, n, 5):
+        assert np.array_equal(oracle_decompress(got["19"][i], chunk), raw[i * chunk:(i + 1) * chunk])
