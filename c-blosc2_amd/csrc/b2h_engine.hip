@@ -1226,7 +1226,7 @@ struct EncFuse {
   const uint8_t* htpl;
   int32_t nchunks, lead;
   int32_t* trace;          // debug (B2H_FUSE_TRACE): per workgroup, the phase it is in (host memory)
-  int32_t mode_bits;       // 1: finalize + scatter fused, 2: shuffle fused
+  int32_t mode_bits;       // fuse_bits()
 };
 constexpr int32_t kFuseHdr = 16;   // [0] shuffle claims [1] scatter claims [2] ready slots [3] published items [4] timeouts
 constexpr int32_t kFuseSpi = 8;    // streams per scatter item
@@ -1361,8 +1361,8 @@ void k_encode_fast_fused(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __r
       const int32_t q = ((pl.csize + 1) / 2 + 15) & ~15;
       const int32_t a = min(pl.csize, wv * q), b = min(pl.csize, a + q);
       if (b > a) {
-        if (f.mode_bits & 32) wave_copy<false, true>((gout_t)(d + pl.off + a), (gin_t)(src + a), b - a);
-        else wave_copy((gout_t)(d + pl.off + a), (gin_t)(src + a), b - a);
+        if ((f.mode_bits & 32) || !aligned16(src + a)) wave_copy((gout_t)(d + pl.off + a), (gin_t)(src + a), b - a);
+        else wave_copy_a16((gout_t)(d + pl.off + a), (gin_t)(src + a), b - a);
       }
     }
   };
@@ -2485,6 +2485,10 @@ __device__ __forceinline__ bool decode_stream(const uint8_t* const* __restrict__
 // issued before this row is transposed through the idle LDS ring (4 KiB) and leaves by 16-byte
 // stores, each instruction 1 KiB contiguous.  The n % 256 remainder and the bsize % 4 tail
 // take the per-quad and byte paths.
+#ifndef B2H_UNSHUF_DEPTH
+#define B2H_UNSHUF_DEPTH 2
+#endif
+constexpr int kUnshufDepth = B2H_UNSHUF_DEPTH;
 __device__ __forceinline__ void unshuffle4_wave_lds(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t bsize,
                                                     B2H_LDS uint8_t* lds) {
   const int lane = lane_id();
@@ -2494,24 +2498,30 @@ __device__ __forceinline__ void unshuffle4_wave_lds(const uint8_t* __restrict__ 
   } else {
     const int32_t rows = (n % 4 == 0) ? n / 1024 : 0;   // 1024 elements = 1 KiB per plane
     if (rows > 0) {
-      u32x4 v[4], v1[4];
+      // kUnshufDepth rows (4 KiB each) in flight: one wave is latency-bound on these loads
+      u32x4 v[kUnshufDepth][4];
 #pragma unroll
-      for (int p = 0; p < 4; p++) v[p] = *reinterpret_cast<const u32x4*>(src + (int64_t)p * n + 16 * lane);
-      if (rows > 1) {
+      for (int d = 0; d < kUnshufDepth; d++) {
+        if (d < rows) {
 #pragma unroll
-        for (int p = 0; p < 4; p++) v1[p] = *reinterpret_cast<const u32x4*>(src + (int64_t)p * n + 1024 + 16 * lane);
+          for (int p = 0; p < 4; p++) v[d][p] = *reinterpret_cast<const u32x4*>(src + (int64_t)p * n + d * 1024 + 16 * lane);
+        }
       }
 #pragma unroll 1
       for (int32_t r = 0; r < rows; r++) {
-        // this row into LDS, then the loads two rows ahead in flight while this one is transposed
+        // this row into LDS, then the loads kUnshufDepth rows ahead in flight while this one is transposed
 #pragma unroll
-        for (int p = 0; p < 4; p++) *reinterpret_cast<B2H_LDS u32x4*>(lds + p * 1024 + 16 * lane) = v[p];
+        for (int p = 0; p < 4; p++) *reinterpret_cast<B2H_LDS u32x4*>(lds + p * 1024 + 16 * lane) = v[0][p];
 #pragma unroll
-        for (int p = 0; p < 4; p++) v[p] = v1[p];
-        if (r + 2 < rows) {
+        for (int d = 0; d + 1 < kUnshufDepth; d++) {
+#pragma unroll
+          for (int p = 0; p < 4; p++) v[d][p] = v[d + 1][p];
+        }
+        if (r + kUnshufDepth < rows) {
 #pragma unroll
           for (int p = 0; p < 4; p++)
-            v1[p] = *reinterpret_cast<const u32x4*>(src + (int64_t)p * n + (int64_t)(r + 2) * 1024 + 16 * lane);
+            v[kUnshufDepth - 1][p] =
+                *reinterpret_cast<const u32x4*>(src + (int64_t)p * n + (int64_t)(r + kUnshufDepth) * 1024 + 16 * lane);
         }
         uint8_t* row = dst + (int64_t)r * 4096;
 #pragma unroll

@@ -788,6 +788,49 @@ __device__ __forceinline__ void wave_copy(gout_t o, gin_t s, int32_t n) {
   for (int32_t j = h + n16 * 16 + lane; j < n; j += 64) st8<WT>(o, r, j, s[j]);
 }
 
+// n bytes from a 16-byte aligned source to a destination of any alignment, with one 16-byte load
+// and one 16-byte store per lane step (wave_copy's dword loads cost 4-5x the address work, which
+// slows the latency-bound encoders sharing the CU when this runs inside their launch): the piece
+// a lane stores straddles its own source chunk and the next lane's, fetched with DPP wave_shl:1
+// (lane 63 loads it); sources are read up to 15 bytes past their end (scratch slack).
+__device__ __forceinline__ u32x4 dpp_next_lane(u32x4 v) {   // lane l gets lane l + 1's value
+  u32x4 r;
+  r.x = __builtin_amdgcn_update_dpp(0, (int)v.x, 0x130, 0xf, 0xf, false);
+  r.y = __builtin_amdgcn_update_dpp(0, (int)v.y, 0x130, 0xf, 0xf, false);
+  r.z = __builtin_amdgcn_update_dpp(0, (int)v.z, 0x130, 0xf, 0xf, false);
+  r.w = __builtin_amdgcn_update_dpp(0, (int)v.w, 0x130, 0xf, 0xf, false);
+  return r;
+}
+__device__ void wave_copy_a16(gout_t o, gin_t s, int32_t n) {
+  const int lane = lane_id();
+  const int32_t head = (int32_t)((16 - (reinterpret_cast<uintptr_t>(o) & 15)) & 15);
+  const int32_t h = min(head, n);
+  if (lane < h) o[lane] = s[lane];
+  const int32_t n16 = (n - h) / 16;
+  const B2H_GLB u32x4* s16 = reinterpret_cast<const B2H_GLB u32x4*>(s);
+  B2H_GLB u32x4* o16 = reinterpret_cast<B2H_GLB u32x4*>(o + h);
+  if (h == 0) {
+    for (int32_t i = lane; i < n16; i += 64) o16[i] = s16[i];
+  } else {
+    const uint32_t ds = (uint32_t)h >> 2, bs = (uint32_t)h & 3;
+    for (int32_t i0 = 0; i0 < n16; i0 += 64) {
+      const int32_t i = i0 + lane;
+      const u32x4 a = i <= n16 ? s16[i] : u32x4{0, 0, 0, 0};   // chunk n16 still holds source bytes
+      u32x4 b = dpp_next_lane(a);
+      if (lane == 63 && i + 1 <= n16) b = s16[i + 1];
+      const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      u32x4 v;
+      // bytes [h, h + 16) of a | b: dword shift ds (wave-uniform), byte shift bs
+      if (ds == 0) v = {funnel(w[0], w[1], bs), funnel(w[1], w[2], bs), funnel(w[2], w[3], bs), funnel(w[3], w[4], bs)};
+      else if (ds == 1) v = {funnel(w[1], w[2], bs), funnel(w[2], w[3], bs), funnel(w[3], w[4], bs), funnel(w[4], w[5], bs)};
+      else if (ds == 2) v = {funnel(w[2], w[3], bs), funnel(w[3], w[4], bs), funnel(w[4], w[5], bs), funnel(w[5], w[6], bs)};
+      else v = {funnel(w[3], w[4], bs), funnel(w[4], w[5], bs), funnel(w[5], w[6], bs), funnel(w[6], w[7], bs)};
+      if (i < n16) o16[i] = v;
+    }
+  }
+  for (int32_t j = h + n16 * 16 + lane; j < n; j += 64) o[j] = s[j];
+}
+
 // ------------------------------------------------------------------------------- decoder ----
 // Double-buffered register window over the compressed stream.  w0 holds stream bytes
 // [wpos, wpos + 256) (lane l: the aligned dword at wpos + 4 l), w1 the next 256; wpos is chosen so
