@@ -805,19 +805,20 @@ __device__ void wave_copy_a16(gout_t o, gin_t s, int32_t n) {
   const int lane = lane_id();
   const int32_t head = (int32_t)((16 - (reinterpret_cast<uintptr_t>(o) & 15)) & 15);
   const int32_t h = min(head, n);
-  if (lane < h) o[lane] = s[lane];
+  auto ld16 = [&](int32_t i) -> u32x4 { return reinterpret_cast<const B2H_GLB u32x4*>(s)[i]; };
+  auto ld8 = [&](int32_t j) -> uint8_t { return s[j]; };
+  if (lane < h) o[lane] = ld8(lane);
   const int32_t n16 = (n - h) / 16;
-  const B2H_GLB u32x4* s16 = reinterpret_cast<const B2H_GLB u32x4*>(s);
   B2H_GLB u32x4* o16 = reinterpret_cast<B2H_GLB u32x4*>(o + h);
   if (h == 0) {
-    for (int32_t i = lane; i < n16; i += 64) o16[i] = s16[i];
+    for (int32_t i = lane; i < n16; i += 64) o16[i] = ld16(i);
   } else {
     const uint32_t ds = (uint32_t)h >> 2, bs = (uint32_t)h & 3;
     for (int32_t i0 = 0; i0 < n16; i0 += 64) {
       const int32_t i = i0 + lane;
-      const u32x4 a = i <= n16 ? s16[i] : u32x4{0, 0, 0, 0};   // chunk n16 still holds source bytes
+      const u32x4 a = i <= n16 ? ld16(i) : u32x4{0, 0, 0, 0};   // chunk n16 still holds source bytes
       u32x4 b = dpp_next_lane(a);
-      if (lane == 63 && i + 1 <= n16) b = s16[i + 1];
+      if (lane == 63 && i + 1 <= n16) b = ld16(i + 1);
       const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
       u32x4 v;
       // bytes [h, h + 16) of a | b: dword shift ds (wave-uniform), byte shift bs
@@ -828,7 +829,7 @@ __device__ void wave_copy_a16(gout_t o, gin_t s, int32_t n) {
       if (i < n16) o16[i] = v;
     }
   }
-  for (int32_t j = h + n16 * 16 + lane; j < n; j += 64) o[j] = s[j];
+  for (int32_t j = h + n16 * 16 + lane; j < n; j += 64) o[j] = ld8(j);
 }
 
 // ------------------------------------------------------------------------------- decoder ----
@@ -1261,8 +1262,35 @@ __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, 
         if (x <= last + lrun) ring[(op + (int32_t)(last_pk >> 6) + (x - last - 1)) & RM] = (uint8_t)byte;
       }
       DPROF_T(t4);
-      // ---- 4b. matches in order ----
-      uint64_t mm = batch & ~__ballot(lit);
+      // ---- 4b. matches ----
+      // Matches whose whole source precedes the batch (src + len <= op, in the ring, <= 64 bytes)
+      // read nothing this batch writes: their ring reads go out four at a time, ahead of the
+      // writes (62 % of T's fast-mode matches); the others follow in order, after them.
+      const bool indep = inb && !lit && olen <= 64 && dist >= ex + olen && op + ex - dist >= F;
+      uint64_t im = __ballot(indep);
+      while (im) {
+        int32_t oj[4], lj[4], sj[4];
+        uint8_t vb[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          lj[u] = 0;
+          oj[u] = 0;
+          sj[u] = 0;
+          if (im) {
+            const int j = __builtin_ctzll(im);
+            im &= im - 1;
+            oj[u] = op + __builtin_amdgcn_readlane(ex, j);
+            lj[u] = __builtin_amdgcn_readlane(olen, j);
+            sj[u] = oj[u] - __builtin_amdgcn_readlane(dist, j);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) vb[u] = lane < lj[u] ? ring[(sj[u] + lane) & RM] : (uint8_t)0;
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if (lane < lj[u]) ring[(oj[u] + lane) & RM] = vb[u];
+      }
+      uint64_t mm = batch & ~__ballot(lit) & ~__ballot(indep);
       while (mm) {
         const int j = __builtin_ctzll(mm);
         mm &= mm - 1;
