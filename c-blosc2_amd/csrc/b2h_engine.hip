@@ -1272,22 +1272,23 @@ __device__ __forceinline__ void tr4(uint32_t a, uint32_t b, uint32_t c, uint32_t
   o[1] = __builtin_amdgcn_perm(t3, t1, 0x05040100u);
   o[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
 }
-__device__ void shuffle4_block_wt(const uint8_t* __restrict__ s, uint8_t* __restrict__ d, int32_t bsize) {
+__device__ void shuffle4_block_wt(const uint8_t* __restrict__ s, uint8_t* __restrict__ d, int32_t bsize,
+                                  int32_t tid = threadIdx.x, int32_t nth = blockDim.x) {
   const int32_t n = bsize / 4, groups = n / 16;
   const __amdgpu_buffer_rsrc_t r = wt_rsrc((gout_t)d);
   const uint4* s4 = reinterpret_cast<const uint4*>(s);
   constexpr int U = 2;
-  for (int32_t g0 = threadIdx.x; g0 < groups; g0 += U * blockDim.x) {
+  for (int32_t g0 = tid; g0 < groups; g0 += U * nth) {
     uint4 w[U][4];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int32_t gi = g0 + u * blockDim.x;
+      const int32_t gi = g0 + u * nth;
 #pragma unroll
       for (int k = 0; k < 4; k++) w[u][k] = gi < groups ? s4[4 * gi + k] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int32_t gi = g0 + u * blockDim.x;
+      const int32_t gi = g0 + u * nth;
       if (gi >= groups) break;
       uint32_t o[4][4];   // [element quad k][plane]
 #pragma unroll
@@ -1501,8 +1502,9 @@ __global__ void k_fuse_check(const int32_t* __restrict__ sync, int32_t* __restri
 }
 
 // B2H_FUSE (A/B runs, tests): 0 separate launches; bit 1 finalize + scatter inside the encode launch,
-// bit 2 + the byte shuffle, bit 16 scatter items only once the stream queue is empty, bit 32
-// non-temporal scatter copies.  Default 19.  Measured on T (tools/fuse_prof.py, profiles/r2_v5_*):
+// bit 2 + the byte shuffle, bit 4 exact mode too (k_encode_fused: per-wave shuffles and copies are
+// latency-bound, T exact 26.98 -> 27.72 ms, so off by default), bit 16 scatter items only once the
+// stream queue is empty, bit 32 plain dword-load scatter copies.  Default 19.  Measured on T (tools/fuse_prof.py, profiles/r2_v5_*):
 // separate 1.54 + 16.55 + 1.10 ms; 19: 17.79 ms; scatter items claimed between streams (3) slow
 // the concurrent encoders' short planes ~2x (22.5 ms), with non-temporal copies too (35).
 static int fuse_bits() {
@@ -1513,6 +1515,20 @@ static bool fuse_enabled() { return (fuse_bits() & 1) != 0; }
 static int fuse_lead() {
   static const int v = [] { const char* e = getenv("B2H_SHUF_LEAD"); return e ? std::max(1, atoi(e)) : 512; }();
   return v;
+}
+
+// Sync words (zeroed) + per-stream results of a fused launch (f.raw / f.filt set by the caller).
+static int fuse_prepare(Workspace* ws, const CGeom& g, int64_t ntot, EncFuse& f, hipStream_t st) {
+  const size_t sync_words = kFuseHdr + (size_t)f.nchunks * g.nblocks + 2 * (size_t)f.nchunks;
+  const size_t sync_bytes = (sync_words * 4 + 15) & ~size_t(15);
+  if (ws->fsync.ensure(sync_bytes + 12 * (size_t)ntot)) return E_MEMORY;
+  f.sync = ws->fsync.as<int32_t>();
+  f.fin = reinterpret_cast<int32_t*>(ws->fsync.as<uint8_t>() + sync_bytes);
+  f.lead = fuse_lead();
+  f.mode_bits = fuse_bits();
+  f.trace = nullptr;
+  HIPCHK(hipMemsetAsync(f.sync, 0, sync_bytes, st));
+  return 0;
 }
 
 // Sync words + per-stream results of the fused launch (f.raw / f.filt set by the caller).
@@ -1530,14 +1546,7 @@ static int launch_encode_fast_fused_t(Workspace* ws, const CGeom& g, const uint8
   }
   const int slots = resident_slots(fn, lds, 128);
   const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(ntot, slots));
-  const size_t sync_words = kFuseHdr + (size_t)f.nchunks * g.nblocks + 2 * (size_t)f.nchunks;
-  const size_t sync_bytes = (sync_words * 4 + 15) & ~size_t(15);
-  if (ws->fsync.ensure(sync_bytes + 12 * (size_t)ntot)) return E_MEMORY;
-  f.sync = ws->fsync.as<int32_t>();
-  f.fin = reinterpret_cast<int32_t*>(ws->fsync.as<uint8_t>() + sync_bytes);
-  f.lead = fuse_lead();
-  f.mode_bits = fuse_bits();
-  HIPCHK(hipMemsetAsync(f.sync, 0, sync_bytes, st));
+  if (fuse_prepare(ws, g, ntot, f, st)) return E_MEMORY;
   static int32_t* trace = nullptr;
   static const bool tr = getenv("B2H_FUSE_TRACE") != nullptr;
   if (tr && !trace) HIPCHK(hipHostMalloc(&trace, 4 << 20, hipHostMallocCoherent));
@@ -1570,8 +1579,15 @@ static int launch_encode_fast_fused_t(Workspace* ws, const CGeom& g, const uint8
 
 // The fused launch applies to BloscLZ fast mode without a dictionary when the chunk's stream
 // results fit the LDS table (the finalizing workgroup stages them there).
+static void enc_mode(int* nlds, int* nglb);
 static bool fused_encode_ok(const CGeom& g) {
-  if (!fuse_enabled() || lz_mode() != 1 || g.compcode != 0 || g.dict_size) return false;
+  if (!fuse_enabled() || g.compcode != 0 || g.dict_size) return false;
+  if (lz_mode() == 0) {   // exact mode: only with bit 4 (measured slower), the default k_encode shape
+    if (!(fuse_bits() & 4)) return false;
+    int nl, ng;
+    enc_mode(&nl, &ng);
+    return nl == 1 && ng == 3;
+  }
   const bool small = std::max(g.neblock, g.leftover) <= 65536;
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
   const int tablog = std::min(fast_tablog(), hashlog);
@@ -1585,6 +1601,195 @@ static int launch_encode_fast_fused(Workspace* ws, const CGeom& g, const uint8_t
   return launch_encode_fast_fused_t<uint32_t>(ws, g, filt, res, ntot, next, porder, f, st);
 }
 
+
+// ------------------------------------------- exact mode, one launch: shuffle -> encode -> scatter ----
+// k_encode's waves pull streams independently, so the fused protocol of k_encode_fast_fused runs
+// per wave here: shuffle claims ahead of the wave's stream, the wave that completes a chunk
+// finalizes it, scatter items once the stream queue is empty.  Every wave-level decision comes
+// from an atomic all 64 lanes take part in (lane 0 adds, the others add 0) and a readfirstlane,
+// never from a value only lane 0 holds (see encode_loop).
+template <typename TAB>
+__device__ void encode_loop_fused(const CGeom& g, TAB htab, B2H_LDS uint32_t* dbits, B2H_LDS uint8_t* oring,
+                                  const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
+                                  StreamResult* __restrict__ res, int32_t nstreams_total, int32_t* __restrict__ next,
+                                  const int32_t* __restrict__ porder, const EncFuse& f) {
+  const int lane = lane_id();
+  const int32_t nblk = f.nchunks * g.nblocks;
+  int32_t* blk_ready = f.sync + kFuseHdr;
+  int32_t* chunk_cnt = blk_ready + nblk;
+  int32_t* ready = chunk_cnt + f.nchunks;
+  int32_t* tmo = f.sync + 4;
+  const int32_t ipc = (g.nsc + kFuseSpi - 1) / kFuseSpi, nitems = f.nchunks * ipc;
+  auto wadd = [&](int32_t* p, int32_t v) -> int32_t {
+    return __builtin_amdgcn_readfirstlane(
+        __hip_atomic_fetch_add((gi32_t)p, lane == 0 ? v : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  };
+  auto wwait = [&](int32_t* p) -> int32_t {   // bounded poll, all lanes
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (int32_t it = 0; it < (1 << 21); it++) {
+      const int32_t v = wadd(p, 0);
+      if (v) return v;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) break;
+      __builtin_amdgcn_s_sleep(8);
+    }
+    if (lane == 0) st_agent(tmo, 1);
+    return 0;
+  };
+  auto claim_block = [&](int32_t target) -> int32_t { return wadd(f.sync, 0) < target ? wadd(f.sync, 1) : -1; };
+  int32_t i = wadd(next, 1);
+  while (i < nstreams_total) {
+    const int32_t s = __builtin_amdgcn_readfirstlane(pull_to_stream(g, porder, g.front, i, nstreams_total));
+    const int32_t c = s / g.nsc, l = s - c * g.nsc;
+    int32_t off, len, blk;
+    stream_locate(g, l, &off, &len, &blk);
+    if (f.raw) {
+      const int32_t gb = c * g.nblocks + blk, target = min(gb + 1 + f.lead, nblk);
+      int32_t k = claim_block(target);
+      while (k >= 0 && k < nblk) {
+        const int32_t cc = k / g.nblocks, b = k - cc * g.nblocks;
+        const int32_t bsize = (b == g.nblocks - 1 && g.leftover) ? g.leftover : g.bs;
+        shuffle4_block_wt(f.raw + (int64_t)cc * f.raw_stride + (int64_t)b * g.bs,
+                          f.filt + (int64_t)cc * g.wstride + (int64_t)b * g.bs, bsize, lane, 64);
+        drain_stores();
+        if (lane == 0) st_agent(blk_ready + k, 1);
+        k = claim_block(target);
+      }
+      (void)wwait(blk_ready + gb);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      drain_stores();
+    }
+    gin_t in = (gin_t)(filt + (int64_t)c * g.wstride + off);
+    gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+    StreamResult r = encode_stream<TAB, true>(in, len, g.clevel, out, htab, dbits, oring, g.overhead == kHdrExt);
+    r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
+    if (TAB::kGlobal) r.windows |= 1 << 30;
+    r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
+    if (lane == 0) {
+      res[s] = r;
+      st_agent(f.fin + 3 * s, r.kind);
+      st_agent(f.fin + 3 * s + 1, r.size);
+      st_agent(f.fin + 3 * s + 2, r.peak);
+    }
+    drain_stores();
+    const int32_t done = wadd(chunk_cnt + c, 1);
+    if (done == g.nsc - 1) {   // this wave completed chunk c: finalize it
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      drain_stores();
+      const bool inreg = g.nsc <= 64;   // lane j holds stream j's results
+      const int32_t* fc = f.fin + 3 * (int64_t)c * g.nsc;
+      int32_t fk = 0, fs = 0, fp = 0;
+      if (inreg && lane < g.nsc) {
+        fk = fc[3 * lane];
+        fs = fc[3 * lane + 1];
+        fp = fc[3 * lane + 2];
+      }
+      if (lane == 0) {
+        Place* pl = f.place + (int64_t)c * g.nsc;
+        int32_t cb = 0;
+        const int32_t m = finalize_chunk(
+            g, f.dst + (int64_t)c * g.dst_stride, f.htpl,
+            [&](int32_t j) {
+              StreamResult x;
+              x.kind = inreg ? __builtin_amdgcn_readlane(fk, j) : fc[3 * j];
+              x.size = inreg ? __builtin_amdgcn_readlane(fs, j) : fc[3 * j + 1];
+              x.peak = inreg ? __builtin_amdgcn_readlane(fp, j) : fc[3 * j + 2];
+              return x;
+            },
+            [&](int32_t j, int32_t o, int32_t cs) { st_agent(&pl[j].off, o); st_agent(&pl[j].csize, cs); }, &cb);
+        st_agent(f.mode + c, m);
+        f.cbytes[c] = cb;
+        drain_stores();
+        const int32_t slot = add_agent(f.sync + 2, 1);
+        st_agent(ready + slot, c + 1);
+        drain_stores();
+        add_agent(f.sync + 3, ipc);
+      }
+    }
+    i = wadd(next, 1);
+  }
+  // stream queue empty: scatter items
+  int32_t k = wadd(f.sync + 1, 1);
+  while (k < nitems) {
+    const int32_t slot = k / ipc, j0 = (k - slot * ipc) * kFuseSpi;
+    const int32_t v = wwait(ready + slot);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    drain_stores();
+    const int32_t c = v - 1;
+    if (v > 0 && __builtin_amdgcn_readfirstlane(f.mode[c]) == 0) {
+      uint8_t* d = f.dst + (int64_t)c * g.dst_stride;
+      for (int32_t l = j0; l < min(j0 + kFuseSpi, g.nsc); l++) {
+        const int32_t s = c * g.nsc + l;
+        const int32_t poff = __builtin_amdgcn_readfirstlane(f.place[s].off);
+        const int32_t pcs = __builtin_amdgcn_readfirstlane(f.place[s].csize);
+        int32_t off, len, blk;
+        stream_locate(g, l, &off, &len, &blk);
+        if (lane == 0) {
+          const uint32_t w = (uint32_t)pcs;
+          uint8_t* q = d + poff - 4;
+          q[0] = (uint8_t)w; q[1] = (uint8_t)(w >> 8); q[2] = (uint8_t)(w >> 16); q[3] = (uint8_t)(w >> 24);
+          if (pcs < 0) d[poff] = 0x1;   // run-length token
+        }
+        if (pcs <= 0) continue;
+        const uint8_t* src = (pcs == len ? filt : sbuf) + (int64_t)c * g.wstride + off;
+        if (aligned16(src)) wave_copy_a16((gout_t)(d + poff), (gin_t)src, pcs);
+        else wave_copy((gout_t)(d + poff), (gin_t)src, pcs);
+      }
+    }
+    k = wadd(f.sync + 1, 1);
+  }
+}
+
+template <typename POS, int NLDS, int NGLB>
+__global__ __launch_bounds__(64 * (NLDS + NGLB)) void k_encode_fused(CGeom g, const uint8_t* __restrict__ filt,
+                                                                     uint8_t* __restrict__ sbuf,
+                                                                     StreamResult* __restrict__ res,
+                                                                     int32_t nstreams_total, int32_t* __restrict__ next,
+                                                                     POS* __restrict__ gtab,
+                                                                     const int32_t* __restrict__ porder, EncFuse f) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const size_t tabsz = sizeof(POS) << hashlog;
+  B2H_LDS uint8_t* mine = (B2H_LDS uint8_t*)(smem + NLDS * tabsz + w * enc_wave_lds(hashlog));
+  B2H_LDS uint32_t* dbits = (B2H_LDS uint32_t*)mine;
+  B2H_LDS uint8_t* oring = mine + ((size_t(1) << hashlog) >> 3);
+  if (NLDS > 0 && w < NLDS) {
+    LdsTab<POS> t;
+    t.t = (volatile B2H_LDS POS*)(smem + w * tabsz);
+    encode_loop_fused(g, t, dbits, oring, filt, sbuf, res, nstreams_total, next, porder, f);
+  } else if (NGLB > 0) {
+    GlbTab<POS> t;
+    t.t = (B2H_GLB POS*)(gtab + (((size_t)blockIdx.x * NGLB + (w - NLDS)) << hashlog));
+    encode_loop_fused(g, t, dbits, oring, filt, sbuf, res, nstreams_total, next, porder, f);
+  }
+}
+
+// exact mode, default shape (1 LDS-table wave + 3 global-table waves, enc_mode hyb3) only
+template <typename POS>
+static int launch_encode_exact_fused(Workspace* ws, const CGeom& g, int hashlog, const uint8_t* filt,
+                                     StreamResult* res, int64_t ntot, int32_t* next, const int32_t* porder, EncFuse f,
+                                     hipStream_t st) {
+  constexpr int NL = 1, NG = 3;
+  const void* fn = reinterpret_cast<const void*>(&k_encode_fused<POS, NL, NG>);
+  const size_t lds = enc_wg_lds<POS>(hashlog, NL, NG);
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  const int slots = resident_slots(fn, lds, 64 * (NL + NG));
+  const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>((ntot + NL + NG - 1) / (NL + NG), slots));
+  if (ws->gtab.ensure(((size_t)grid * NG << hashlog) * sizeof(POS))) return E_MEMORY;
+  if (fuse_prepare(ws, g, ntot, f, st)) return E_MEMORY;
+  k_encode_fused<POS, NL, NG><<<grid, 64 * (NL + NG), lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot,
+                                                               next, ws->gtab.as<POS>(), porder, f);
+  HIPCHK(hipGetLastError());
+  k_fuse_check<<<(f.nchunks + 255) / 256, 256, 0, st>>>(f.sync, f.cbytes, f.nchunks);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
 // ============================================================ compression: host driver ====
 static int32_t split_block(int32_t splitmode, int compcode, const uint8_t* filters, int32_t ts, int32_t bs) {
   // blosc/stune.c:186-215
@@ -1991,7 +2196,9 @@ static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const ui
       f.cbytes = d_cbytes;
       f.htpl = htpl;
       f.nchunks = nchunks;
-      rc = launch_encode_fast_fused(ws, g, filt, res, ntot, next, porder, f, st);
+      if (lz_mode() == 1) rc = launch_encode_fast_fused(ws, g, filt, res, ntot, next, porder, f, st);
+      else rc = small ? launch_encode_exact_fused<uint16_t>(ws, g, hashlog, filt, res, ntot, next, porder, f, st)
+                      : launch_encode_exact_fused<uint32_t>(ws, g, hashlog, filt, res, ntot, next, porder, f, st);
     } else if (lz_mode() == 1) rc = launch_encode_fast(ws, g, filt, res, ntot, next, porder, st);
     else rc = small ? launch_encode<uint16_t>(ws, g, hashlog, filt, res, ntot, next, porder, st)
                     : launch_encode<uint32_t>(ws, g, hashlog, filt, res, ntot, next, porder, st);

@@ -64,6 +64,49 @@ __device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh
   return __builtin_amdgcn_alignbyte(hi, lo, sh_bytes);
 }
 
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// ---------------------------------------------------------------- plain / write-through stores ----
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(gout_t base) {
+  const uint64_t a = reinterpret_cast<uintptr_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+template <bool WT>
+__device__ __forceinline__ void st16(gout_t base, __amdgpu_buffer_rsrc_t r, int32_t off, u32x4 v) {
+  if constexpr (WT) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+  else *reinterpret_cast<B2H_GLB u32x4*>(base + off) = v;
+}
+template <bool WT>
+__device__ __forceinline__ void st8(gout_t base, __amdgpu_buffer_rsrc_t r, int32_t off, uint8_t v) {
+  if constexpr (WT) __builtin_amdgcn_raw_buffer_store_b8(v, r, off, 0, 16);
+  else base[off] = v;
+}
+
+// Output ring -> global bytes [F, to) of `out` (one wave).  16-byte stores (the ring index of a
+// byte is its output offset mod kOutRing, so a 16-aligned output offset is a 16-aligned ring
+// offset when `out` is 16-aligned), bytes at the ends; WT: write-through (`sc1`) stores, for
+// streams another workgroup copies inside the same launch (k_encode_fast_fused).
+template <bool WT>
+__device__ __forceinline__ void ring_flush(gout_t out, const B2H_LDS uint8_t* oring, int32_t F, int32_t to) {
+  constexpr int32_t ORM = kOutRing - 1;
+  const int lane = lane_id();
+  const __amdgpu_buffer_rsrc_t r = wt_rsrc(out);
+  if ((reinterpret_cast<uintptr_t>(out) & 15) != 0 || to - F < 32) {
+    for (int32_t y = F + lane; y < to; y += 64) st8<WT>(out, r, y, oring[y & ORM]);
+    return;
+  }
+  const int32_t a = (F + 15) & ~15, b = to & ~15;
+  if (lane < a - F) st8<WT>(out, r, F + lane, oring[(F + lane) & ORM]);
+  if (lane < to - b) st8<WT>(out, r, b + lane, oring[(b + lane) & ORM]);
+  for (int32_t y = a + 16 * lane; y < b; y += 1024)
+    st16<WT>(out, r, y, *reinterpret_cast<const B2H_LDS u32x4*>(oring + (y & ORM)));
+}
+
+
 // Unaligned little-endian u32 from global memory: two aligned dword loads + funnel shift.
 // Callers guarantee 8 readable bytes past p & ~3 (buffers carry slack).
 __device__ __forceinline__ uint32_t ldu32(gin_t p) {
@@ -103,7 +146,6 @@ __device__ __forceinline__ void ld28(gin_t p, uint32_t (&w)[7]) {
   for (int i = 0; i < 7; i++) w[i] = funnel(d[i], d[i + 1], sh);
 }
 
-__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 __device__ __forceinline__ int32_t rdlane(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
@@ -231,7 +273,7 @@ __device__ uint64_t g_enc_prof[16];
 
 // One greedy parse.  PROBE: get_cratio (counts only, limit = min(length, 2^hashlog), no far
 // short-match rule, no clevel-9 double rehash, no tail).  !PROBE: the emitting main loop + tail.
-template <bool PROBE, typename TAB>
+template <bool PROBE, typename TAB, bool WT = false>
 __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashlog, int clevel, gout_t out,
                                              int32_t maxout, TAB htab, B2H_LDS uint32_t* dbits,
                                              B2H_LDS uint8_t* oring) {
@@ -242,7 +284,7 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
   constexpr int32_t ORM = kOutRing - 1;
   int32_t F = 0;   // output [0, F) already in `out`
   auto flush = [&](int32_t to) {
-    for (int32_t y = F + lane; y < to; y += 64) out[y] = oring[y & ORM];
+    ring_flush<WT>(out, oring, F, to);
     F = to;
   };
   int32_t limit = length;
@@ -602,7 +644,7 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashl
       } else {
         flush(o);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the flushed byte 0 first
-        if (lane == 0) out[0] = (uint8_t)(byte0 | 0x20u);
+        if (lane == 0) st8<WT>(out, wt_rsrc(out), 0, (uint8_t)(byte0 | 0x20u));
       }
     }
   }
@@ -663,7 +705,7 @@ __device__ __forceinline__ bool wave_is_run_from(gin_t s, int32_t from, int32_t 
 }
 
 // Full per-stream encode with maxout = neblock: run test, entropy probe, main pass.
-template <typename TAB>
+template <typename TAB, bool WT = false>
 __device__ __forceinline__ StreamResult encode_stream(gin_t in, int32_t n, int clevel, gout_t out,
                                                       TAB htab, B2H_LDS uint32_t* dbits,
                                                       B2H_LDS uint8_t* oring, bool allow_runs) {
@@ -683,13 +725,13 @@ __device__ __forceinline__ StreamResult encode_stream(gin_t in, int32_t n, int c
   if (clevel < 2) maxlen /= 8;
   else if (clevel < 4) maxlen /= 4;
   else if (clevel < 7) maxlen /= 2;
-  const LzPassOut pr = lz_pass<true, TAB>(in + (n - maxlen), maxlen, hashlog, clevel, out, 0, htab, dbits, oring);
+  const LzPassOut pr = lz_pass<true, TAB, WT>(in + (n - maxlen), maxlen, hashlog, clevel, out, 0, htab, dbits, oring);
   res.windows = pr.windows;
   const double ratio = (double)pr.pos / (double)pr.o;
   // cratio_ thresholds of blosc/blosclz.c:465 (compared in double, as the reference does)
   const double thr = clevel == 1 ? 2.0 : clevel == 2 ? 1.5 : clevel <= 6 ? 1.2 : clevel == 7 ? 1.15 : clevel == 8 ? 1.1 : 1.0;
   if (pr.early || (!pr.sure && ratio < thr) || n < 16 || n < 66) return res;
-  const LzPassOut em = lz_pass<false, TAB>(in, n, hashlog, clevel, out, n, htab, dbits, oring);
+  const LzPassOut em = lz_pass<false, TAB, WT>(in, n, hashlog, clevel, out, n, htab, dbits, oring);
   res.windows += em.windows;
   if (em.fail) return res;
   res.kind = kStreamLz;
@@ -704,25 +746,6 @@ __device__ __forceinline__ StreamResult encode_stream(gin_t in, int32_t n, int c
 // wave that completes a block can hand the block's planes to its own unshuffle inside the launch:
 // every stream's bytes are in memory once its wave has drained them (vmcnt(0)), whichever XCD wrote
 // them.  The descriptor is built from the wave-uniform base (no waterfall loops).
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(gout_t base) {
-  const uint64_t a = reinterpret_cast<uintptr_t>(base);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, 0x7fffffff,
-                                           0x00020000);
-}
-template <bool WT>
-__device__ __forceinline__ void st16(gout_t base, __amdgpu_buffer_rsrc_t r, int32_t off, u32x4 v) {
-  if constexpr (WT) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
-  else *reinterpret_cast<B2H_GLB u32x4*>(base + off) = v;
-}
-template <bool WT>
-__device__ __forceinline__ void st8(gout_t base, __amdgpu_buffer_rsrc_t r, int32_t off, uint8_t v) {
-  if constexpr (WT) __builtin_amdgcn_raw_buffer_store_b8(v, r, off, 0, 16);
-  else base[off] = v;
-}
-
 template <bool WT = false>
 __device__ __forceinline__ void wave_fill(gout_t o, uint8_t v, int32_t n) {
   const int lane = lane_id();

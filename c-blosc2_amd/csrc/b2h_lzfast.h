@@ -76,26 +76,6 @@ __device__ __forceinline__ void rawc_load(gin_t p, RawCmp& r) {
 }
 __device__ __forceinline__ uint32_t rawc_word(const RawCmp& r, int i) { return funnel(r.d[i], r.d[i + 1], r.sh); }
 
-// Output ring -> global bytes [F, to) of `out` (one wave).  16-byte stores (the ring index of a
-// byte is its output offset mod kOutRing, so a 16-aligned output offset is a 16-aligned ring
-// offset when `out` is 16-aligned), bytes at the ends; WT: write-through (`sc1`) stores, for
-// streams another workgroup copies inside the same launch (k_encode_fast_fused).
-template <bool WT>
-__device__ __forceinline__ void ring_flush(gout_t out, const B2H_LDS uint8_t* oring, int32_t F, int32_t to) {
-  constexpr int32_t ORM = kOutRing - 1;
-  const int lane = lane_id();
-  const __amdgpu_buffer_rsrc_t r = wt_rsrc(out);
-  if ((reinterpret_cast<uintptr_t>(out) & 15) != 0 || to - F < 32) {
-    for (int32_t y = F + lane; y < to; y += 64) st8<WT>(out, r, y, oring[y & ORM]);
-    return;
-  }
-  const int32_t a = (F + 15) & ~15, b = to & ~15;
-  if (lane < a - F) st8<WT>(out, r, F + lane, oring[(F + lane) & ORM]);
-  if (lane < to - b) st8<WT>(out, r, b + lane, oring[(b + lane) & ORM]);
-  for (int32_t y = a + 16 * lane; y < b; y += 1024)
-    st16<WT>(out, r, y, *reinterpret_cast<const B2H_LDS u32x4*>(oring + (y & ORM)));
-}
-
 // ============================================================ matcher / parser workgroup ====
 // One stream per workgroup of two waves (k_encode_fast):
 //   wave 0, the MATCHER: tile exchanges, candidate loads and 60-byte compares -- for each lane of a

@@ -15,7 +15,8 @@ import torch  # noqa: E402
 import blosc2_amd as B  # noqa: E402
 from bench import gen_f32_device  # noqa: E402
 
-modes = sys.argv[1:] or ["0", "1", "3"]
+lzm = int(os.environ.get("LZMODE", "1"))   # 1 fast, 0 exact
+modes = sys.argv[1:] or ["0", "19"]
 nch, chunk = 1024, 4 << 20
 src = gen_f32_device(0, nch * chunk // 4, torch.device("cuda", 0)).view(torch.uint8)
 stride = chunk + 256
@@ -23,7 +24,7 @@ dst = torch.empty(nch * stride, dtype=torch.uint8, device="cuda")
 cb = torch.zeros(nch, dtype=torch.int32, device="cuda")
 cp = B.cparams(clevel=5, typesize=4)
 L = B.lib()
-L.b2h_set_blosclz_mode(1)
+L.b2h_set_blosclz_mode(lzm)
 L.b2h_enable_timing(1)
 L.b2h_debug_stream_results.argtypes = [C.c_void_p, C.c_int32]
 ns = nch * 64

@@ -11,7 +11,7 @@ echo "fast-mode tests..."
 timeout -k 10 300 python -u -m pytest tests/test_fast_mode.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/fuse_tests_$TAG.log 2>&1 || { echo "fast tests failed"; tail -40 $O/fuse_tests_$TAG.log; exit 1; }
 tail -2 $O/fuse_tests_$TAG.log
 echo "bench fused..."
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --lz-mode fast > $O/bench_fused_$TAG.log 2>&1 || { echo "bench failed"; tail -30 $O/bench_fused_$TAG.log; exit 1; }
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --lz-mode both > $O/bench_fused_$TAG.log 2>&1 || { echo "bench failed"; tail -30 $O/bench_fused_$TAG.log; exit 1; }
 tail -1 $O/bench_fused_$TAG.log
 echo "bench separate..."
 B2H_FUSE=0 timeout -k 10 300 python -u bench.py --no-cpu-baseline --lz-mode fast > $O/bench_sep_$TAG.log 2>&1 || { echo "bench sep failed"; tail -30 $O/bench_sep_$TAG.log; exit 1; }
