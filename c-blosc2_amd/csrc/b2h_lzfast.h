@@ -130,12 +130,18 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
   const double thr_s = thr_o * (1.001 / 0.999);
   EPROF_DECL;
 
-  // ---- matcher: the input words of tile `ant` (prefetched one step ahead) ----
+  // ---- matcher: the first input words of tile `ant` (prefetched one step ahead); the other 14
+  // are loaded only when some lane's candidate matches its first 4 bytes, together with the
+  // candidates' words (the same round trip): incompressible tiles issue 4 loads per lane, not 18 ----
   RawCmp na;
   int32_t ant = -1;
   auto load_a = [&](int32_t t, RawCmp& a) {
     const int32_t p = t * kFastTile + lane;
-    rawc_load(in + (p < loop_end ? p : 0), a);
+    gin_t q8 = in + (p < loop_end ? p : 0);
+    const B2H_GLB uint32_t* q = align4(q8);
+    a.sh = (uint32_t)(reinterpret_cast<uintptr_t>(q8) & 3);
+    a.d[0] = q[0];
+    a.d[1] = q[1];
   };
   // insert tile t, test every lane's candidate, hand the results over in slot `slot`
   auto produce = [&](int32_t t, int slot) {
@@ -162,8 +168,12 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
       uint32_t c[kCmpWords + 1];
       c[0] = c0;
       c[1] = c1;
+      const B2H_GLB uint32_t* aw = align4(in + (p < loop_end ? p : 0));
 #pragma unroll
-      for (int i = 2; i < kCmpWords + 1; i++) c[i] = cw[i];
+      for (int i = 2; i < kCmpWords + 1; i++) {
+        c[i] = cw[i];
+        a.d[i] = aw[i];
+      }
       mm = kCmpBytes;
 #pragma unroll
       for (int i = kCmpWords - 1; i >= 1; i--) {
