@@ -1382,13 +1382,11 @@ void k_encode_fast_fused(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __r
     }
     return -1;
   };
-  auto scatter_available = [&](int max_items) {
-    int32_t k = bcast(threadIdx.x == 0 ? try_claim_item() : 0);
-    int it = 1;
-    while (k >= 0) {
-      scatter_item(k);
-      k = it < max_items ? bcast(threadIdx.x == 0 ? try_claim_item() : 0) : -1;
-      it++;
+  auto scatter_available = [&](int max_items) {   // the broadcast unconditional in every iteration
+    int32_t k = 0;
+    for (int it = 0; it < max_items && k >= 0; it++) {
+      k = bcast(threadIdx.x == 0 ? try_claim_item() : -1);
+      if (k >= 0) scatter_item(k);
     }
   };
   // lane 0: claim the next block to shuffle while the claims are behind `target`, else -1
