@@ -456,7 +456,7 @@ def run(args):
         # the encoder kernel of the headline mode (rocprof names: k_encode_fast / k_encode)
         # fast mode runs shuffle + encode + finalize + scatter as ONE launch, k_encode_fast_fused
         # (B2H_FUSE, c-blosc2_amd/csrc/b2h_engine.hip); B2H_FUSE=0 restores the separate launches
-        fused = lz_name == "fast" and int(os.environ.get("B2H_FUSE", "19")) & 1
+        fused = lz_name == "fast" and int(os.environ.get("B2H_FUSE", "83")) & 1
         enc_name = ("k_encode_fast_fused" if fused else "k_encode_fast") if lz_name == "fast" else "k_encode"
         dominant = enc_name if enc >= dec else "k_decode"
         kms = enc if enc >= dec else dec

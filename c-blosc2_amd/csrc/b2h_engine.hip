@@ -458,6 +458,7 @@ void k_encode_fast(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restric
   B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + (sizeof(POS) << tablog));
   B2H_LDS FastShared* sh = (B2H_LDS FastShared*)(smem + (sizeof(POS) << tablog) + kOutRing);
   const bool matcher = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
+  if (!matcher) __builtin_amdgcn_s_setprio(2);   // the parser issues first (see k_encode_fast_fused)
   for (;;) {
     if (threadIdx.x == 0) sh->pull = atomicAdd(next, 1);
     __syncthreads();
@@ -1317,6 +1318,9 @@ void k_encode_fast_fused(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __r
   int32_t* chunk_cnt = blk_ready + nblk;
   int32_t* ready = chunk_cnt + f.nchunks;
   int32_t* tmo = f.sync + 4;
+  // wave priority (B2H_FUSE bit 64, default): the parser -- the tile's latency chain -- issues
+  // ahead of the matchers sharing its SIMD (T encode 18.0 -> 17.6 ms; the matcher first: 19.3)
+  if ((f.mode_bits & 64) && !matcher) __builtin_amdgcn_s_setprio(2);
   // lane 0 of the workgroup computes v, everyone gets it
   auto bcast = [&](int32_t v) -> int32_t {
     if (threadIdx.x == 0) sh->bcast = v;
@@ -1502,12 +1506,13 @@ __global__ void k_fuse_check(const int32_t* __restrict__ sync, int32_t* __restri
 // B2H_FUSE (A/B runs, tests): 0 separate launches; bit 1 finalize + scatter inside the encode launch,
 // bit 2 + the byte shuffle, bit 4 exact mode too (k_encode_fused: per-wave shuffles and copies are
 // latency-bound, T exact 26.98 -> 27.72 ms, so off by default), bit 16 scatter items only once the
-// stream queue is empty, bit 32 plain dword-load scatter copies.  Default 19.  Measured on T (tools/fuse_prof.py, profiles/r2_v5_*):
+// stream queue is empty, bit 32 plain dword-load scatter copies, bit 64 the parser wave at a
+// higher issue priority.  Default 83 (1 + 2 + 16 + 64).  Measured on T (tools/fuse_prof.py, profiles/r2_v5_*):
 // separate 1.54 + 16.55 + 1.10 ms; 19: 17.79 ms; scatter items claimed between streams (3) slow
 // the concurrent encoders' short planes ~2x (22.5 ms), with non-temporal copies too (35).
 static int fuse_bits() {
   const char* e = getenv("B2H_FUSE");
-  return e ? atoi(e) : 19;
+  return e ? atoi(e) : 83;
 }
 static bool fuse_enabled() { return (fuse_bits() & 1) != 0; }
 static int fuse_lead() {

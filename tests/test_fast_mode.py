@@ -273,7 +273,7 @@ def test_gpu_fast_ratio_T(fast):
 def test_gpu_fused_launch_matches_separate_launches(fast, shape, lzmode, monkeypatch):
     """The one-launch fast-mode encode (byte shuffle, finalize and payload scatter inside the
     encoder launch, k_encode_fast_fused) writes the same chunks as the separate launches
-    (B2H_FUSE=0; 19 is the default, 3 also claims scatter items between streams), in both BloscLZ
+    (B2H_FUSE=0; 83 is the default, 3 also claims scatter items between streams), in both BloscLZ
     modes (exact: k_encode_fused, per-wave hand-offs; its chunks also equal the oracle's), on T's shape (4 MiB chunks: fused shuffle) and on shapes where only the
     finalize/scatter is fused (a leftover block not of whole 64-byte groups, typesize 8)."""
     import torch
@@ -291,7 +291,7 @@ def test_gpu_fused_launch_matches_separate_launches(fast, shape, lzmode, monkeyp
     cp = B.cparams(**kw)
     B.lib().b2h_set_blosclz_mode(lzmode)
     got = {}
-    for fuse in ("19", "3", "0"):
+    for fuse in ("83", "3", "0"):
         # exact mode fuses only with bit 4 (k_encode_fused)
         monkeypatch.setenv("B2H_FUSE", fuse if lzmode == 1 or fuse == "0" else str(int(fuse) | 4))
         comp = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
@@ -302,13 +302,13 @@ def test_gpu_fused_launch_matches_separate_launches(fast, shape, lzmode, monkeyp
         assert (cbh > 0).all(), cbh
         compb = comp.cpu().numpy().reshape(n, stride)
         got[fuse] = [compb[i, :cbh[i]].copy() for i in range(n)]
-    for fz in ("19", "3"):
+    for fz in ("83", "3"):
         for a, b in zip(got[fz], got["0"]):
             assert np.array_equal(a, b), fz
     raw = src.cpu().numpy()
     B.lib().b2h_set_blosclz_mode(1)
     for i in range(0, n, 5):
-        assert np.array_equal(oracle_decompress(got["19"][i], chunk), raw[i * chunk:(i + 1) * chunk])
+        assert np.array_equal(oracle_decompress(got["83"][i], chunk), raw[i * chunk:(i + 1) * chunk])
         if lzmode == 0:   # exact mode: the reference's own chunk
             ex = oracle_compress(raw[i * chunk:(i + 1) * chunk], **kw)
-            assert np.array_equal(got["19"][i], ex)
+            assert np.array_equal(got["83"][i], ex)
