@@ -87,6 +87,7 @@ def _bind(lib):
         "b2h_enable_timing": ([C.c_int], None),
         "b2h_set_blosclz_mode": ([C.c_int], C.c_int),
         "b2h_last_times": ([C.POINTER(C.c_float)], None),
+        "b2h_mean_times": ([C.POINTER(C.c_float)], None),
         "b2h_last_error": ([], C.c_char_p),
         "b2h_device_count": ([], C.c_int),
     }
@@ -211,6 +212,14 @@ def device_copy(d_dst: int, d_src: int, nbytes: int, stream: int = 0):
 
 
 def last_times():
+    """Per-phase kernel times (ms) of the latest batch (waits for its events)."""
     buf = (C.c_float * 5)()
     lib().b2h_last_times(buf)
+    return dict(zip(("filter_ms", "encode_ms", "finalize_ms", "decode_ms", "unfilter_ms"), list(buf)))
+
+
+def mean_times():
+    """Per-phase kernel times (ms), mean over every batch since b2h_enable_timing(1)."""
+    buf = (C.c_float * 5)()
+    lib().b2h_mean_times(buf)
     return dict(zip(("filter_ms", "encode_ms", "finalize_ms", "decode_ms", "unfilter_ms"), list(buf)))

@@ -92,7 +92,8 @@ int unpack_chunks(const uint8_t* d_src, const int64_t* d_offsets, int32_t n, uin
 
 // Single-chunk stages of host-driven pipelines (chunks with user-registered filters / codecs):
 // one forward filter slot of P over the blocks of `pass` (0 all, 1 block 0, 2 blocks >= 1); the
-// built-in codec stage from an already-filtered image; one backward filter over a pass.  Device
+// built-in codec stage from an already-filtered image; one backward filter over a pass (0 all
+// blocks, 1 block 0, 2 blocks >= 1, 3 all blocks with DELTA decoded per block against itself).  Device
 // buffers need >= 256 bytes of slack.  decompress_batch(..., kDecRawStreams) decodes the streams
 // only, leaving the backward filters to the caller.
 int forward_filter_chunk(const CompressPlan& P, int slot, int pass, const uint8_t* d_in, uint8_t* d_out,
@@ -119,7 +120,8 @@ struct KernelTimes { float filter_ms, encode_ms, finalize_ms, decode_ms, unfilte
 void enable_timing(bool on);
 int debug_stream_results(void* host, int32_t n);
 int debug_decode_cycles(void* host, int32_t n);
-KernelTimes last_times();
+KernelTimes last_times();   // the latest batch (waits for its events)
+KernelTimes mean_times();   // mean over every batch since enable_timing(true)
 
 // Device bookkeeping
 int device_count();

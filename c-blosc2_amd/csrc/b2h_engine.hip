@@ -169,8 +169,6 @@ int device_count() {
 
 // ------------------------------------------------------------------------------- timing -----
 static bool g_timing = false;
-static KernelTimes g_times{};
-void enable_timing(bool on) { g_timing = on; }
 
 // Diagnostics: copy the per-stream encoder results of the last compression batch to the host.
 int debug_stream_results(void* host, int32_t n) {
@@ -181,7 +179,6 @@ int debug_stream_results(void* host, int32_t n) {
   HIPCHK(hipMemcpy(host, ws->res.p, (size_t)n * sizeof(StreamResult), hipMemcpyDeviceToHost));
   return n;
 }
-KernelTimes last_times() { return g_times; }
 
 // Diagnostics: per-stream decoder cycles of the last decompression batch (B2H_DECODE_DEBUG=1).
 static const bool g_ddebug = getenv("B2H_DECODE_DEBUG") != nullptr;
@@ -211,23 +208,55 @@ static int resident_slots(const void* fn, size_t lds, int block = 64) {
   return slots;
 }
 
+// Per-phase HIP events of every batch call since timing was enabled (a pool of event pairs,
+// reused from the start by each enable_timing(true)).  Recording never waits on the host: the
+// elapsed times are read only when asked for (last_times / mean_times), after the timed loop.
 struct EvPair {
-  hipEvent_t a = nullptr, b = nullptr;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> rec;
+  size_t used = 0;
+  bool open = false;
   void start(hipStream_t s) {
     if (!g_timing) return;
-    if (!a) { (void)hipEventCreate(&a); (void)hipEventCreate(&b); }
-    (void)hipEventRecord(a, s);
+    if (used == rec.size()) {
+      hipEvent_t a = nullptr, b = nullptr;
+      if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+      rec.push_back({a, b});
+    }
+    (void)hipEventRecord(rec[used].first, s);
+    open = true;
   }
-  void stop(hipStream_t s) { if (g_timing) (void)hipEventRecord(b, s); }
-  float ms() {
-    if (!g_timing || !a) return 0.f;
-    (void)hipEventSynchronize(b);
+  void stop(hipStream_t s) {
+    if (!g_timing || !open) return;
+    (void)hipEventRecord(rec[used].second, s);
+    used++;
+    open = false;
+  }
+  float elapsed(size_t i) {
     float t = 0.f;
-    (void)hipEventElapsedTime(&t, a, b);
+    (void)hipEventSynchronize(rec[i].second);
+    (void)hipEventElapsedTime(&t, rec[i].first, rec[i].second);
     return t;
   }
+  float last() { return used ? elapsed(used - 1) : 0.f; }
+  float mean() {
+    double t = 0;
+    for (size_t i = 0; i < used; i++) t += elapsed(i);
+    return used ? (float)(t / (double)used) : 0.f;
+  }
+  void reset() { used = 0; open = false; }
 };
 static EvPair ev_filter, ev_encode, ev_final, ev_decode, ev_unfilter;
+void enable_timing(bool on) {
+  g_timing = on;
+  if (on)
+    for (EvPair* e : {&ev_filter, &ev_encode, &ev_final, &ev_decode, &ev_unfilter}) e->reset();
+}
+KernelTimes last_times() {
+  return KernelTimes{ev_filter.last(), ev_encode.last(), ev_final.last(), ev_decode.last(), ev_unfilter.last()};
+}
+KernelTimes mean_times() {
+  return KernelTimes{ev_filter.mean(), ev_encode.mean(), ev_final.mean(), ev_decode.mean(), ev_unfilter.mean()};
+}
 
 // ================================================================ compression: geometry ====
 struct CGeom {
@@ -2226,11 +2255,6 @@ static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const ui
   }
   ev_final.stop(st);
   HIPCHK(hipGetLastError());
-  if (g_timing) {
-    g_times.filter_ms = ev_filter.ms();
-    g_times.encode_ms = ev_encode.ms();
-    g_times.finalize_ms = ev_final.ms();
-  }
   return 0;
 }
 
@@ -2293,7 +2317,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_dfilter_chunk(uint8_t filter,
     case kBitshuffle: block_bitunshuffle(in + off, out + off, bsize, ts, version); break;
     case kBytedelta: block_bytedelta_decode(in + off, out + off, bsize, meta ? meta : ts); break;
     case kDelta:
-      if (b == 0) block_delta_decode_first(in + off, out + off, bsize, ts);
+      if (b == 0 || pass == 3) block_delta_decode_first(in + off, out + off, bsize, ts);   // 3: each block self
       else block_delta_decode_rest(in + off, final_out, out + off, bsize, ts);
       break;
     default: break;
@@ -3033,10 +3057,6 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
   }
   k_dstatus<<<(n + 255) / 256, 256, 0, st>>>(ch, d_status, n);
   HIPCHK(hipGetLastError());
-  if (g_timing) {
-    g_times.decode_ms = ev_decode.ms();
-    g_times.unfilter_ms = ev_unfilter.ms();
-  }
   return 0;
 }
 

@@ -213,7 +213,7 @@ bool lookup_codec(int compcode, blosc2_codec* out);
 int compress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void* dest, int32_t destsize,
                     int32_t blocksize_in, bool sticky, bool extended);
 int decompress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void* dest, int32_t destsize,
-                      const std::vector<uint8_t>* mask);
+                      const std::vector<uint8_t>* mask, int mode);
 
 // Compress one host buffer through the engine (n = 1 batch).
 int compress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void* dest, int32_t destsize,
@@ -350,7 +350,7 @@ int decompress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void*
       for (int i = 0; i < 6; i++)
         if (!device_filter(fl[i]) && !lookup_filter(fl[i], &fi)) found = false;
       if (udcodec && !lookup_codec(s[22], &co)) found = false;
-      if (found) return decompress_hybrid(ctx, src, srcsize, dest, destsize, mask);
+      if (found) return decompress_hybrid(ctx, src, srcsize, dest, destsize, mask, mode);
     }
   }
   // The device reads what the reference may read: srcsize bytes (the blosc1 entry points pass
@@ -689,9 +689,12 @@ int compress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void*
 }
 
 int decompress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void* dest, int32_t destsize,
-                      const std::vector<uint8_t>* mask) {
+                      const std::vector<uint8_t>* mask, int mode) {
   const uint8_t* s = static_cast<const uint8_t*>(src);
   const int32_t nbytes = rd32(s + 4), cbytes = rd32(s + 12);
+  // lazy chunks (their blocks live in a frame) are not read here: init_from_header skips their
+  // cbytes <= srcsize check, and the copy below reads cbytes bytes of `src`
+  if (cbytes > srcsize) return BLOSC2_ERROR_INVALID_PARAM;
   int32_t bs = rd32(s + 8);
   const int ts = s[3];
   if (nbytes > 0 && bs > nbytes) bs = nbytes;
@@ -725,10 +728,12 @@ int decompress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, voi
       const int32_t ns = (split && bsize == bs) ? ts : 1, neblock = bsize / ns;
       int32_t pos = rd32(s + ovh + 4 * b);
       for (int32_t j = 0; j < ns; j++) {
-        if (pos < 0 || pos + 4 > srcsize) return BLOSC2_ERROR_READ_BUFFER;
+        if (pos < 0 || pos > srcsize - 4) return BLOSC2_ERROR_READ_BUFFER;
         const int32_t cs = rd32(s + pos);
         streams.push_back({pos, b * bs + j * neblock});
-        pos += 4 + (cs > 0 ? cs : (cs < 0 ? 1 : 0));
+        // 64-bit: a csize near INT32_MAX must not wrap the cursor back into the buffer
+        const int64_t next = (int64_t)pos + 4 + (cs > 0 ? cs : (cs < 0 ? 1 : 0));
+        pos = next > srcsize ? srcsize : (int32_t)next;
         (void)neblock;
       }
     }
@@ -746,7 +751,7 @@ int decompress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, voi
         memset(o, -cs, (size_t)neblock);
         return 0;
       }
-      if (pos + 4 + cs > srcsize) return (int)BLOSC2_ERROR_READ_BUFFER;
+      if (cs > srcsize - pos - 4) return (int)BLOSC2_ERROR_READ_BUFFER;   // subtraction form: no int32 overflow
       if (cs == neblock) { memcpy(o, in, (size_t)neblock); return 0; }
       blosc2_dparams dpl = dp;
       const int r = codec.decoder(in, cs, o, neblock, (uint8_t)cmeta, &dpl, src);
@@ -776,7 +781,13 @@ int decompress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, voi
   for (int i = 0; i < 6; i++) has_delta |= filters[i] == BLOSC_DELTA;
   std::vector<uint8_t> hs, hd;
   uint8_t* fin = hb.out.u8();
-  for (int pass = (has_delta && nblocks > 1) ? 1 : 0; pass <= ((has_delta && nblocks > 1) ? 2 : 0); pass++) {
+  // DELTA: block 0 first, then the others against the final block 0 (blosc/blosc2.c:1505-1529);
+  // kDecDeltaSelf (getitem / decompress_block): every block un-deltas against itself, as blosc_d
+  // does with dest_offset 0 -- one pass, backward_filter_chunk's pass 3
+  const bool self = (mode & b2h::kDecDeltaSelf) != 0;
+  const bool two = has_delta && nblocks > 1 && !self;
+  const int pfirst = two ? 1 : (self && has_delta ? 3 : 0), plast = two ? 2 : pfirst;
+  for (int pass = pfirst; pass <= plast; pass++) {
     uint8_t *cur = unf, *nxt = hb.c.u8();
     const int32_t b0 = pass == 2 ? 1 : 0, b1 = pass == 1 ? 1 : nblocks;
     const int64_t lo = (int64_t)b0 * bs, hi = std::min<int64_t>((int64_t)b1 * bs, nbytes);
@@ -1584,6 +1595,10 @@ int b2h_set_blosclz_mode(int mode) { return b2h::set_blosclz_mode(mode); }
 void b2h_enable_timing(int on) { b2h::enable_timing(on != 0); }
 void b2h_last_times(float out[5]) {
   const b2h::KernelTimes t = b2h::last_times();
+  out[0] = t.filter_ms; out[1] = t.encode_ms; out[2] = t.finalize_ms; out[3] = t.decode_ms; out[4] = t.unfilter_ms;
+}
+void b2h_mean_times(float out[5]) {
+  const b2h::KernelTimes t = b2h::mean_times();
   out[0] = t.filter_ms; out[1] = t.encode_ms; out[2] = t.finalize_ms; out[3] = t.decode_ms; out[4] = t.unfilter_ms;
 }
 const char* b2h_last_error(void) { return b2h::last_error(); }

@@ -54,6 +54,17 @@ def _all_gather(t, group):
     return [o.to(t.device) for o in outs]
 
 
+def _agree(ok, group):
+    """All ranks agree on success (a MIN all-reduce of one flag): a rank whose chunks failed must
+    not leave the collective sequence alone -- the others would block in their next collective
+    until the process-group timeout.  Every rank then raises together."""
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    if dist.get_backend(group) != "gloo":
+        flag = flag.cuda()
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    return bool(flag.item())
+
+
 def _p2p(sends, recvs, group):
     """Grouped point-to-point exchange: sends = [(tensor, dst)], recvs = [(tensor, src)].  Empty
     tensors are skipped (both sides know every size).  Receives land in the given tensors."""
@@ -147,6 +158,9 @@ def scatter_chunks(full, chunk_nbytes, nchunks, device, root=0, group=None):
             dist.scatter(recv, parts, src=root, group=group)
         return recv
     recv = torch.empty((hi - lo) * chunk_nbytes, dtype=torch.uint8, device=device)
+    # every rank joins one collective first: with NCCL a group's first P2P batch must include all
+    # ranks, and a rank with an empty shard posts no send / receive at all
+    _agree(True, group)
     if rank == root:
         recv.copy_(full[lo * chunk_nbytes:hi * chunk_nbytes])
         _p2p([(full[a * chunk_nbytes:b * chunk_nbytes], r) for r, (a, b) in enumerate(spans) if r != root], [], group)
@@ -266,10 +280,16 @@ def compress_schunk(full, chunk_nbytes, nchunks, cparams, device, compress_batch
     n = hi - lo
     comp = torch.empty(max(1, n) * stride, dtype=torch.uint8, device=device)
     cbytes = torch.zeros(max(1, n), dtype=torch.int32, device=device)
+    err = None
     if n:
-        compress_batch(cparams, local, chunk_nbytes, n, comp, stride, cap, cbytes)
-        if not bool((cbytes[:n] > 0).all()):   # 0: did not fit (cannot happen at cap = nbytes + 32)
-            raise RuntimeError(f"rank {rank}: a chunk failed to compress: {cbytes[:n].min().item()}")
+        try:
+            compress_batch(cparams, local, chunk_nbytes, n, comp, stride, cap, cbytes)
+            if not bool((cbytes[:n] > 0).all()):   # 0: did not fit (cannot happen at cap = nbytes + 32)
+                err = f"rank {rank}: a chunk failed to compress: {cbytes[:n].min().item()}"
+        except RuntimeError as e:
+            err = f"rank {rank}: {e}"
+    if not _agree(err is None, group):   # raise on every rank together, before the gather
+        raise RuntimeError(err or f"rank {rank}: another rank failed to compress its chunks")
     return gather_compressed(comp, stride, cbytes[:n], nchunks, root, group)
 
 
@@ -282,8 +302,14 @@ def decompress_schunk(frame, offsets, chunk_nbytes, nchunks, device, decompress_
     comp, cbytes = scatter_compressed(frame, offsets, nchunks, stride, device, root, group)
     n = hi - lo
     out = torch.empty(max(1, n) * chunk_nbytes, dtype=torch.uint8, device=device)
+    err = None
     if n:
-        status = decompress_batch(comp, stride, cbytes, n, out, chunk_nbytes)
-        if status is not None and not bool((status == chunk_nbytes).all()):
-            raise RuntimeError(f"rank {rank}: decompression status {status.min().item()}")
+        try:
+            status = decompress_batch(comp, stride, cbytes, n, out, chunk_nbytes)
+            if status is not None and not bool((status == chunk_nbytes).all()):
+                err = f"rank {rank}: decompression status {status.min().item()}"
+        except RuntimeError as e:
+            err = f"rank {rank}: {e}"
+    if not _agree(err is None, group):
+        raise RuntimeError(err or f"rank {rank}: another rank failed to decompress its chunks")
     return gather_chunks(out[:n * chunk_nbytes], chunk_nbytes, nchunks, root, group)

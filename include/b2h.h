@@ -127,10 +127,12 @@ BLOSC_EXPORT int b2h_frame_get_sparse_buffer(b2h_frame *frame, int64_t ncoords, 
  * Any other value only queries. */
 BLOSC_EXPORT int b2h_set_blosclz_mode(int mode);
 
-/* Per-phase HIP-event timings of the last batch on this process (ms): filter, encode, finalize,
- * decode, unfilter.  Enabling adds event records only (no extra synchronisation until read). */
+/* Per-phase HIP-event timings (ms): filter, encode, finalize, decode, unfilter.  Enabling
+ * (re)starts the log and adds event records only: the batch calls never wait on the host; the
+ * times are read after the timed work.  last: the latest batch; mean: every batch since enabled. */
 BLOSC_EXPORT void b2h_enable_timing(int on);
 BLOSC_EXPORT void b2h_last_times(float out[5]);
+BLOSC_EXPORT void b2h_mean_times(float out[5]);
 
 BLOSC_EXPORT const char *b2h_last_error(void);
 /* Diagnostics: per-stream encoder records of the last compression batch on this device

@@ -116,3 +116,40 @@ def test_shard_ranges_cover():
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
             assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
+
+
+def _failing_worker(rank, world, port, q):
+    """Rank 1's chunk engine reports a chunk that did not fit (cbytes 0)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def comp(cparams, src, chunk_nbytes, n, out, stride, cap, cbytes):
+        _oracle_compress_batch(cparams, src, chunk_nbytes, n, out, stride, cap, cbytes)
+        if rank == 1:
+            cbytes[0] = 0
+
+    try:
+        full = torch.from_numpy(_data(4)) if rank == 0 else None
+        SD.compress_schunk(full, CHUNK, 4, KW, torch.device("cpu"), comp)
+        q.put((rank, "no error"))
+    except RuntimeError as e:
+        q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_schunk_failure_on_one_rank_raises_everywhere():
+    """a rank whose chunk fails must not leave the others blocked in the gather: all
+    ranks agree on the failure (one MIN all-reduce) and raise together, well before any timeout."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_failing_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert "failed to compress" in got[1], got
+    assert "another rank failed" in got[0], got
