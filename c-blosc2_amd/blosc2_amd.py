@@ -38,8 +38,19 @@ class DParams(C.Structure):
                 ("postparams", C.c_void_p), ("typesize", C.c_int32)]
 
 
+B2H_CODEC_PARAMS_MAGIC = 0x68623262
+EXACT, FAST = 0, 1   # BloscLZ encoder modes (include/b2h.h b2h_codec_params)
+
+
+class CodecParams(C.Structure):
+    """b2h_codec_params (include/b2h.h): a context's BloscLZ encoder, carried by cparams.codec_params."""
+    _fields_ = [("magic", C.c_uint32), ("blosclz_mode", C.c_int32)]
+
+
 def cparams(clevel=5, typesize=8, filters=(0, 0, 0, 0, 0, SHUFFLE), filters_meta=(0,) * 6,
-            blocksize=0, splitmode=FORWARD_COMPAT_SPLIT, compcode=0, nthreads=1, use_dict=0):
+            blocksize=0, splitmode=FORWARD_COMPAT_SPLIT, compcode=0, nthreads=1, use_dict=0, lz_mode=None):
+    """blosc2_cparams; lz_mode (EXACT / FAST) selects the BloscLZ encoder of this context only
+    (None: the process default, b2h_set_blosclz_mode)."""
     p = CParams()
     p.compcode, p.clevel, p.typesize, p.nthreads = compcode, clevel, typesize, nthreads
     p.use_dict = use_dict
@@ -47,6 +58,10 @@ def cparams(clevel=5, typesize=8, filters=(0, 0, 0, 0, 0, SHUFFLE), filters_meta
     for i in range(MAX_FILTERS):
         p.filters[i] = filters[i]
         p.filters_meta[i] = filters_meta[i] & 0xFF
+    if lz_mode is not None:
+        cpp = CodecParams(B2H_CODEC_PARAMS_MAGIC, lz_mode)
+        p._codec_params_keep = cpp   # kept alive with the struct that points at it
+        p.codec_params = C.cast(C.pointer(cpp), C.c_void_p)
     return p
 
 

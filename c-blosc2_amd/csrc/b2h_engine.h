@@ -36,6 +36,7 @@ struct CompressPlan {
   int32_t compcode;        // BLOSC_BLOSCLZ (0) or BLOSC_LZ4 (1)
   bool use_dict;           // LZ4 with a dictionary requested and in force (clevel > 0, not memcpyed)
   int32_t dict_size;       // its size (0: the reference falls back to no dictionary)
+  int32_t lz_mode = -1;    // BloscLZ encoder: 0 exact, 1 fast, -1 the process default (set_blosclz_mode)
 };
 
 // Fill the plan from cparams-level values the way blosc2_compress_ctx does (initialize_context_
@@ -112,8 +113,11 @@ int shuffle_dev(int32_t typesize, int32_t nbytes, const uint8_t* d_src, uint8_t*
 int bitshuffle_dev(int32_t typesize, int32_t nbytes, const uint8_t* d_src, uint8_t* d_dst, bool inverse,
                    uint8_t format_version, hipStream_t s);
 
-// BloscLZ encoder mode, process-wide: 0 exact (default), 1 fast.  Returns the previous mode.
+// BloscLZ encoder mode, process-wide default: 0 exact (default), 1 fast.  Returns the previous
+// mode.  A plan's own lz_mode (a context's cparams.codec_params, see include/b2h.h) overrides it.
 int set_blosclz_mode(int mode);
+// The BloscLZ mode a cparams.codec_params selects (b2h_codec_params), or -1 (none / not ours).
+int codec_params_lz_mode(const void* codec_params);
 
 // Kernel timing hook for bench.py (HIP events around the dominant kernels of the last batch).
 struct KernelTimes { float filter_ms, encode_ms, finalize_ms, decode_ms, unfilter_ms; };

@@ -263,6 +263,7 @@ struct CGeom {
   int32_t nbytes, bs, nblocks, leftover, spb, nsc, neblock, ts, destsize, clevel, overhead, compcode;
   int32_t dict_size;   // LZ4 dictionary section [int32 size | bytes] after the bstarts (0: none)
   int32_t front;   // encoder pull schedule (pull_to_stream), 0 = stream order
+  int32_t lzmode;  // BloscLZ encoder of this batch: 0 exact, 1 fast (the plan's, else the process default)
   int64_t src_stride, wstride, dst_stride;
 };
 
@@ -414,37 +415,89 @@ __global__ __launch_bounds__(1024) void k_plane_cost(CGeom g, const StreamResult
   }
 }
 
+// A wave-uniform copy of an LDS-resident value (word by word through readfirstlane).
+template <typename T>
+__device__ __forceinline__ T lds_uniform(const B2H_LDS T* p) {
+  static_assert(sizeof(T) % 4 == 0, "word-sized fields only");
+  union U {
+    T v;
+    uint32_t w[sizeof(T) / 4];
+    __device__ U() {}
+  } u;
+  const volatile B2H_LDS uint32_t* q = (const volatile B2H_LDS uint32_t*)p;
+#pragma unroll
+  for (size_t k = 0; k < sizeof(T) / 4; k++) u.w[k] = __builtin_amdgcn_readfirstlane(q[k]);
+  return u.v;
+}
+template <typename T>
+__device__ __forceinline__ void lds_store(B2H_LDS T* p, const T& v) {
+  static_assert(sizeof(T) % 4 == 0, "word-sized fields only");
+  union U {
+    T v;
+    uint32_t w[sizeof(T) / 4];
+    __device__ U() {}
+  } u;
+  u.v = v;
+  B2H_LDS uint32_t* q = (B2H_LDS uint32_t*)p;
+#pragma unroll
+  for (size_t k = 0; k < sizeof(T) / 4; k++) q[k] = u.w[k];
+}
+// The exact encoder's arguments, staged in LDS at launch (see FusedArgs below: kept in kernel
+// arguments they stayed live in SGPRs through the encode and ~100 SGPRs spilled into VGPR lanes).
+struct EncArgs {
+  CGeom g;
+  const uint8_t* filt;
+  uint8_t* sbuf;
+  StreamResult* res;
+  int32_t* next;
+  const int32_t* porder;
+  int32_t nstreams_total, pad;
+};
+
 template <typename TAB>
-__device__ __forceinline__ void encode_loop(const CGeom& g, TAB htab, B2H_LDS uint32_t* dbits, B2H_LDS uint8_t* oring,
-                                            const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
-                                            StreamResult* __restrict__ res, int32_t nstreams_total,
-                                            int32_t* __restrict__ next, const int32_t* __restrict__ porder) {
+__device__ __forceinline__ void encode_loop(const B2H_LDS EncArgs* A, TAB htab, B2H_LDS uint32_t* dbits,
+                                            B2H_LDS uint8_t* oring) {
   for (;;) {
     // branch-free grab: every lane takes part (lane 0 adds 1, the others 0), so no divergent
     // region sits between the atomic and the broadcast -- with a lane-0 branch the structurizer
     // let lanes 1..63 run ahead into the next iteration and re-read a stale index.
-    const int32_t i = __builtin_amdgcn_readfirstlane(atomicAdd(next, lane_id() == 0 ? 1 : 0));
-    if (i >= nstreams_total) return;
-    const int32_t s = __builtin_amdgcn_readfirstlane(pull_to_stream(g, porder, g.front, i, nstreams_total));
-    const int32_t c = s / g.nsc, l = s - c * g.nsc;
-    int32_t off, len, blk;
-    stream_locate(g, l, &off, &len, &blk);
-    gin_t in = (gin_t)(filt + (int64_t)c * g.wstride + off);
-    gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
+    // (a global-address-space atomic: the backend's atomic optimizer folds the 64 lanes into one;
+    // through the generic pointer read back from LDS it issued 64 flat atomics per grab, and
+    // ~4 M serialised RMWs on the one counter doubled the T encode)
+    const int32_t i = __builtin_amdgcn_readfirstlane(__hip_atomic_fetch_add(
+        (B2H_GLB int32_t*)lds_uniform(&A->next), lane_id() == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const int32_t ntot = lds_uniform(&A->nstreams_total);
+    if (i >= ntot) return;
+    int32_t s, len, clevel;
+    gin_t in;
+    gout_t out;
+    bool runs;
+    {
+      const CGeom g = lds_uniform(&A->g);
+      s = __builtin_amdgcn_readfirstlane(pull_to_stream(g, lds_uniform(&A->porder), g.front, i, ntot));
+      const int32_t c = s / g.nsc, l = s - c * g.nsc;
+      int32_t off, blk;
+      stream_locate(g, l, &off, &len, &blk);
+      in = (gin_t)(lds_uniform(&A->filt) + (int64_t)c * g.wstride + off);
+      out = (gout_t)(lds_uniform(&A->sbuf) + (int64_t)c * g.wstride + off);
+      clevel = g.clevel;
+      runs = g.overhead == kHdrExt;
+    }
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide time base
-    StreamResult r = encode_stream<TAB>(in, len, g.clevel, out, htab, dbits, oring, g.overhead == kHdrExt);
+    StreamResult r = encode_stream<TAB>(in, len, clevel, out, htab, dbits, oring, runs);
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     if (TAB::kGlobal) r.windows |= 1 << 30;   // diagnostics: the stream ran on a global-table wave
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
-    if (lane_id() == 0) res[s] = r;
+    if (lane_id() == 0) lds_uniform(&A->res)[s] = r;
   }
 }
 
 __host__ __device__ constexpr size_t enc_wave_lds(int hashlog) { return ((size_t(1) << hashlog) >> 3) + kOutRing; }
 template <typename POS>
 __host__ __device__ constexpr size_t enc_wg_lds(int hashlog, int nlds, int nglb) {
-  return (size_t)nlds * (sizeof(POS) << hashlog) + (size_t)(nlds + nglb) * enc_wave_lds(hashlog);
+  return (size_t)nlds * (sizeof(POS) << hashlog) + (size_t)(nlds + nglb) * enc_wave_lds(hashlog) +
+         ((sizeof(EncArgs) + 15) & ~size_t(15));
 }
 
 template <typename POS, int NLDS, int NGLB>
@@ -456,17 +509,28 @@ __global__ __launch_bounds__(64 * (NLDS + NGLB)) void k_encode(CGeom g, const ui
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const size_t tabsz = sizeof(POS) << hashlog;
+  B2H_LDS EncArgs* A = (B2H_LDS EncArgs*)(smem + NLDS * tabsz + (NLDS + NGLB) * enc_wave_lds(hashlog));
+  if (threadIdx.x == 0) {
+    lds_store(&A->g, g);
+    A->filt = filt;
+    A->sbuf = sbuf;
+    A->res = res;
+    A->next = next;
+    A->porder = porder;
+    A->nstreams_total = nstreams_total;
+  }
+  __syncthreads();
   B2H_LDS uint8_t* mine = (B2H_LDS uint8_t*)(smem + NLDS * tabsz + w * enc_wave_lds(hashlog));
   B2H_LDS uint32_t* dbits = (B2H_LDS uint32_t*)mine;
   B2H_LDS uint8_t* oring = mine + ((size_t(1) << hashlog) >> 3);
   if (NLDS > 0 && w < NLDS) {
     LdsTab<POS> t;
     t.t = (volatile B2H_LDS POS*)(smem + w * tabsz);
-    encode_loop(g, t, dbits, oring, filt, sbuf, res, nstreams_total, next, porder);
+    encode_loop(A, t, dbits, oring);
   } else if (NGLB > 0) {
     GlbTab<POS> t;
     t.t = (B2H_GLB POS*)(gtab + (((size_t)blockIdx.x * NGLB + (w - NLDS)) << hashlog));
-    encode_loop(g, t, dbits, oring, filt, sbuf, res, nstreams_total, next, porder);
+    encode_loop(A, t, dbits, oring);
   }
 }
 
@@ -1286,10 +1350,12 @@ __device__ int32_t wait_nonzero(int32_t* p, int32_t* tmo) {
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 #define FUSE_TRACE(code, v)                                                                                  \
   do {                                                                                                     \
-    if (f.trace && threadIdx.x == 0)                                                                        \
-      __hip_atomic_store(f.trace + blockIdx.x, (int32_t)((code) | ((v) << 4)), __ATOMIC_RELAXED,            \
+    int32_t* tr_ = FUSE_TRACE_PTR;                                                                         \
+    if (tr_ && threadIdx.x == 0)                                                                            \
+      __hip_atomic_store(tr_ + blockIdx.x, (int32_t)((code) | ((v) << 4)), __ATOMIC_RELAXED,                \
                          __HIP_MEMORY_SCOPE_SYSTEM);                                                        \
   } while (0)
+#define FUSE_TRACE_PTR f.trace
 
 // Typesize-4 byte shuffle of one block by the workgroup (bsize % 64 == 0, s and d 16-aligned):
 // 16 elements per lane step, 4 x 16 B loads, a 4x4 byte transpose per 4 elements (v_perm), one
@@ -1332,24 +1398,54 @@ __device__ void shuffle4_block_wt(const uint8_t* __restrict__ s, uint8_t* __rest
   }
 }
 
+// The fused kernel's arguments, staged in LDS at launch and read back (as wave-uniform values) in
+// each phase that needs them.  Kept in kernel arguments, the ~60 words of geometry, sync pointers
+// and strides stayed live in SGPRs through the whole launch, the encoder's loops ran out of SGPRs
+// and the compiler spilled ~170 of them into VGPR lanes (a v_readlane / v_writelane per reload in
+// the tile loops).  A phase's copy is dead once it ends; the encode's barriers end every live range.
+struct FusedArgs {
+  CGeom g;
+  EncFuse f;
+  const uint8_t* filt;
+  uint8_t* sbuf;
+  StreamResult* res;
+  int32_t* next;
+  const int32_t* porder;
+  int32_t nstreams_total, tablog;
+};
+__host__ __device__ constexpr size_t fused_lds(size_t pos_bytes, int tablog) {
+  return fast_lds(pos_bytes, tablog) + ((sizeof(FusedArgs) + 15) & ~size_t(15));
+}
+
+#undef FUSE_TRACE_PTR
+#define FUSE_TRACE_PTR lds_uniform(&A->f.trace)
 template <typename POS>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4, 8)))   // as k_encode_fast
-void k_encode_fast_fused(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
-                         StreamResult* __restrict__ res, int32_t nstreams_total, int32_t* __restrict__ next, int tablog,
-                         const int32_t* __restrict__ porder, EncFuse f) {
+void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint8_t* __restrict__ sbuf_arg,
+                         StreamResult* __restrict__ res_arg, int32_t nstreams_total_arg, int32_t* __restrict__ next_arg,
+                         int tablog_arg, const int32_t* __restrict__ porder_arg, EncFuse f_arg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int tablog0 = tablog_arg;
   B2H_LDS uint8_t* tab = (B2H_LDS uint8_t*)smem;
-  B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + (sizeof(POS) << tablog));
-  B2H_LDS FastShared* sh = (B2H_LDS FastShared*)(smem + (sizeof(POS) << tablog) + kOutRing);
+  B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + (sizeof(POS) << tablog0));
+  B2H_LDS FastShared* sh = (B2H_LDS FastShared*)(smem + (sizeof(POS) << tablog0) + kOutRing);
+  B2H_LDS FusedArgs* A = (B2H_LDS FusedArgs*)(smem + fast_lds(sizeof(POS), tablog0));
+  if (threadIdx.x == 0) {
+    lds_store(&A->g, g_arg);
+    lds_store(&A->f, f_arg);
+    A->filt = filt_arg;
+    A->sbuf = sbuf_arg;
+    A->res = res_arg;
+    A->next = next_arg;
+    A->porder = porder_arg;
+    A->nstreams_total = nstreams_total_arg;
+    A->tablog = tablog_arg;
+  }
+  __syncthreads();
   const bool matcher = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
-  const int32_t nblk = f.nchunks * g.nblocks;
-  int32_t* blk_ready = f.sync + kFuseHdr;
-  int32_t* chunk_cnt = blk_ready + nblk;
-  int32_t* ready = chunk_cnt + f.nchunks;
-  int32_t* tmo = f.sync + 4;
   // wave priority (B2H_FUSE bit 64, default): the parser -- the tile's latency chain -- issues
   // ahead of the matchers sharing its SIMD (T encode 18.0 -> 17.6 ms; the matcher first: 19.3)
-  if ((f.mode_bits & 64) && !matcher) __builtin_amdgcn_s_setprio(2);
+  if ((lds_uniform(&A->f.mode_bits) & 64) && !matcher) __builtin_amdgcn_s_setprio(2);
   // lane 0 of the workgroup computes v, everyone gets it
   auto bcast = [&](int32_t v) -> int32_t {
     if (threadIdx.x == 0) sh->bcast = v;
@@ -1360,30 +1456,36 @@ void k_encode_fast_fused(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __r
   };
   // scatter item k: streams [j0, j0 + kFuseSpi) of the chunk in ready slot k / ipc (the publish
   // poll, ONE agent acquire for the item, then plain loads of the placements and payloads)
-  const int32_t ipc = (g.nsc + kFuseSpi - 1) / kFuseSpi;   // items per chunk
-  const int32_t nitems = f.nchunks * ipc;
   auto scatter_item = [&](int32_t k) {
+    const CGeom g = lds_uniform(&A->g);
+    const EncFuse f = lds_uniform(&A->f);
+    const int32_t ipc = (g.nsc + kFuseSpi - 1) / kFuseSpi;   // items per chunk
+    int32_t* ready = f.sync + kFuseHdr + f.nchunks * g.nblocks + f.nchunks;
     const int32_t slot = k / ipc, j0 = (k - slot * ipc) * kFuseSpi;
     int32_t v = 0;
     FUSE_TRACE(1, k);
     if (threadIdx.x == 0) {
-      v = wait_nonzero(ready + slot, tmo);
+      v = wait_nonzero(ready + slot, f.sync + 4);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       drain_stores();
     }
     v = bcast(v);
     if (v <= 0) return;
+    const CGeom g2 = lds_uniform(&A->g);   // re-read after the barriers of bcast
+    const EncFuse f2 = lds_uniform(&A->f);
+    const uint8_t* filt = lds_uniform(&A->filt);
+    const uint8_t* sbuf = lds_uniform(&A->sbuf);
     const int32_t c = v - 1;
-    if (__builtin_amdgcn_readfirstlane(f.mode[c]) != 0) return;
-    uint8_t* d = f.dst + (int64_t)c * g.dst_stride;
+    if (__builtin_amdgcn_readfirstlane(f2.mode[c]) != 0) return;
+    uint8_t* d = f2.dst + (int64_t)c * g2.dst_stride;
     const int32_t wv = threadIdx.x >> 6;
-    for (int32_t l = j0; l < min(j0 + kFuseSpi, g.nsc); l++) {
-      const int32_t s = c * g.nsc + l;
+    for (int32_t l = j0; l < min(j0 + kFuseSpi, g2.nsc); l++) {
+      const int32_t s = c * g2.nsc + l;
       Place pl;
-      pl.off = __builtin_amdgcn_readfirstlane(f.place[s].off);
-      pl.csize = __builtin_amdgcn_readfirstlane(f.place[s].csize);
+      pl.off = __builtin_amdgcn_readfirstlane(f2.place[s].off);
+      pl.csize = __builtin_amdgcn_readfirstlane(f2.place[s].csize);
       int32_t off, len, blk;
-      stream_locate(g, l, &off, &len, &blk);
+      stream_locate(g2, l, &off, &len, &blk);
       if (threadIdx.x == 0) {
         const uint32_t w = (uint32_t)pl.csize;
         uint8_t* q = d + pl.off - 4;
@@ -1391,11 +1493,11 @@ void k_encode_fast_fused(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __r
         if (pl.csize < 0) d[pl.off] = 0x1;   // run-length token
       }
       if (pl.csize <= 0) continue;
-      const uint8_t* src = (pl.csize == len ? filt : sbuf) + (int64_t)c * g.wstride + off;
+      const uint8_t* src = (pl.csize == len ? filt : sbuf) + (int64_t)c * g2.wstride + off;
       const int32_t q = ((pl.csize + 1) / 2 + 15) & ~15;
       const int32_t a = min(pl.csize, wv * q), b = min(pl.csize, a + q);
       if (b > a) {
-        if ((f.mode_bits & 32) || !aligned16(src + a)) wave_copy((gout_t)(d + pl.off + a), (gin_t)(src + a), b - a);
+        if ((f2.mode_bits & 32) || !aligned16(src + a)) wave_copy((gout_t)(d + pl.off + a), (gin_t)(src + a), b - a);
         else wave_copy_a16((gout_t)(d + pl.off + a), (gin_t)(src + a), b - a);
       }
     }
@@ -1405,11 +1507,12 @@ void k_encode_fast_fused(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __r
   // a `break` after lane-0-only code lets the compiler structurize the loop as divergent, and its
   // waves then meet different barriers (seen: a workgroup re-shuffling one block forever).
   auto try_claim_item = [&]() -> int32_t {   // lane 0
-    const int32_t pub = rd_agent(f.sync + 3);
-    int32_t cur = rd_agent(f.sync + 1);
+    int32_t* sync = lds_uniform(&A->f.sync);
+    const int32_t pub = rd_agent(sync + 3);
+    int32_t cur = rd_agent(sync + 1);
     for (int tries = 0; tries < 8 && cur < pub; tries++) {
       const int32_t want = cur;
-      if (__hip_atomic_compare_exchange_strong((gi32_t)(f.sync + 1), &cur, want + 1, __ATOMIC_RELAXED,
+      if (__hip_atomic_compare_exchange_strong((gi32_t)(sync + 1), &cur, want + 1, __ATOMIC_RELAXED,
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
         return want;
     }
@@ -1424,61 +1527,87 @@ void k_encode_fast_fused(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __r
   };
   // lane 0: claim the next block to shuffle while the claims are behind `target`, else -1
   auto claim_block = [&](int32_t target) -> int32_t {
-    return rd_agent(f.sync) < target ? add_agent(f.sync, 1) : -1;
+    int32_t* sync = lds_uniform(&A->f.sync);
+    return rd_agent(sync) < target ? add_agent(sync, 1) : -1;
   };
-  int32_t i = bcast(threadIdx.x == 0 ? atomicAdd(next, 1) : 0);
-  while (i < nstreams_total) {
+  int32_t i = bcast(threadIdx.x == 0 ? atomicAdd(lds_uniform(&A->next), 1) : 0);
+  while (i < lds_uniform(&A->nstreams_total)) {
     FUSE_TRACE(3, i);
-    const int32_t s = __builtin_amdgcn_readfirstlane(pull_to_stream(g, porder, g.front, i, nstreams_total));
-    const int32_t c = s / g.nsc, l = s - c * g.nsc;
-    int32_t off, len, blk;
-    stream_locate(g, l, &off, &len, &blk);
-    if (f.raw) {
-      const int32_t gb = c * g.nblocks + blk, target = min(gb + 1 + f.lead, nblk);
-      int32_t k = bcast(threadIdx.x == 0 ? claim_block(target) : -1);
-      while (k >= 0 && k < nblk) {   // keep the shuffle claims ahead of the streams
-        FUSE_TRACE(4, k);
-        const int32_t cc = k / g.nblocks, b = k - cc * g.nblocks;
-        const int32_t bsize = (b == g.nblocks - 1 && g.leftover) ? g.leftover : g.bs;
-        shuffle4_block_wt(f.raw + (int64_t)cc * f.raw_stride + (int64_t)b * g.bs,
-                          f.filt + (int64_t)cc * g.wstride + (int64_t)b * g.bs, bsize);
-        drain_stores();
-        __syncthreads();
-        int32_t nk = -1;
-        if (threadIdx.x == 0) {
-          st_agent(blk_ready + k, 1);
-          nk = claim_block(target);
+    int32_t s, c;
+    gin_t in;
+    gout_t out;
+    int32_t len, clevel, tablog;
+    bool runs;
+    {
+      const CGeom g = lds_uniform(&A->g);
+      s = __builtin_amdgcn_readfirstlane(pull_to_stream(g, lds_uniform(&A->porder), g.front, i,
+                                                         lds_uniform(&A->nstreams_total)));
+      c = s / g.nsc;
+      const int32_t l = s - c * g.nsc;
+      int32_t off, blk;
+      stream_locate(g, l, &off, &len, &blk);
+      const EncFuse f = lds_uniform(&A->f);
+      if (f.raw) {
+        const int32_t nblk = f.nchunks * g.nblocks;
+        const int32_t gb = c * g.nblocks + blk, target = min(gb + 1 + f.lead, nblk);
+        int32_t k = bcast(threadIdx.x == 0 ? claim_block(target) : -1);
+        while (k >= 0 && k < nblk) {   // keep the shuffle claims ahead of the streams
+          FUSE_TRACE(4, k);
+          const CGeom gk = lds_uniform(&A->g);
+          const EncFuse fk = lds_uniform(&A->f);
+          const int32_t cc = k / gk.nblocks, b = k - cc * gk.nblocks;
+          const int32_t bsize = (b == gk.nblocks - 1 && gk.leftover) ? gk.leftover : gk.bs;
+          shuffle4_block_wt(fk.raw + (int64_t)cc * fk.raw_stride + (int64_t)b * gk.bs,
+                            fk.filt + (int64_t)cc * gk.wstride + (int64_t)b * gk.bs, bsize);
+          drain_stores();
+          __syncthreads();
+          int32_t nk = -1;
+          if (threadIdx.x == 0) {
+            st_agent(fk.sync + kFuseHdr + k, 1);
+            nk = claim_block(target);
+          }
+          k = bcast(nk);
         }
-        k = bcast(nk);
+        FUSE_TRACE(5, gb);
+        if (threadIdx.x == 0) {
+          int32_t* sync = lds_uniform(&A->f.sync);
+          (void)wait_nonzero(sync + kFuseHdr + gb, sync + 4);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          drain_stores();
+        }
+        __syncthreads();
       }
-      FUSE_TRACE(5, gb);
-      if (threadIdx.x == 0) {
-        (void)wait_nonzero(blk_ready + gb, tmo);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        drain_stores();
-      }
-      __syncthreads();
+      const CGeom g2 = lds_uniform(&A->g);
+      in = (gin_t)(lds_uniform(&A->filt) + (int64_t)c * g2.wstride + off);
+      out = (gout_t)(lds_uniform(&A->sbuf) + (int64_t)c * g2.wstride + off);
+      clevel = g2.clevel;
+      runs = g2.overhead == kHdrExt;
+      tablog = lds_uniform(&A->tablog);
     }
-    gin_t in = (gin_t)(filt + (int64_t)c * g.wstride + off);
-    gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
     FUSE_TRACE(6, s);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
-    StreamResult r = encode_stream_fast<POS, true>(in, len, g.clevel, out, tab, tablog, oring, sh,
-                                                   g.overhead == kHdrExt, matcher);
+    StreamResult r = encode_stream_fast<POS, true>(in, len, clevel, out, tab, tablog, oring, sh, runs, matcher);
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
     if (!matcher && lane_id() == 0) {
-      res[s] = r;
-      st_agent(f.fin + 3 * s, r.kind);
-      st_agent(f.fin + 3 * s + 1, r.size);
-      st_agent(f.fin + 3 * s + 2, r.peak);
+      int32_t* fin = lds_uniform(&A->f.fin);
+      lds_uniform(&A->res)[s] = r;
+      st_agent(fin + 3 * s, r.kind);
+      st_agent(fin + 3 * s + 1, r.size);
+      st_agent(fin + 3 * s + 2, r.peak);
     }
     FUSE_TRACE(7, s);
     drain_stores();
     __syncthreads();
-    const int32_t done = bcast(threadIdx.x == 0 ? add_agent(chunk_cnt + c, 1) : 0);
-    if (done == g.nsc - 1) {   // last stream of chunk c: finalize it (its stream results -> LDS)
+    int32_t done;
+    {
+      const CGeom g = lds_uniform(&A->g);
+      const EncFuse f = lds_uniform(&A->f);
+      int32_t* chunk_cnt = f.sync + kFuseHdr + f.nchunks * g.nblocks;
+      done = bcast(threadIdx.x == 0 ? add_agent(chunk_cnt + c, 1) : 0);
+    }
+    if (done == lds_uniform(&A->g.nsc) - 1) {   // last stream of chunk c: finalize it (its stream results -> LDS)
       B2H_LDS int32_t* fl = (B2H_LDS int32_t*)tab;
       FUSE_TRACE(8, c);
       if (threadIdx.x == 0) {   // the counter add returned: ONE acquire, then plain loads
@@ -1486,9 +1615,17 @@ void k_encode_fast_fused(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __r
         drain_stores();
       }
       __syncthreads();
-      for (int32_t j = threadIdx.x; j < 3 * g.nsc; j += blockDim.x) fl[j] = f.fin[3 * c * g.nsc + j];
+      {
+        const int32_t nsc = lds_uniform(&A->g.nsc);
+        const int32_t* fin = lds_uniform(&A->f.fin);
+        for (int32_t j = threadIdx.x; j < 3 * nsc; j += blockDim.x) fl[j] = fin[3 * c * nsc + j];
+      }
       __syncthreads();
       if (threadIdx.x == 0) {
+        const CGeom g = lds_uniform(&A->g);
+        const EncFuse f = lds_uniform(&A->f);
+        const int32_t ipc = (g.nsc + kFuseSpi - 1) / kFuseSpi;
+        int32_t* ready = f.sync + kFuseHdr + f.nchunks * g.nblocks + f.nchunks;
         Place* pl = f.place + (int64_t)c * g.nsc;
         int32_t cb = 0;
         const int32_t m = finalize_chunk(
@@ -1512,19 +1649,23 @@ void k_encode_fast_fused(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __r
       __syncthreads();
     }
     FUSE_TRACE(2, 0);
-    if (!(f.mode_bits & 16)) scatter_available(2);
-    i = bcast(threadIdx.x == 0 ? atomicAdd(next, 1) : 0);
+    if (!(lds_uniform(&A->f.mode_bits) & 16)) scatter_available(2);
+    i = bcast(threadIdx.x == 0 ? atomicAdd(lds_uniform(&A->next), 1) : 0);
   }
   // stream queue empty: every remaining scatter item
   FUSE_TRACE(9, 0);
-  int32_t k = bcast(threadIdx.x == 0 ? add_agent(f.sync + 1, 1) : 0);
-  while (k < nitems) {
+  int32_t k = bcast(threadIdx.x == 0 ? add_agent(lds_uniform(&A->f.sync) + 1, 1) : 0);
+  while (true) {
+    const CGeom g = lds_uniform(&A->g);
+    const int32_t nitems = lds_uniform(&A->f.nchunks) * ((g.nsc + kFuseSpi - 1) / kFuseSpi);
+    if (k >= nitems) break;
     scatter_item(k);
-    k = bcast(threadIdx.x == 0 ? add_agent(f.sync + 1, 1) : 0);
+    k = bcast(threadIdx.x == 0 ? add_agent(lds_uniform(&A->f.sync) + 1, 1) : 0);
   }
   FUSE_TRACE(15, 0);
 }
-
+#undef FUSE_TRACE_PTR
+#define FUSE_TRACE_PTR f.trace
 
 // A timed-out hand-off wait inside k_encode_fast_fused fails every chunk of the batch.
 __global__ void k_fuse_check(const int32_t* __restrict__ sync, int32_t* __restrict__ cbytes, int32_t nchunks) {
@@ -1569,7 +1710,7 @@ static int launch_encode_fast_fused_t(Workspace* ws, const CGeom& g, const uint8
                                       int64_t ntot, int32_t* next, const int32_t* porder, EncFuse f, hipStream_t st) {
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
   const int tablog = std::min(fast_tablog(), hashlog);
-  const size_t lds = fast_lds(sizeof(POS), tablog);
+  const size_t lds = fused_lds(sizeof(POS), tablog);
   const void* fn = reinterpret_cast<const void*>(&k_encode_fast_fused<POS>);
   static bool attr_set = false;
   if (!attr_set) {
@@ -1614,7 +1755,7 @@ static int launch_encode_fast_fused_t(Workspace* ws, const CGeom& g, const uint8
 static void enc_mode(int* nlds, int* nglb);
 static bool fused_encode_ok(const CGeom& g) {
   if (!fuse_enabled() || g.compcode != 0 || g.dict_size) return false;
-  if (lz_mode() == 0) {   // exact mode: only with bit 4 (measured slower), the default k_encode shape
+  if (g.lzmode == 0) {   // exact mode: only with bit 4 (measured slower), the default k_encode shape
     if (!(fuse_bits() & 4)) return false;
     int nl, ng;
     enc_mode(&nl, &ng);
@@ -2014,6 +2155,7 @@ static CGeom make_geom(const CompressPlan& P, int64_t src_stride, int64_t dst_st
   g.overhead = P.overhead;
   g.compcode = P.compcode;
   g.dict_size = P.use_dict ? P.dict_size : 0;
+  g.lzmode = (P.lz_mode == 0 || P.lz_mode == 1) ? P.lz_mode : lz_mode();
   g.src_stride = src_stride;
   g.dst_stride = dst_stride;
   g.wstride = ((int64_t)n + 255) / 256 * 256 + 256;
@@ -2228,10 +2370,10 @@ static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const ui
       f.cbytes = d_cbytes;
       f.htpl = htpl;
       f.nchunks = nchunks;
-      if (lz_mode() == 1) rc = launch_encode_fast_fused(ws, g, filt, res, ntot, next, porder, f, st);
+      if (g.lzmode == 1) rc = launch_encode_fast_fused(ws, g, filt, res, ntot, next, porder, f, st);
       else rc = small ? launch_encode_exact_fused<uint16_t>(ws, g, hashlog, filt, res, ntot, next, porder, f, st)
                       : launch_encode_exact_fused<uint32_t>(ws, g, hashlog, filt, res, ntot, next, porder, f, st);
-    } else if (lz_mode() == 1) rc = launch_encode_fast(ws, g, filt, res, ntot, next, porder, st);
+    } else if (g.lzmode == 1) rc = launch_encode_fast(ws, g, filt, res, ntot, next, porder, st);
     else rc = small ? launch_encode<uint16_t>(ws, g, hashlog, filt, res, ntot, next, porder, st)
                     : launch_encode<uint32_t>(ws, g, hashlog, filt, res, ntot, next, porder, st);
     if (rc) return rc;

@@ -274,7 +274,7 @@ __device__ uint64_t g_enc_prof[16];
 // One greedy parse.  PROBE: get_cratio (counts only, limit = min(length, 2^hashlog), no far
 // short-match rule, no clevel-9 double rehash, no tail).  !PROBE: the emitting main loop + tail.
 template <bool PROBE, typename TAB, bool WT = false>
-__device__ __forceinline__ LzPassOut lz_pass(gin_t in, int32_t length, int hashlog, int clevel, gout_t out,
+__device__ __forceinline__ LzPassOut lz_pass(gin_t __restrict__ in, int32_t length, int hashlog, int clevel, gout_t __restrict__ out,
                                              int32_t maxout, TAB htab, B2H_LDS uint32_t* dbits,
                                              B2H_LDS uint8_t* oring) {
   const int lane = lane_id();
@@ -706,7 +706,7 @@ __device__ __forceinline__ bool wave_is_run_from(gin_t s, int32_t from, int32_t 
 
 // Full per-stream encode with maxout = neblock: run test, entropy probe, main pass.
 template <typename TAB, bool WT = false>
-__device__ __forceinline__ StreamResult encode_stream(gin_t in, int32_t n, int clevel, gout_t out,
+__device__ __forceinline__ StreamResult encode_stream(gin_t __restrict__ in, int32_t n, int clevel, gout_t __restrict__ out,
                                                       TAB htab, B2H_LDS uint32_t* dbits,
                                                       B2H_LDS uint8_t* oring, bool allow_runs) {
   StreamResult res;

@@ -94,42 +94,45 @@ struct FastShared {          // per workgroup, after the table and the output ri
   int32_t bcast;             // k_encode_fast_fused: claims and hand-off words, lane 0 -> workgroup
 };
 
-template <bool PROBE, typename POS, bool WT>
-__device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int probe_hashlog, int tablog, gout_t out,
-                                                   int32_t maxout, B2H_LDS uint8_t* tab, B2H_LDS uint8_t* oring,
-                                                   B2H_LDS FastShared* sh, int clevel, bool matcher) {
-  const int lane = lane_id();
-  constexpr int32_t ORM = kOutRing - 1;
-  int32_t limit = length;
+// Pass limits shared by both roles (blosc/blosclz.c:440-482, get_cratio 320-419).
+template <bool PROBE>
+__device__ __forceinline__ void fast_limits(int32_t length, int probe_hashlog, int32_t* limit, int32_t* bound,
+                                            int32_t* loop_end) {
+  int32_t lim = length;
   if (PROBE) {
     const int32_t hl = 1 << probe_hashlog;
-    limit = length > hl ? hl : length;
+    lim = length > hl ? hl : length;
   }
-  const int32_t bound = limit - 1, loop_end = limit - 12;
-  {  // clear the table: each wave half of it
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    B2H_LDS u32x4* t16 = (B2H_LDS u32x4*)tab;
-    const int32_t n16 = (int32_t)((sizeof(POS) << tablog) / 16);
-    const int32_t h = n16 / 2;
-    for (int32_t i = (matcher ? 0 : h) + lane; i < (matcher ? h : n16); i += 64) t16[i] = u32x4{0u, 0u, 0u, 0u};
-  }
-  LzPassOut r;
-  int32_t windows = 0;
-  int32_t F = 0;   // parser: output [0, F) already in `out`
-  auto flush = [&](int32_t to) {
-    ring_flush<WT>(out, oring, F, to);
-    F = to;
-  };
-  int32_t o = 5, lit = 4, pos = PROBE ? 0 : 4;
-  uint32_t byte0 = kLzMaxCopy - 1;
-  if (!PROBE && !matcher && lane < 5) oring[lane] = lane == 0 ? (uint8_t)(kLzMaxCopy - 1) : in[lane - 1];
-  int32_t peak = 0;
-  bool fail = false, early = false, sure = false;
-  const double thr_o = PROBE ? 0.999 * (clevel == 1 ? 2.0 : clevel == 2 ? 1.5 : clevel <= 6 ? 1.2
-                                        : clevel == 7 ? 1.15 : clevel == 8 ? 1.1 : 1.0) : 0.0;
-  const double thr_s = thr_o * (1.001 / 0.999);
-  EPROF_DECL;
+  *limit = lim;
+  *bound = lim - 1;
+  *loop_end = lim - 12;
+}
 
+// Clear one wave's half of the table (the matcher the first half, the parser the second).
+template <typename POS>
+__device__ __forceinline__ void fast_clear_half(B2H_LDS uint8_t* tab, int tablog, bool first) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  B2H_LDS u32x4* t16 = (B2H_LDS u32x4*)tab;
+  const int32_t n16 = (int32_t)((sizeof(POS) << tablog) / 16);
+  const int32_t h = n16 / 2;
+  for (int32_t i = (first ? 0 : h) + lane_id(); i < (first ? h : n16); i += 64) t16[i] = u32x4{0u, 0u, 0u, 0u};
+}
+
+// The two roles of one pass run as two SEPARATE loops with the same barrier sequence (one barrier
+// per step; the step's control word is read by both from LDS after it, as a uniform value): each
+// role's loop-carried state is live in its own loop only, so the kernel's register allocation is
+// the larger of the two, not their sum (one shared loop with a role branch inside kept both roles'
+// state live everywhere and spilled ~170 SGPRs into VGPR lanes).
+//
+// MATCHER: tile exchanges, candidate loads and 60-byte compares -> the hand-over slots.
+template <bool PROBE, typename POS>
+__device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int32_t length, int probe_hashlog, int tablog,
+                                                               B2H_LDS uint8_t* tab, B2H_LDS FastShared* sh) {
+  const int lane = lane_id();
+  int32_t limit, bound, loop_end;
+  fast_limits<PROBE>(length, probe_hashlog, &limit, &bound, &loop_end);
+  (void)bound;
+  fast_clear_half<POS>(tab, tablog, true);
   // ---- matcher: the first input words of tile `ant` (prefetched one step ahead); the other 14
   // are loaded only when some lane's candidate matches its first 4 bytes, together with the
   // candidates' words (the same round trip): incompressible tiles issue 4 loads per lane, not 18 ----
@@ -186,21 +189,69 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
     sh->aux[slot][lane] = (uint32_t)(cok ? mm + 1 : 0) | ((rawc_word(a, 0) & 0xffu) << 8);
   };
 
+  const int32_t pos = PROBE ? 0 : 4;
   int32_t T = pos / kFastTile, pend = -1;
   int cur = 0, it = 0;
   const bool any = pos < loop_end;
   __syncthreads();                           // table cleared
-  if (any && matcher) produce(T, 0);         // entering T: T and T + 1
+  if (any) produce(T, 0);                    // entering T: T and T + 1
   __syncthreads();
   while (any) {
-    EPROF_T(tm0);
-    if (matcher) {
-      if (pend >= 0) produce(pend, cur ^ 1);               // the parser jumps to `pend`
-      else if ((T + 1) * kFastTile < loop_end) produce(T + 1, cur ^ 1);
-      EPROF_T(tm1);
-      EPROF_ADD(0, tm0, tm1);   // diagnostics: matcher busy
-    } else if (pend < 0) {
-      // ================= parser: tile T from slot `cur` =================
+    if (pend >= 0) produce(pend, cur ^ 1);               // the parser jumps to `pend`
+    else if ((T + 1) * kFastTile < loop_end) produce(T + 1, cur ^ 1);
+    __syncthreads();
+    if (pend >= 0) {   // the matcher produced the jump target: the parser takes it next
+      T = pend;
+      cur ^= 1;
+      pend = -1;
+      continue;
+    }
+    const int32_t c = __builtin_amdgcn_readfirstlane(sh->ctrl[it & 1]);
+    it++;
+    if (c < 0) break;
+    if (c == T + 1) {
+      T = c;
+      cur ^= 1;
+    } else {
+      pend = c;
+    }
+  }
+}
+
+// PARSER: chain walk, token emission, output ring and flushes, the tail.
+template <bool PROBE, typename POS, bool WT>
+__device__ __forceinline__ LzPassOut lz_pass_fast_parser(gin_t __restrict__ in, int32_t length, int probe_hashlog,
+                                                                   int tablog, gout_t __restrict__ out, int32_t maxout,
+                                                                   B2H_LDS uint8_t* tab, B2H_LDS uint8_t* oring,
+                                                                   B2H_LDS FastShared* sh, int clevel) {
+  const int lane = lane_id();
+  constexpr int32_t ORM = kOutRing - 1;
+  int32_t limit, bound, loop_end;
+  fast_limits<PROBE>(length, probe_hashlog, &limit, &bound, &loop_end);
+  fast_clear_half<POS>(tab, tablog, false);
+  LzPassOut r;
+  int32_t windows = 0;
+  int32_t F = 0;   // output [0, F) already in `out`
+  auto flush = [&](int32_t to) {
+    ring_flush<WT>(out, oring, F, to);
+    F = to;
+  };
+  int32_t o = 5, lit = 4, pos = PROBE ? 0 : 4;
+  uint32_t byte0 = kLzMaxCopy - 1;
+  if (!PROBE && lane < 5) oring[lane] = lane == 0 ? (uint8_t)(kLzMaxCopy - 1) : in[lane - 1];
+  int32_t peak = 0;
+  bool fail = false, early = false, sure = false;
+  const double thr_o = PROBE ? 0.999 * (clevel == 1 ? 2.0 : clevel == 2 ? 1.5 : clevel <= 6 ? 1.2
+                                        : clevel == 7 ? 1.15 : clevel == 8 ? 1.1 : 1.0) : 0.0;
+  const double thr_s = thr_o * (1.001 / 0.999);
+  EPROF_DECL;
+  int32_t T = pos / kFastTile, pend = -1;
+  int cur = 0, it = 0;
+  const bool any = pos < loop_end;
+  __syncthreads();                           // table cleared
+  __syncthreads();                           // the matcher produced the first tile
+  while (any) {
+    if (pend < 0) {
       int32_t nt = -1;
       do {
         if (PROBE) {
@@ -383,15 +434,14 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
     EPROF_T(tb0);
     __syncthreads();
     EPROF_T(tb1);
-    if (matcher) EPROF_ADD(4, tb0, tb1);   // diagnostics: barrier wait, matcher / parser
-    else EPROF_ADD(6, tb0, tb1);
-    if (pend >= 0) {   // the matcher produced the jump target: the parser takes it next
+    EPROF_ADD(6, tb0, tb1);
+    if (pend >= 0) {   // the matcher produced the jump target: take it
       T = pend;
       cur ^= 1;
       pend = -1;
       continue;
     }
-    const int32_t c = sh->ctrl[it & 1];
+    const int32_t c = __builtin_amdgcn_readfirstlane(sh->ctrl[it & 1]);
     it++;
     if (c < 0) break;
     if (c == T + 1) {
@@ -402,7 +452,7 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
     }
   }
   EPROF_FLUSH;
-  if (!matcher && !PROBE && !fail) {
+  if (!PROBE && !fail) {
     // tail literals [pos, bound]
     while (pos <= bound) {
       if (o - F >= 1024) flush(F + 512);
@@ -447,10 +497,30 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
   return r;
 }
 
+// One pass, both roles (the matcher's result is not used).
+template <bool PROBE, typename POS, bool WT>
+__device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int probe_hashlog, int tablog, gout_t out,
+                                                   int32_t maxout, B2H_LDS uint8_t* tab, B2H_LDS uint8_t* oring,
+                                                   B2H_LDS FastShared* sh, int clevel, bool matcher) {
+  if (matcher) {
+    lz_pass_fast_matcher<PROBE, POS>(in, length, probe_hashlog, tablog, tab, sh);
+    LzPassOut r;
+    r.o = 1;
+    r.pos = 0;
+    r.peak = 0;
+    r.fail = false;
+    r.early = false;
+    r.sure = false;
+    r.windows = 0;
+    return r;
+  }
+  return lz_pass_fast_parser<PROBE, POS, WT>(in, length, probe_hashlog, tablog, out, maxout, tab, oring, sh, clevel);
+}
+
 // Two-wave fast-mode stream encode: both waves run this; the parser's StreamResult is the one
 // to keep.  The run test is split between the waves; decisions travel through sh->decide.
 template <typename POS, bool WT = false>
-__device__ __forceinline__ StreamResult encode_stream_fast(gin_t in, int32_t n, int clevel, gout_t out,
+__device__ __forceinline__ StreamResult encode_stream_fast(gin_t __restrict__ in, int32_t n, int clevel, gout_t __restrict__ out,
                                                             B2H_LDS uint8_t* tab, int tablog, B2H_LDS uint8_t* oring,
                                                             B2H_LDS FastShared* sh, bool allow_runs, bool matcher) {
   StreamResult res;

@@ -135,6 +135,7 @@ struct blosc2_context_s {
   int tuner_id = 0;
   bool instr_codec = false;
   void* codec_params = nullptr;
+  int lz_mode = -1;          // BloscLZ encoder chosen through codec_params at creation (-1: process default)
   void* filter_params[6] = {nullptr};
   // decompression parameters
   blosc2_dparams dparams = BLOSC2_DPARAMS_DEFAULTS;
@@ -144,6 +145,17 @@ struct blosc2_context_s {
   Device dev;
   std::mutex mu;
 };
+
+namespace b2h {
+// cparams.codec_params -> BloscLZ encoder mode (include/b2h.h b2h_codec_params), or -1.  Only a
+// struct carrying the magic word is ours: a user codec's own parameters are left alone.
+int codec_params_lz_mode(const void* codec_params) {
+  if (!codec_params) return -1;
+  const b2h_codec_params* p = static_cast<const b2h_codec_params*>(codec_params);
+  if (p->magic != B2H_CODEC_PARAMS_MAGIC) return -1;
+  return (p->blosclz_mode == 0 || p->blosclz_mode == 1) ? p->blosclz_mode : -1;
+}
+}  // namespace b2h
 
 namespace {
 
@@ -227,6 +239,7 @@ int compress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void* d
                                    ctx->filters, ctx->filters_meta, &computed, extended, ctx->compcode,
                                    ctx->compcode_meta, 1, ctx->use_dict);
   if (rc < 0) return rc;
+  plan.lz_mode = ctx->lz_mode;
   if (sticky) ctx->blocksize = computed;
   if ((rc = check_supported(ctx)) < 0) return rc;
   Device& d = ctx->dev;
@@ -544,6 +557,7 @@ int compress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void*
                                    ctx->filters, ctx->filters_meta, &computed, extended, ctx->compcode,
                                    ctx->compcode_meta, ucodec ? codec.version : 1);
   if (rc < 0) return rc;
+  P.lz_mode = ctx->lz_mode;
   if (sticky) ctx->blocksize = computed;
   if ((rc = check_supported(ctx)) < 0) return rc;
   if (P.use_dict) {
@@ -925,6 +939,7 @@ blosc2_context* blosc2_create_cctx(blosc2_cparams cparams) {
   c->tuner_params = cparams.tuner_params;
   c->tuner_id = cparams.tuner_id;
   c->codec_params = cparams.codec_params;
+  c->lz_mode = b2h::codec_params_lz_mode(cparams.codec_params);
   for (int i = 0; i < 6; i++) c->filter_params[i] = cparams.filter_params[i];
   return c;
 }
@@ -1515,6 +1530,7 @@ int b2h_compress_batch(const blosc2_cparams* cp, const void* d_src, int32_t chun
                                cp->splitmode, cp->filters, cp->filters_meta, &computed, true, cp->compcode, cp->compcode_meta,
                                1, cp->use_dict);
   if (rc < 0) return rc;
+  plan.lz_mode = b2h::codec_params_lz_mode(cp->codec_params);
   return b2h::compress_batch(plan, static_cast<const uint8_t*>(d_src), src_stride, nchunks,
                              static_cast<uint8_t*>(d_dst), dst_stride, d_cbytes, static_cast<hipStream_t>(stream));
 }

@@ -118,7 +118,20 @@ BLOSC_EXPORT int b2h_frame_get_slice(b2h_frame *frame, int64_t start, int64_t st
  * chunksize / blocksize, or sizes that are not multiples of typesize. */
 BLOSC_EXPORT int b2h_frame_get_sparse_buffer(b2h_frame *frame, int64_t ncoords, const int64_t *coords, void *buffer);
 
-/* BloscLZ encoder mode (process-wide), returns the previous one.
+/* Per-context BloscLZ encoder mode.  Built-in BloscLZ does not read blosc2_cparams.codec_params
+ * (reference include/blosc2.h:1207; only user codecs receive it), so a context selects its encoder
+ * by pointing codec_params at one of these when it is created (blosc2_create_cctx copies the mode;
+ * the b2h_compress_batch* entry points read it from their cparams).  No chunk byte changes with the
+ * carrier: the mode only picks which encoder writes the streams.  Anything else in codec_params
+ * (a NULL pointer, a user codec's own struct) leaves the process default (b2h_set_blosclz_mode). */
+#define B2H_CODEC_PARAMS_MAGIC 0x68623262u /* "b2bh" */
+typedef struct {
+  uint32_t magic;       /* B2H_CODEC_PARAMS_MAGIC */
+  int32_t blosclz_mode; /* 0 exact (byte-identical to the reference), 1 fast */
+} b2h_codec_params;
+
+/* BloscLZ encoder mode, the process-wide default of contexts that do not choose one through
+ * codec_params (above); returns the previous one.
  *   0 exact (default): byte-identical to blosclz_compress (blosc/blosclz.c:422-619).
  *   1 fast: same token grammar, greedy rule, limits, entropy-probe thresholds and emission, but the
  *     hash-table candidates come from positions inserted in 64-position tiles independently of the

