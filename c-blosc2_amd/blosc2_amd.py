@@ -71,6 +71,60 @@ def dparams(nthreads=1):
     return d
 
 
+class Storage(C.Structure):
+    """blosc2_storage (reference include/blosc2.h:1758-1776); params as plain pointers."""
+    _fields_ = [("contiguous", C.c_bool), ("urlpath", C.c_char_p), ("cparams", C.c_void_p),
+                ("dparams", C.c_void_p), ("io", C.c_void_p)]
+
+
+class Schunk(C.Structure):
+    """blosc2_schunk (reference include/blosc2.h:1823-1892), ABI-identical."""
+    _fields_ = [
+        ("version", C.c_uint8), ("compcode", C.c_uint8), ("compcode_meta", C.c_uint8), ("clevel", C.c_uint8),
+        ("splitmode", C.c_uint8), ("typesize", C.c_int32), ("blocksize", C.c_int32), ("chunksize", C.c_int32),
+        ("flags2", C.c_uint8), ("use_dict", C.c_uint8), ("filters", C.c_uint8 * MAX_FILTERS),
+        ("filters_meta", C.c_uint8 * MAX_FILTERS), ("nchunks", C.c_int64), ("current_nchunk", C.c_int64),
+        ("nbytes", C.c_int64), ("cbytes", C.c_int64), ("data", C.POINTER(C.c_void_p)), ("data_len", C.c_size_t),
+        ("storage", C.POINTER(Storage)), ("frame", C.c_void_p), ("cctx", C.c_void_p), ("dctx", C.c_void_p),
+        ("metalayers", C.c_void_p * 16), ("nmetalayers", C.c_uint16), ("vlmetalayers", C.c_void_p * 8192),
+        ("nvlmetalayers", C.c_int16), ("tuner_params", C.c_void_p), ("tuner_id", C.c_int), ("ndim", C.c_int8),
+        ("blockshape", C.c_void_p), ("view", C.c_bool), ("change_tick", C.c_int64),
+    ]
+
+
+SCHUNK_COUNTERS = ("nchunks", "current_nchunk", "nbytes", "cbytes", "chunksize", "flags2", "typesize",
+                   "blocksize", "clevel", "compcode", "splitmode", "use_dict", "data_len")
+
+
+def bind_schunk(lib):
+    """argtypes of the super-chunk entry points (include/blosc2.h:1905-2328): shared by the product
+    and the oracle/_ref build, whose structs are the same ABI."""
+    vp, i32, i64, sp = C.c_void_p, C.c_int32, C.c_int64, C.POINTER(Schunk)
+    sig = {
+        "blosc2_schunk_new": ([C.POINTER(Storage)], sp), "blosc2_schunk_free": ([sp], C.c_int),
+        "blosc2_schunk_append_chunk": ([sp, vp, C.c_bool], i64),
+        "blosc2_schunk_insert_chunk": ([sp, i64, vp, C.c_bool], i64),
+        "blosc2_schunk_update_chunk": ([sp, i64, vp, C.c_bool], i64),
+        "blosc2_schunk_delete_chunk": ([sp, i64], i64),
+        "blosc2_schunk_append_buffer": ([sp, vp, i32], i64),
+        "blosc2_schunk_decompress_chunk": ([sp, i64, vp, i32], C.c_int),
+        "blosc2_schunk_get_chunk": ([sp, i64, C.POINTER(vp), C.POINTER(C.c_bool)], C.c_int),
+        "blosc2_schunk_get_lazychunk": ([sp, i64, C.POINTER(vp), C.POINTER(C.c_bool)], C.c_int),
+        "blosc2_schunk_get_slice_buffer": ([sp, i64, i64, vp], C.c_int),
+        "blosc2_schunk_get_cparams": ([sp, C.POINTER(vp)], C.c_int),
+        "blosc2_schunk_get_dparams": ([sp, C.POINTER(vp)], C.c_int),
+        "blosc2_getitem_bytes_ctx": ([vp, vp, i32, i32, i32, vp, i32], C.c_int),
+        "b2h_schunk_append_device": ([sp, vp, vp, i32, i64], i64),
+        "b2h_schunk_decompress_device": ([sp, i64, i32, vp, i64, i32, vp], C.c_int),
+        "b2h_schunk_get_slice_device": ([sp, i64, i64, vp], C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(lib, name, None)
+        if f is not None:
+            f.argtypes, f.restype = args, res
+    return lib
+
+
 def _bind(lib):
     vp, i32, i16, i64 = C.c_void_p, C.c_int32, C.c_int16, C.c_int64
     sig = {
@@ -109,7 +163,7 @@ def _bind(lib):
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
         f.argtypes, f.restype = args, res
-    return lib
+    return bind_schunk(lib)
 
 
 _lib = None
@@ -238,3 +292,66 @@ def mean_times():
     buf = (C.c_float * 5)()
     lib().b2h_mean_times(buf)
     return dict(zip(("filter_ms", "encode_ms", "finalize_ms", "decode_ms", "unfilter_ms"), list(buf)))
+
+
+# ------------------------------------------------------------------------- super-chunks ----
+class SChunk:
+    """An in-memory super-chunk (blosc2_schunk_new with sparse storage) of a library `L` (the
+    product by default; tests drive the oracle/_ref build through the same class).  `cparams` /
+    `dparams` are that library's own structs."""
+
+    def __init__(self, cparams_, dparams_=None, L=None):
+        self.L = L if L is not None else lib()
+        self._keep = (cparams_, dparams_)
+        st = Storage(False, None, C.cast(C.pointer(cparams_), C.c_void_p),
+                     C.cast(C.pointer(dparams_), C.c_void_p) if dparams_ is not None else None, None)
+        self.p = self.L.blosc2_schunk_new(C.byref(st))
+        if not self.p:
+            raise RuntimeError("blosc2_schunk_new failed")
+
+    @property
+    def s(self):
+        return self.p.contents
+
+    def counters(self):
+        return {k: getattr(self.s, k) for k in SCHUNK_COUNTERS}
+
+    def append_buffer(self, a: np.ndarray):
+        raw = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+        return self.L.blosc2_schunk_append_buffer(self.p, _p(raw), raw.nbytes)
+
+    def append_chunk(self, chunk: np.ndarray, copy=True):
+        return self.L.blosc2_schunk_append_chunk(self.p, _p(chunk), copy)
+
+    def insert_chunk(self, n, chunk: np.ndarray, copy=True):
+        return self.L.blosc2_schunk_insert_chunk(self.p, n, _p(chunk), copy)
+
+    def update_chunk(self, n, chunk: np.ndarray, copy=True):
+        return self.L.blosc2_schunk_update_chunk(self.p, n, _p(chunk), copy)
+
+    def delete_chunk(self, n):
+        return self.L.blosc2_schunk_delete_chunk(self.p, n)
+
+    def chunk(self, n):
+        """The n-th compressed chunk (a copy), or the error code."""
+        cp, nf = C.c_void_p(), C.c_bool()
+        cb = self.L.blosc2_schunk_get_chunk(self.p, n, C.byref(cp), C.byref(nf))
+        if cb <= 0:
+            return cb
+        return np.ctypeslib.as_array(C.cast(cp, C.POINTER(C.c_uint8)), (cb,)).copy()
+
+    def decompress_chunk(self, n, nbytes):
+        out = np.zeros(max(nbytes, 1), np.uint8)
+        rc = self.L.blosc2_schunk_decompress_chunk(self.p, n, _p(out), nbytes)
+        return (rc, out[:max(rc, 0)])
+
+    def get_slice(self, start, stop, itemsize=None):
+        ts = itemsize or self.s.typesize
+        out = np.zeros(max((stop - start) * ts, 1), np.uint8)
+        rc = self.L.blosc2_schunk_get_slice_buffer(self.p, start, stop, _p(out))
+        return (rc, out[:max((stop - start) * ts, 0)])
+
+    def free(self):
+        if self.p:
+            self.L.blosc2_schunk_free(self.p)
+            self.p = None

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+struct blosc2_context_s;   // include/blosc2.h (opaque blosc2_context)
+
 namespace b2h {
 
 // Device scratch of one user (the process-wide default of a device, a blosc2 context, a frame).
@@ -126,6 +128,20 @@ int debug_stream_results(void* host, int32_t n);
 int debug_decode_cycles(void* host, int32_t n);
 KernelTimes last_times();   // the latest batch (waits for its events)
 KernelTimes mean_times();   // mean over every batch since enable_timing(true)
+
+// The super-chunk layer's device batches over a context (blosc2_api.cpp; used by b2h_schunk.cpp).
+// ctx_compress_device: n consecutive blosc2_compress_ctx calls (chunk i = d_src + i*src_stride,
+//   nbytes[i] bytes, destsize nbytes[i] + 32) into d_dst + i*dst_stride, as device batches.  Async.
+// ctx_append_device: the same, returning each chunk as a malloc'd host buffer of exactly its cbytes
+//   (what blosc2_schunk_append_buffer hands to blosc2_schunk_append_chunk).  Synchronous.
+// ctx_decompress_device: n host chunks decoded into d_dst + i*dst_stride (capacity dst_cap) in one
+//   device batch; status[i] = blosc2_schunk_decompress_chunk's return for that chunk.  Synchronous.
+int ctx_compress_device(::blosc2_context_s* ctx, const uint8_t* d_src, const int32_t* nbytes, int32_t n,
+                        int64_t src_stride, uint8_t* d_dst, int64_t dst_stride, int32_t* d_cbytes);
+int ctx_append_device(::blosc2_context_s* ctx, const uint8_t* d_src, const int32_t* nbytes, int32_t n,
+                      int64_t src_stride, uint8_t** chunks_out);
+int ctx_decompress_device(::blosc2_context_s* ctx, const uint8_t* const* chunks, int32_t n, uint8_t* d_dst,
+                          int64_t dst_stride, int32_t dst_cap, int32_t* status);
 
 // Device bookkeeping
 int device_count();

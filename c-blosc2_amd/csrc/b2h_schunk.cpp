@@ -1,0 +1,590 @@
+// b2h_schunk.cpp -- in-memory super-chunks (include/blosc2.h blosc2_schunk) over the MI355X engine.
+//
+// The super-chunk is the container the reference's callers reach the chunk engine through
+// (blosc/schunk.c): a list of compressed chunks plus counters, one compression and one
+// decompression context.  This file is host bookkeeping only -- every chunk is compressed and
+// decompressed by the device engine through the contexts (blosc2_api.cpp).  It keeps the
+// reference's frame-less (sparse, in-memory) super-chunk: chunks are malloc'd buffers indexed by
+// schunk->data, and the counters (nbytes, cbytes, chunksize, flags2, current_nchunk) move exactly
+// as blosc/schunk.c moves them, quirks included (a 32-byte chunk is counted when appended but not
+// when replaced or deleted, schunk.c:1300-1302), so a caller sees the same numbers.  Frame-backed
+// storage (contiguous frames, files, directories) is outside the device engine: blosc2_schunk_new
+// returns NULL for it (the read side of contiguous frames is b2h_frame_* in b2h.h).
+//
+// The b2h_schunk_* entry points (include/b2h.h) are the batch forms: many appends / decompressions
+// of one super-chunk as one device batch, chunk-for-chunk identical to the serial calls.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../include/b2h.h"
+#include "../../include/blosc2.h"
+#include "b2h_engine.h"
+
+namespace {
+
+bool trace_on() {
+  static int on = -1;
+  if (on < 0) on = getenv("BLOSC_TRACE") != nullptr;
+  return on;
+}
+#define TRACE_ERROR(...)                                 \
+  do {                                                   \
+    if (trace_on()) {                                    \
+      fprintf(stderr, "[error] - ");                     \
+      fprintf(stderr, __VA_ARGS__);                      \
+      fprintf(stderr, " (%s:%d)\n", __FILE__, __LINE__); \
+    }                                                    \
+  } while (0)
+
+// Sizes and the flags2 byte of a chunk.  flags2 exists only in an extended header, which the flags
+// byte announces (both shuffle bits set); the size bound keeps a short chunk from being over-read
+// (get_chunk_flags2, schunk.c:942-949).
+struct ChunkInfo {
+  int32_t nbytes = 0, cbytes = 0;
+  uint8_t flags2 = 0;
+  bool vl() const { return (flags2 & BLOSC2_VL_BLOCKS) != 0; }
+};
+
+int chunk_info(const uint8_t* c, ChunkInfo* ci) {
+  const int rc = blosc2_cbuffer_sizes(c, &ci->nbytes, &ci->cbytes, nullptr);
+  if (rc < 0) return rc;
+  const uint8_t fl = c[BLOSC2_CHUNK_FLAGS];
+  const bool ext = (fl & BLOSC_DOSHUFFLE) && (fl & BLOSC_DOBITSHUFFLE);
+  ci->flags2 = (ext && ci->cbytes >= BLOSC_EXTENDED_HEADER_LENGTH) ? c[BLOSC2_CHUNK_BLOSC2_FLAGS2] : 0;
+  return 0;
+}
+
+// A replaced / deleted chunk's sizes; a header-only chunk (32 bytes) counts 0 compressed bytes
+// (schunk.c:1295-1303, 1392-1400).
+void old_sizes(const uint8_t* c, int32_t* nb, int32_t* cb) {
+  *nb = *cb = 0;
+  if (!c) return;
+  if (blosc2_cbuffer_sizes(c, nb, cb, nullptr) < 0) *nb = *cb = 0;
+  if (*cb == BLOSC2_MAX_OVERHEAD) *cb = 0;
+}
+
+int validate_nchunk(const blosc2_schunk* s, int64_t nchunk, bool allow_end, const char* fn) {   // schunk.c:44-66
+  if (nchunk < 0) {
+    TRACE_ERROR("nchunk ('%lld') is negative in %s.", (long long)nchunk, fn);
+    return BLOSC2_ERROR_INVALID_PARAM;
+  }
+  if (allow_end ? nchunk > s->nchunks : nchunk >= s->nchunks) {
+    TRACE_ERROR("nchunk ('%lld') is out of range (%lld chunks) in %s.", (long long)nchunk, (long long)s->nchunks, fn);
+    return BLOSC2_ERROR_INVALID_PARAM;
+  }
+  return 0;
+}
+
+enum Op { kAppend, kInsert, kUpdate };
+
+// A super-chunk holds regular chunks or VL-block chunks, never both: the new chunk is checked
+// against chunk `ref` (< 0: none left to compare with, the super-chunk adopts its flags2).
+// schunk.c:985-1000 (append), 1114-1129 (insert), 1248-1264 (update).
+int check_kind(blosc2_schunk* s, int64_t ref, const ChunkInfo& ci, int err) {
+  if (ref < 0) {
+    s->flags2 = ci.flags2;
+    return 0;
+  }
+  ChunkInfo r;
+  const int rc = chunk_info(s->data[ref], &r);
+  if (rc < 0) return rc;
+  if (r.vl() != ci.vl()) {
+    TRACE_ERROR("schunks cannot mix regular chunks and VL-block chunks.");
+    return err;
+  }
+  return 0;
+}
+
+// The fixed-chunksize bookkeeping: -1 until the first chunk, then that chunk's nbytes while every
+// chunk but the last has it; 0 (variable) from the first chunk that breaks the pattern.
+// schunk.c:1002-1023 (append), 1131-1154 (insert), 1266-1282 (update).
+int settle_chunksize(blosc2_schunk* s, Op op, int64_t nchunk, int32_t nb, int err) {
+  const bool variable = s->chunksize == 0;
+  if (s->chunksize == -1) s->chunksize = nb;
+  const int32_t cs = s->chunksize;
+  if (variable) return 0;
+  bool breaks = false;
+  if (op == kUpdate) {
+    breaks = nb > cs || (nchunk != s->nchunks - 1 && nb != cs);
+  } else if (s->nchunks > 0) {
+    int32_t last_nb = 0;
+    const int rc = blosc2_cbuffer_sizes(s->data[s->nchunks - 1], &last_nb, nullptr, nullptr);
+    if (rc < 0) return rc;
+    breaks = last_nb < cs || nb > cs || (op == kInsert && nchunk != s->nchunks && nb != cs);
+  }
+  if (breaks) {
+    s->chunksize = 0;
+    return 0;
+  }
+  if (cs > 0 && nb > cs) {
+    TRACE_ERROR("Chunks of different lengths in the same schunk are not supported yet: %d > %d.", nb, cs);
+    return err;
+  }
+  return 0;
+}
+
+// The chunk the super-chunk keeps: a copy, or the caller's buffer shrunk to its cbytes
+// (schunk.c:1045-1058).
+uint8_t* keep_chunk(uint8_t* chunk, const ChunkInfo& ci, bool copy) {
+  if (copy) {
+    uint8_t* c = static_cast<uint8_t*>(malloc((size_t)ci.cbytes));
+    if (c) memcpy(c, chunk, (size_t)ci.cbytes);
+    return c;
+  }
+  if (ci.cbytes < ci.nbytes) {
+    uint8_t* c = static_cast<uint8_t*>(realloc(chunk, (size_t)ci.cbytes));
+    return c ? c : chunk;
+  }
+  return chunk;
+}
+
+// Room for one more slot: the index grows one 4 KiB page at a time (schunk.c:1060-1065).
+bool grow_index(blosc2_schunk* s) {
+  if ((size_t)(s->nchunks + 1) * sizeof(void*) <= s->data_len) return true;
+  uint8_t** d = static_cast<uint8_t**>(realloc(s->data, s->data_len + 4096));
+  if (!d) return false;
+  s->data = d;
+  s->data_len += 4096;
+  return true;
+}
+
+// blosc2_schunk_insert_chunk / append_chunk on a frame-less super-chunk (schunk.c:976-1075,
+// 1100-1212): nchunk == nchunks appends.
+int64_t put_chunk(blosc2_schunk* s, Op op, int64_t nchunk, uint8_t* chunk, bool copy) {
+  const int err = op == kAppend ? BLOSC2_ERROR_CHUNK_APPEND : BLOSC2_ERROR_CHUNK_INSERT;
+  if (!s || !chunk) return BLOSC2_ERROR_NULL_POINTER;
+  ChunkInfo ci;
+  int rc = chunk_info(chunk, &ci);
+  if (rc < 0) return rc;
+  if ((rc = check_kind(s, s->nchunks > 0 ? 0 : -1, ci, err)) < 0) return rc;
+  if ((rc = settle_chunksize(s, op, nchunk, ci.nbytes, err)) < 0) return rc;
+  if (!grow_index(s)) return BLOSC2_ERROR_MEMORY_ALLOC;
+  uint8_t* kept = keep_chunk(chunk, ci, copy);
+  if (!kept) return BLOSC2_ERROR_MEMORY_ALLOC;
+  const int64_t n = s->nchunks;
+  s->current_nchunk = op == kAppend ? n : nchunk;
+  s->nchunks = n + 1;
+  s->nbytes += ci.nbytes;
+  s->cbytes += ci.cbytes;
+  if (nchunk < n) memmove(s->data + nchunk + 1, s->data + nchunk, (size_t)(n - nchunk) * sizeof(uint8_t*));
+  s->data[nchunk] = kept;
+  return s->nchunks;
+}
+
+// schunk.c:108-153
+int update_schunk_properties(blosc2_schunk* s) {
+  blosc2_cparams* cp = s->storage->cparams;
+  blosc2_dparams* dp = s->storage->dparams;
+  memcpy(s->filters, cp->filters, BLOSC2_MAX_FILTERS);
+  memcpy(s->filters_meta, cp->filters_meta, BLOSC2_MAX_FILTERS);
+  s->compcode = cp->compcode;
+  s->compcode_meta = cp->compcode_meta;
+  s->clevel = cp->clevel;
+  s->splitmode = (uint8_t)cp->splitmode;
+  s->use_dict = (uint8_t)cp->use_dict;
+  s->typesize = cp->typesize;
+  s->blocksize = cp->blocksize;
+  s->chunksize = -1;
+  s->flags2 = 0;
+  s->tuner_params = cp->tuner_params;
+  s->tuner_id = cp->tuner_id;
+  if (s->cctx) blosc2_free_ctx(s->cctx);
+  cp->schunk = s;
+  s->cctx = blosc2_create_cctx(*cp);
+  if (!s->cctx) {
+    TRACE_ERROR("Could not create compression ctx");
+    return BLOSC2_ERROR_NULL_POINTER;
+  }
+  if (s->dctx) blosc2_free_ctx(s->dctx);
+  dp->schunk = s;
+  s->dctx = blosc2_create_dctx(*dp);
+  if (!s->dctx) {
+    TRACE_ERROR("Could not create decompression ctx");
+    return BLOSC2_ERROR_NULL_POINTER;
+  }
+  return 0;
+}
+
+void free_layers(blosc2_metalayer** layers, int n) {   // schunk.c:653-676
+  for (int i = 0; i < n; i++) {
+    if (!layers[i]) continue;
+    free(layers[i]->name);
+    free(layers[i]->content);
+    free(layers[i]);
+    layers[i] = nullptr;
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------ defaults getters ----
+// blosc/blosc2.c:6896-6911
+blosc2_cparams blosc2_get_blosc2_cparams_defaults(void) { return BLOSC2_CPARAMS_DEFAULTS; }
+blosc2_dparams blosc2_get_blosc2_dparams_defaults(void) { return BLOSC2_DPARAMS_DEFAULTS; }
+blosc2_storage blosc2_get_blosc2_storage_defaults(void) { return BLOSC2_STORAGE_DEFAULTS; }
+blosc2_io blosc2_get_blosc2_io_defaults(void) { return BLOSC2_IO_DEFAULTS; }
+
+// ------------------------------------------------------------------------------ lifetime ----
+// schunk.c:163-242 with get_new_storage (frame.c:2834-2877): the storage, its cparams, dparams and
+// io are private copies (defaults where the caller passed NULL).
+blosc2_schunk* blosc2_schunk_new(blosc2_storage* storage) {
+  const blosc2_storage st = storage ? *storage : BLOSC2_STORAGE_DEFAULTS;
+  if (st.contiguous || st.urlpath) {
+    TRACE_ERROR("frame-backed super-chunks (contiguous / urlpath) are outside the device engine; "
+                "use an in-memory sparse storage (contiguous = false, urlpath = NULL)");
+    return nullptr;
+  }
+  blosc2_schunk* s = static_cast<blosc2_schunk*>(calloc(1, sizeof(blosc2_schunk)));
+  blosc2_storage* ns = static_cast<blosc2_storage*>(calloc(1, sizeof(blosc2_storage)));
+  blosc2_cparams* cp = static_cast<blosc2_cparams*>(malloc(sizeof(blosc2_cparams)));
+  blosc2_dparams* dp = static_cast<blosc2_dparams*>(malloc(sizeof(blosc2_dparams)));
+  blosc2_io* io = static_cast<blosc2_io*>(malloc(sizeof(blosc2_io)));
+  if (!s || !ns || !cp || !dp || !io) {
+    free(s);
+    free(ns);
+    free(cp);
+    free(dp);
+    free(io);
+    return nullptr;
+  }
+  *ns = st;
+  *cp = st.cparams ? *st.cparams : BLOSC2_CPARAMS_DEFAULTS;
+  *dp = st.dparams ? *st.dparams : BLOSC2_DPARAMS_DEFAULTS;
+  *io = st.io ? *st.io : BLOSC2_IO_DEFAULTS;
+  ns->cparams = cp;
+  ns->dparams = dp;
+  ns->io = io;
+  s->storage = ns;
+  s->version = 0;   // pre-first version
+  s->view = false;
+  if (update_schunk_properties(s) < 0) {
+    TRACE_ERROR("Error when updating schunk properties");
+    blosc2_schunk_free(s);
+    return nullptr;
+  }
+  return s;
+}
+
+// schunk.c:679-727
+int blosc2_schunk_free(blosc2_schunk* schunk) {
+  if (!schunk) return 0;
+  if (schunk->data && !schunk->view) {
+    for (int64_t i = 0; i < schunk->nchunks; i++) free(schunk->data[i]);
+    free(schunk->data);
+  }
+  if (schunk->cctx) blosc2_free_ctx(schunk->cctx);
+  if (schunk->dctx) blosc2_free_ctx(schunk->dctx);
+  free(schunk->blockshape);
+  free_layers(schunk->metalayers, schunk->nmetalayers);
+  schunk->nmetalayers = 0;
+  if (schunk->storage) {
+    free(schunk->storage->urlpath);
+    free(schunk->storage->cparams);
+    free(schunk->storage->dparams);
+    free(schunk->storage->io);
+    free(schunk->storage);
+  }
+  free_layers(schunk->vlmetalayers, schunk->nvlmetalayers);
+  schunk->nvlmetalayers = 0;
+  free(schunk);
+  return 0;
+}
+
+// ---------------------------------------------------------------------- chunk index ops ----
+int64_t blosc2_schunk_append_chunk(blosc2_schunk* schunk, uint8_t* chunk, bool copy) {
+  if (!schunk) return BLOSC2_ERROR_NULL_POINTER;
+  return put_chunk(schunk, kAppend, schunk->nchunks, chunk, copy);
+}
+
+int64_t blosc2_schunk_insert_chunk(blosc2_schunk* schunk, int64_t nchunk, uint8_t* chunk, bool copy) {
+  if (!schunk) return BLOSC2_ERROR_NULL_POINTER;
+  const int rc = validate_nchunk(schunk, nchunk, true, "blosc2_schunk_insert_chunk");
+  if (rc < 0) return rc;
+  return put_chunk(schunk, kInsert, nchunk, chunk, copy);
+}
+
+// schunk.c:1235-1360
+int64_t blosc2_schunk_update_chunk(blosc2_schunk* schunk, int64_t nchunk, uint8_t* chunk, bool copy) {
+  if (!schunk || !chunk) return BLOSC2_ERROR_NULL_POINTER;
+  int rc = validate_nchunk(schunk, nchunk, false, "blosc2_schunk_update_chunk");
+  if (rc < 0) return rc;
+  ChunkInfo ci;
+  if ((rc = chunk_info(chunk, &ci)) < 0) return rc;
+  // compared with another chunk when there is one (chunk 1 when chunk 0 itself is replaced)
+  const int64_t ref = (schunk->nchunks > 1 || nchunk != 0) ? (nchunk == 0 ? 1 : 0) : -1;
+  if ((rc = check_kind(schunk, ref, ci, BLOSC2_ERROR_CHUNK_UPDATE)) < 0) return rc;
+  if ((rc = settle_chunksize(schunk, kUpdate, nchunk, ci.nbytes, BLOSC2_ERROR_CHUNK_UPDATE)) < 0) return rc;
+  int32_t nb_old, cb_old;
+  old_sizes(schunk->data[nchunk], &nb_old, &cb_old);
+  schunk->current_nchunk = nchunk;
+  uint8_t* kept = keep_chunk(chunk, ci, copy);
+  if (!kept) return BLOSC2_ERROR_MEMORY_ALLOC;
+  schunk->nbytes += (int64_t)ci.nbytes - nb_old;
+  schunk->cbytes += (int64_t)ci.cbytes - cb_old;
+  free(schunk->data[nchunk]);
+  schunk->data[nchunk] = kept;
+  return schunk->nchunks;
+}
+
+// schunk.c:1375-1442
+int64_t blosc2_schunk_delete_chunk(blosc2_schunk* schunk, int64_t nchunk) {
+  if (!schunk) return BLOSC2_ERROR_NULL_POINTER;
+  const int rc = validate_nchunk(schunk, nchunk, false, "blosc2_schunk_delete_chunk");
+  if (rc < 0) return rc;
+  int32_t nb_old, cb_old;
+  old_sizes(schunk->data[nchunk], &nb_old, &cb_old);
+  schunk->current_nchunk = nchunk;
+  schunk->nchunks -= 1;
+  if (schunk->nchunks == 0) schunk->flags2 = 0;
+  schunk->nbytes -= nb_old;
+  schunk->cbytes -= cb_old;
+  free(schunk->data[nchunk]);
+  memmove(schunk->data + nchunk, schunk->data + nchunk + 1, (size_t)(schunk->nchunks - nchunk) * sizeof(uint8_t*));
+  schunk->data[schunk->nchunks] = nullptr;
+  return schunk->nchunks;
+}
+
+// ---------------------------------------------------------------------- compress / decode ----
+// schunk.c:1459-1477
+int64_t blosc2_schunk_append_buffer(blosc2_schunk* schunk, const void* src, int32_t nbytes) {
+  if (!schunk) return BLOSC2_ERROR_NULL_POINTER;
+  if (nbytes < 0 || nbytes > BLOSC2_MAX_BUFFERSIZE) return BLOSC2_ERROR_INVALID_PARAM;
+  uint8_t* chunk = static_cast<uint8_t*>(malloc((size_t)nbytes + BLOSC2_MAX_OVERHEAD));
+  if (!chunk) return BLOSC2_ERROR_MEMORY_ALLOC;
+  schunk->current_nchunk = schunk->nchunks;
+  const int cbytes = blosc2_compress_ctx(schunk->cctx, src, nbytes, chunk, nbytes + BLOSC2_MAX_OVERHEAD);
+  if (cbytes < 0) {
+    free(chunk);
+    return cbytes;
+  }
+  const int64_t n = blosc2_schunk_append_chunk(schunk, chunk, false);
+  if (n < 0) {
+    TRACE_ERROR("Error appending a buffer in super-chunk");
+    free(chunk);
+  }
+  return n;
+}
+
+// schunk.c:1481-1530
+int blosc2_schunk_decompress_chunk(blosc2_schunk* schunk, int64_t nchunk, void* dest, int32_t nbytes) {
+  if (!schunk) return BLOSC2_ERROR_NULL_POINTER;
+  int rc = validate_nchunk(schunk, nchunk, false, "blosc2_schunk_decompress_chunk");
+  if (rc < 0) return rc;
+  schunk->current_nchunk = nchunk;
+  const uint8_t* src = schunk->data[nchunk];
+  if (!src) return 0;
+  int32_t chunk_nbytes, chunk_cbytes;
+  if ((rc = blosc2_cbuffer_sizes(src, &chunk_nbytes, &chunk_cbytes, nullptr)) < 0) return rc;
+  if (nbytes < chunk_nbytes) {
+    TRACE_ERROR("Buffer size is too small for the decompressed buffer ('%d' bytes, but '%d' are needed).", nbytes,
+                chunk_nbytes);
+    return BLOSC2_ERROR_INVALID_PARAM;
+  }
+  const int got = blosc2_decompress_ctx(schunk->dctx, src, chunk_cbytes, dest, nbytes);
+  if (got < 0) return got;
+  if (got != chunk_nbytes) {
+    TRACE_ERROR("Error in decompressing chunk.");
+    return BLOSC2_ERROR_FAILURE;
+  }
+  return got;
+}
+
+// schunk.c:1543-1632 (frame-less: the chunk is the super-chunk's own buffer, never to be freed)
+static int get_chunk(blosc2_schunk* schunk, int64_t nchunk, uint8_t** chunk, bool* needs_free, const char* fn) {
+  if (!schunk || !chunk || !needs_free) return BLOSC2_ERROR_NULL_POINTER;
+  int rc = validate_nchunk(schunk, nchunk, false, fn);
+  if (rc < 0) return rc;
+  schunk->current_nchunk = nchunk;
+  *chunk = schunk->data[nchunk];
+  *needs_free = false;
+  if (!*chunk) return 0;
+  int32_t cbytes;
+  if ((rc = blosc2_cbuffer_sizes(*chunk, nullptr, &cbytes, nullptr)) < 0) return rc;
+  return cbytes;
+}
+
+int blosc2_schunk_get_chunk(blosc2_schunk* schunk, int64_t nchunk, uint8_t** chunk, bool* needs_free) {
+  return get_chunk(schunk, nchunk, chunk, needs_free, "blosc2_schunk_get_chunk");
+}
+
+int blosc2_schunk_get_lazychunk(blosc2_schunk* schunk, int64_t nchunk, uint8_t** chunk, bool* needs_free) {
+  return get_chunk(schunk, nchunk, chunk, needs_free, "blosc2_schunk_get_lazychunk");
+}
+
+// Items [start, stop) of the super-chunk.  The range is checked (the reference reads past the
+// super-chunk for a range outside it); chunks are walked as schunk.c:1662-1783 walks them: a chunk
+// wholly inside the range decompresses straight into the buffer, an edge chunk goes through
+// blosc2_getitem_bytes_ctx.
+int blosc2_schunk_get_slice_buffer(blosc2_schunk* schunk, int64_t start, int64_t stop, void* buffer) {
+  if (!schunk || !buffer) return BLOSC2_ERROR_NULL_POINTER;
+  const int64_t ts = schunk->typesize;
+  if (start < 0 || stop < start || ts <= 0 || stop * ts > schunk->nbytes || schunk->chunksize <= 0) {
+    TRACE_ERROR("slice [%lld, %lld) is outside the super-chunk (or the super-chunk has no fixed chunksize)",
+                (long long)start, (long long)stop);
+    return BLOSC2_ERROR_INVALID_PARAM;
+  }
+  const int64_t cs = schunk->chunksize, b0 = start * ts, b1 = stop * ts;
+  uint8_t* dst = static_cast<uint8_t*>(buffer);
+  for (int64_t k = b0 / cs; k * cs < b1; k++) {
+    uint8_t* chunk;
+    bool needs_free;
+    const int cbytes = blosc2_schunk_get_lazychunk(schunk, k, &chunk, &needs_free);
+    if (cbytes < 0) {
+      TRACE_ERROR("Cannot get lazychunk ('%lld').", (long long)k);
+      return BLOSC2_ERROR_FAILURE;
+    }
+    const int64_t len = (k == schunk->nchunks - 1 && schunk->nbytes % cs) ? schunk->nbytes % cs : cs;
+    const int32_t lo = (int32_t)(std::max(b0, k * cs) - k * cs), hi = (int32_t)(std::min(b1, k * cs + len) - k * cs);
+    int got;
+    if (lo == 0 && hi == len) {
+      got = blosc2_decompress_ctx(schunk->dctx, chunk, cbytes, dst, (int32_t)len);
+      if (got < 0) {
+        TRACE_ERROR("Cannot decompress chunk ('%lld').", (long long)k);
+        return BLOSC2_ERROR_FAILURE;
+      }
+    } else {
+      got = blosc2_getitem_bytes_ctx(schunk->dctx, chunk, cbytes, lo, hi - lo, dst, hi - lo);
+      if (got != hi - lo) {
+        TRACE_ERROR("Cannot get items from ('%lld') chunk (%d of %d bytes).", (long long)k, got, hi - lo);
+        return BLOSC2_ERROR_FAILURE;
+      }
+    }
+    dst += got;
+  }
+  return BLOSC2_ERROR_SUCCESS;
+}
+
+// schunk.c:70-105
+int blosc2_schunk_get_cparams(blosc2_schunk* schunk, blosc2_cparams** cparams) {
+  if (!schunk || !cparams) return BLOSC2_ERROR_NULL_POINTER;
+  blosc2_cparams* cp = static_cast<blosc2_cparams*>(calloc(1, sizeof(blosc2_cparams)));
+  if (!cp) return BLOSC2_ERROR_MEMORY_ALLOC;
+  cp->schunk = schunk;
+  memcpy(cp->filters, schunk->filters, BLOSC2_MAX_FILTERS);
+  memcpy(cp->filters_meta, schunk->filters_meta, BLOSC2_MAX_FILTERS);
+  cp->compcode = schunk->compcode;
+  cp->compcode_meta = schunk->compcode_meta;
+  cp->clevel = schunk->clevel;
+  cp->typesize = schunk->typesize;
+  cp->blocksize = schunk->blocksize;
+  cp->splitmode = schunk->splitmode;
+  cp->use_dict = schunk->use_dict;
+  blosc2_cparams ctx_cp;
+  cp->nthreads = (schunk->cctx && blosc2_ctx_get_cparams(schunk->cctx, &ctx_cp) == 0) ? ctx_cp.nthreads
+                                                                                      : blosc2_get_nthreads();
+  *cparams = cp;
+  return 0;
+}
+
+int blosc2_schunk_get_dparams(blosc2_schunk* schunk, blosc2_dparams** dparams) {
+  if (!schunk || !dparams) return BLOSC2_ERROR_NULL_POINTER;
+  blosc2_dparams* dp = static_cast<blosc2_dparams*>(calloc(1, sizeof(blosc2_dparams)));
+  if (!dp) return BLOSC2_ERROR_MEMORY_ALLOC;
+  dp->schunk = schunk;
+  blosc2_dparams ctx_dp;
+  dp->nthreads = (schunk->dctx && blosc2_ctx_get_dparams(schunk->dctx, &ctx_dp) == 0) ? ctx_dp.nthreads
+                                                                                      : blosc2_get_nthreads();
+  *dparams = dp;
+  return 0;
+}
+
+// ------------------------------------------------------------------ device batch forms ----
+// n blosc2_schunk_append_buffer calls in one: the chunks are compressed by device batches on the
+// super-chunk's cctx (its sticky blocksize carried as the serial calls carry it), brought back in one
+// copy per group and appended in order.  A pipeline with user-registered filters / codecs runs the
+// serial calls instead (chunk by chunk through host memory).
+int64_t b2h_schunk_append_device(blosc2_schunk* schunk, const void* d_src, const int32_t* nbytes, int32_t n,
+                                 int64_t src_stride) {
+  if (!schunk || (n > 0 && (!d_src || !nbytes))) return BLOSC2_ERROR_NULL_POINTER;
+  if (n < 0) return BLOSC2_ERROR_INVALID_PARAM;
+  if (n == 0) return schunk->nchunks;
+  const uint8_t* src = static_cast<const uint8_t*>(d_src);
+  std::vector<uint8_t*> chunks((size_t)n, nullptr);
+  int rc = b2h::ctx_append_device(schunk->cctx, src, nbytes, n, src_stride, chunks.data());
+  if (rc == BLOSC2_ERROR_FILTER_PIPELINE) {
+    std::vector<uint8_t> host;
+    int64_t r = schunk->nchunks;
+    for (int32_t i = 0; i < n && r >= 0; i++) {
+      host.resize((size_t)std::max(nbytes[i], 1));
+      if (hipMemcpy(host.data(), src + (int64_t)i * src_stride, (size_t)nbytes[i], hipMemcpyDeviceToHost) != hipSuccess)
+        return BLOSC2_ERROR_FAILURE;
+      r = blosc2_schunk_append_buffer(schunk, host.data(), nbytes[i]);
+    }
+    return r;
+  }
+  if (rc < 0) return rc;
+  int64_t r = schunk->nchunks;
+  for (int32_t i = 0; i < n; i++) {
+    r = blosc2_schunk_append_chunk(schunk, chunks[i], false);
+    if (r < 0) {
+      for (int32_t j = i; j < n; j++) free(chunks[j]);
+      return r;
+    }
+  }
+  return r;
+}
+
+// Chunks [nchunk, nchunk + n) into d_dst + i * dst_stride in one device batch; status[i] (optional)
+// = what blosc2_schunk_decompress_chunk(schunk, nchunk + i, ., dst_capacity) returns.
+int b2h_schunk_decompress_device(blosc2_schunk* schunk, int64_t nchunk, int32_t n, void* d_dst, int64_t dst_stride,
+                                 int32_t dst_capacity, int32_t* status) {
+  if (!schunk) return BLOSC2_ERROR_NULL_POINTER;
+  if (n < 0 || nchunk < 0 || nchunk + n > schunk->nchunks) {
+    TRACE_ERROR("chunks [%lld, %lld) are outside the super-chunk (%lld chunks)", (long long)nchunk,
+                (long long)(nchunk + n), (long long)schunk->nchunks);
+    return BLOSC2_ERROR_INVALID_PARAM;
+  }
+  if (n == 0) return 0;
+  std::vector<int32_t> st((size_t)n);
+  schunk->current_nchunk = nchunk + n - 1;
+  const int rc = b2h::ctx_decompress_device(schunk->dctx, schunk->data + nchunk, n, static_cast<uint8_t*>(d_dst),
+                                            dst_stride, dst_capacity, st.data());
+  if (status) memcpy(status, st.data(), sizeof(int32_t) * (size_t)n);
+  return rc;
+}
+
+// blosc2_schunk_get_slice_buffer into device memory: the chunks wholly inside [start, stop) decode
+// in one device batch straight into place, the (at most two) edge chunks through getitem.
+int b2h_schunk_get_slice_device(blosc2_schunk* schunk, int64_t start, int64_t stop, void* d_dst) {
+  if (!schunk || !d_dst) return BLOSC2_ERROR_NULL_POINTER;
+  const int64_t ts = schunk->typesize;
+  if (start < 0 || stop < start || ts <= 0 || stop * ts > schunk->nbytes || schunk->chunksize <= 0)
+    return BLOSC2_ERROR_INVALID_PARAM;
+  if (start == stop) return 0;
+  const int64_t cs = schunk->chunksize, b0 = start * ts, b1 = stop * ts;
+  uint8_t* dst = static_cast<uint8_t*>(d_dst);
+  int64_t f0 = -1, f1 = -1;   // the run of whole chunks
+  std::vector<uint8_t> edge;
+  for (int64_t k = b0 / cs; k * cs < b1; k++) {
+    const int64_t len = (k == schunk->nchunks - 1 && schunk->nbytes % cs) ? schunk->nbytes % cs : cs;
+    const int32_t lo = (int32_t)(std::max(b0, k * cs) - k * cs), hi = (int32_t)(std::min(b1, k * cs + len) - k * cs);
+    if (lo == 0 && hi == len) {
+      if (f0 < 0) f0 = k;
+      f1 = k;
+      continue;
+    }
+    uint8_t* chunk;
+    bool needs_free;
+    const int cbytes = blosc2_schunk_get_lazychunk(schunk, k, &chunk, &needs_free);
+    if (cbytes <= 0) return BLOSC2_ERROR_FAILURE;
+    edge.resize((size_t)(hi - lo));
+    if (blosc2_getitem_bytes_ctx(schunk->dctx, chunk, cbytes, lo, hi - lo, edge.data(), hi - lo) != hi - lo)
+      return BLOSC2_ERROR_FAILURE;
+    if (hipMemcpy(dst + (k * cs + lo - b0), edge.data(), edge.size(), hipMemcpyHostToDevice) != hipSuccess)
+      return BLOSC2_ERROR_FAILURE;
+  }
+  if (f0 >= 0) {
+    const int32_t m = (int32_t)(f1 - f0 + 1);
+    std::vector<int32_t> st((size_t)m);
+    int rc = b2h::ctx_decompress_device(schunk->dctx, schunk->data + f0, m, dst + (f0 * cs - b0), cs, (int32_t)cs,
+                                        st.data());
+    if (rc < 0) return BLOSC2_ERROR_FAILURE;
+    schunk->current_nchunk = f1;
+  }
+  return 0;
+}

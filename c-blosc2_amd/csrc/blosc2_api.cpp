@@ -66,6 +66,28 @@ struct DevBuf {
   uint8_t* u8() const { return static_cast<uint8_t*>(p); }
 };
 
+// Pinned host staging of the super-chunk batches (one DMA per direction instead of one per chunk).
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t n) {
+    if (n <= cap) return true;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    n = std::max<size_t>(n, 1 << 20);
+    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return false;
+    cap = n;
+    return true;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  uint8_t* u8() const { return static_cast<uint8_t*>(p); }
+};
+
 // Per-context device state: its own stream, staging buffers and engine workspace, so distinct
 // contexts run concurrently (include/blosc2.h:1462-1466); all of it is freed by blosc2_free_ctx
 // (the reference frees its context scratch there, blosc/blosc2.c:6290).
@@ -73,6 +95,7 @@ struct Device {
   int dev = -1;
   hipStream_t stream = nullptr;
   DevBuf in, out, small;
+  PinnedBuf host;   // super-chunk batches only
   b2h::Workspace* ws = nullptr;
   bool init() {
     if (stream) return true;
@@ -93,6 +116,7 @@ struct Device {
     in.release();
     out.release();
     small.release();
+    host.release();
     if (stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
   }
@@ -325,6 +349,29 @@ int init_from_header(ChunkHdr* h, int32_t srcsize) {
   return 0;
 }
 
+// User filters / codecs in an extended header (not memcpyed, not special) -> host callbacks.
+// Unknown ids <= BLOSC2_DEFINED_FILTERS_STOP stay on the device, which fails them as
+// pipeline_backward does (blosc/blosc2.c:1534-1539); so does a plugin that is neither registered
+// nor loadable: it fails where the reference's block walk meets it (the codec at its first stream,
+// a filter after the block's streams), and the device planner keys those failures in order.
+bool chunk_needs_host(const uint8_t* s, const ChunkHdr& H) {
+  if (!H.ext || H.memcpyed || H.special != 0 || H.nbytes <= 0) return false;
+  uint8_t fl[6];
+  for (int i = 0; i < 6; i++) {
+    fl[i] = s[16 + i];
+    if (fl[i] <= BLOSC2_DEFINED_FILTERS_STOP) fl[i] = 0;
+  }
+  if (s[0] == BLOSC2_VERSION_FORMAT_ALPHA) fl[5] = 0;
+  const bool udcodec = (s[2] >> 5) == BLOSC_UDCODEC_FORMAT;
+  if (!needs_host_callbacks(fl, udcodec ? 255 : 0)) return false;
+  blosc2_filter fi;
+  blosc2_codec co;
+  for (int i = 0; i < 6; i++)
+    if (!device_filter(fl[i]) && !lookup_filter(fl[i], &fi)) return false;
+  if (udcodec && !lookup_codec(s[22], &co)) return false;
+  return true;
+}
+
 // Decompress one host chunk through the engine.  With a block mask only unmasked blocks are
 // copied back so masked regions of `dest` keep the caller's bytes (blosc/blosc2.c:1734-1737).
 // `mode`: b2h::kDecDeltaSelf for the per-block entry points (getitem, decompress_block).
@@ -341,31 +388,8 @@ int decompress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void*
                 mask->size(), nblocks);
     return BLOSC2_ERROR_DATA;
   }
-  const uint8_t* s = static_cast<const uint8_t*>(src);
-  // user filters / codecs in an extended header (not memcpyed, not special) -> host callbacks;
-  // unknown ids <= BLOSC2_DEFINED_FILTERS_STOP stay on the device, which fails them as
-  // pipeline_backward does (blosc/blosc2.c:1534-1539)
-  if (H.ext && !H.memcpyed && H.special == 0 && nbytes > 0) {
-    uint8_t fl[6];
-    for (int i = 0; i < 6; i++) {
-      fl[i] = s[16 + i];
-      if (fl[i] <= BLOSC2_DEFINED_FILTERS_STOP) fl[i] = 0;
-    }
-    if (s[0] == BLOSC2_VERSION_FORMAT_ALPHA) fl[5] = 0;
-    const bool udcodec = (s[2] >> 5) == BLOSC_UDCODEC_FORMAT;
-    if (needs_host_callbacks(fl, udcodec ? 255 : 0)) {
-      // A plugin that is neither registered nor loadable fails where the reference's block walk
-      // meets it (the codec at its first stream, a filter after the block's streams): the device
-      // planner keys those failures in order, so such chunks stay on the device path.
-      bool found = true;
-      blosc2_filter fi;
-      blosc2_codec co;
-      for (int i = 0; i < 6; i++)
-        if (!device_filter(fl[i]) && !lookup_filter(fl[i], &fi)) found = false;
-      if (udcodec && !lookup_codec(s[22], &co)) found = false;
-      if (found) return decompress_hybrid(ctx, src, srcsize, dest, destsize, mask, mode);
-    }
-  }
+  if (chunk_needs_host(static_cast<const uint8_t*>(src), H))
+    return decompress_hybrid(ctx, src, srcsize, dest, destsize, mask, mode);
   // The device reads what the reference may read: srcsize bytes (the blosc1 entry points pass
   // INT32_MAX for "unknown": the chunk's own cbytes then).
   const int32_t ss = srcsize == INT32_MAX ? std::max<int32_t>(H.cbytes, BLOSC_EXTENDED_HEADER_LENGTH) : srcsize;
@@ -845,6 +869,232 @@ int decompress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, voi
   return nbytes;
 }
 
+}  // namespace
+
+// --------------------------------------------------- super-chunk layer helpers (b2h_schunk.cpp) ----
+namespace b2h {
+// Consecutive blosc2_compress_ctx calls on one context, as ONE queue of device batches: chunk i =
+// d_src + i * src_stride (nbytes[i] bytes) into d_dst + i * dst_stride with destsize nbytes[i] + 32
+// (blosc2_schunk_append_buffer, blosc/schunk.c:1459-1477).  The context's sticky blocksize is
+// carried from chunk to chunk exactly as the serial calls carry it (blosc/blosc2.c:3130-3133: the
+// previous call's blocksize is the next call's request), so runs of chunks whose plans agree share
+// one launch and every chunk equals the serial call's bytes.  Asynchronous on the context's stream.
+// Caller holds ctx->mu.
+static int compress_device_locked(blosc2_context* ctx, const uint8_t* d_src, const int32_t* nbytes, int32_t n,
+                                  int64_t src_stride, uint8_t* d_dst, int64_t dst_stride, int32_t* d_cbytes) {
+  if (n > 0 && (!nbytes || !d_src || !d_dst || !d_cbytes)) return BLOSC2_ERROR_NULL_POINTER;
+  if (ctx->do_compress != 1) return BLOSC2_ERROR_INVALID_PARAM;
+  int rc = check_supported(ctx);
+  if (rc < 0) return rc;
+  if (needs_host_callbacks(ctx->filters, ctx->compcode)) {
+    TRACE_ERROR("user filters / codecs run per chunk through blosc2_compress_ctx, not the device batch");
+    return BLOSC2_ERROR_FILTER_PIPELINE;
+  }
+  Device& d = ctx->dev;
+  if (!d.init()) return BLOSC2_ERROR_FAILURE;
+  int32_t i = 0;
+  while (i < n) {
+    if (nbytes[i] < 0 || (int64_t)nbytes[i] > src_stride || (int64_t)nbytes[i] + BLOSC2_MAX_OVERHEAD > dst_stride)
+      return BLOSC2_ERROR_INVALID_PARAM;
+    b2h::CompressPlan plan;
+    int32_t computed = 0;
+    rc = b2h::make_compress_plan(&plan, nbytes[i], nbytes[i] + BLOSC2_MAX_OVERHEAD, ctx->clevel, ctx->typesize,
+                                 ctx->blocksize, ctx->splitmode, ctx->filters, ctx->filters_meta, &computed, true,
+                                 ctx->compcode, ctx->compcode_meta, 1, ctx->use_dict);
+    if (rc < 0) return rc;
+    plan.lz_mode = ctx->lz_mode;
+    ctx->blocksize = computed;
+    // the following chunks of the same size request `computed`: same plan while it stays put
+    int32_t j = i + 1;
+    while (j < n && nbytes[j] == nbytes[i]) {
+      b2h::CompressPlan q;
+      int32_t c2 = 0;
+      if (b2h::make_compress_plan(&q, nbytes[j], nbytes[j] + BLOSC2_MAX_OVERHEAD, ctx->clevel, ctx->typesize,
+                                  ctx->blocksize, ctx->splitmode, ctx->filters, ctx->filters_meta, &c2, true,
+                                  ctx->compcode, ctx->compcode_meta, 1, ctx->use_dict) < 0 ||
+          c2 != computed || q.blocksize != plan.blocksize || q.split != plan.split || q.memcpyed != plan.memcpyed ||
+          memcmp(q.header, plan.header, sizeof q.header) != 0)
+        break;
+      j++;
+    }
+    rc = b2h::compress_batch(plan, d_src + (int64_t)i * src_stride, src_stride, j - i, d_dst + (int64_t)i * dst_stride,
+                             dst_stride, d_cbytes + i, d.stream, d.ws);
+    if (rc < 0) {
+      TRACE_ERROR("device compression failed: %s", b2h::last_error());
+      return rc;
+    }
+    i = j;
+  }
+  return 0;
+}
+
+int ctx_compress_device(blosc2_context* ctx, const uint8_t* d_src, const int32_t* nbytes, int32_t n,
+                        int64_t src_stride, uint8_t* d_dst, int64_t dst_stride, int32_t* d_cbytes) {
+  if (!ctx) return BLOSC2_ERROR_NULL_POINTER;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  return compress_device_locked(ctx, d_src, nbytes, n, src_stride, d_dst, dst_stride, d_cbytes);
+}
+
+// n appends' worth of chunks: compressed in groups of <= 512 MiB of output slots, each group
+// packed on the device (pack_chunks) and brought back in ONE copy through pinned memory, then split
+// into malloc'd chunks of exactly cbytes bytes (the shrunk chunk blosc2_schunk_append_chunk keeps,
+// blosc/schunk.c:1055-1058).  On failure nothing is returned (every chunk produced so far is freed).
+int ctx_append_device(blosc2_context* ctx, const uint8_t* d_src, const int32_t* nbytes, int32_t n,
+                      int64_t src_stride, uint8_t** chunks_out) {
+  if (!ctx || (n > 0 && (!nbytes || !d_src || !chunks_out))) return BLOSC2_ERROR_NULL_POINTER;
+  if (n < 0) return BLOSC2_ERROR_INVALID_PARAM;
+  int32_t maxnb = 0;
+  for (int32_t i = 0; i < n; i++) {
+    chunks_out[i] = nullptr;
+    if (nbytes[i] < 0 || nbytes[i] > BLOSC2_MAX_BUFFERSIZE || (int64_t)nbytes[i] > src_stride)
+      return BLOSC2_ERROR_INVALID_PARAM;
+    maxnb = std::max(maxnb, nbytes[i]);
+  }
+  if (n == 0) return 0;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  Device& d = ctx->dev;
+  if (!d.init()) return BLOSC2_ERROR_FAILURE;
+  const int64_t dst_stride = ((int64_t)maxnb + BLOSC2_MAX_OVERHEAD + 255) & ~int64_t(255);
+  const int32_t group = (int32_t)std::max<int64_t>(1, std::min<int64_t>(n, (int64_t(512) << 20) / dst_stride));
+  const size_t cb_bytes = ((size_t)group * 4 + 63) & ~size_t(63);
+  if (!d.out.ensure((size_t)(group * dst_stride)) || !d.in.ensure((size_t)(group * dst_stride)) ||
+      !d.small.ensure(cb_bytes + 8 * ((size_t)group + 1)))
+    return BLOSC2_ERROR_MEMORY_ALLOC;
+  int32_t* d_cb = reinterpret_cast<int32_t*>(d.small.p);
+  int64_t* d_off = reinterpret_cast<int64_t*>(d.small.u8() + cb_bytes);
+  std::vector<int64_t> off((size_t)group + 1);
+  auto fail = [&](int rc) {
+    for (int32_t i = 0; i < n; i++) {
+      free(chunks_out[i]);
+      chunks_out[i] = nullptr;
+    }
+    return rc;
+  };
+  for (int32_t g0 = 0; g0 < n; g0 += group) {
+    const int32_t m = std::min(group, n - g0);
+    int rc = compress_device_locked(ctx, d_src + (int64_t)g0 * src_stride, nbytes + g0, m, src_stride, d.out.u8(),
+                                    dst_stride, d_cb);
+    if (rc < 0) return fail(rc);
+    if (b2h::pack_chunks(d.out.u8(), dst_stride, d_cb, m, d.in.u8(), d_off, d.stream) < 0) return fail(BLOSC2_ERROR_FAILURE);
+    if (hipMemcpyAsync(off.data(), d_off, 8 * ((size_t)m + 1), hipMemcpyDeviceToHost, d.stream) != hipSuccess ||
+        hipStreamSynchronize(d.stream) != hipSuccess)
+      return fail(BLOSC2_ERROR_FAILURE);
+    for (int32_t k = 0; k < m; k++)
+      if (off[k + 1] - off[k] < BLOSC_MIN_HEADER_LENGTH) return fail(BLOSC2_ERROR_FAILURE);   // never with destsize nbytes + 32
+    const int64_t total = off[m];
+    if (!d.host.ensure((size_t)total)) return fail(BLOSC2_ERROR_MEMORY_ALLOC);
+    if (hipMemcpyAsync(d.host.p, d.in.p, (size_t)total, hipMemcpyDeviceToHost, d.stream) != hipSuccess ||
+        hipStreamSynchronize(d.stream) != hipSuccess)
+      return fail(BLOSC2_ERROR_FAILURE);
+    for (int32_t k = 0; k < m; k++) {
+      const size_t sz = (size_t)(off[k + 1] - off[k]);
+      uint8_t* c = static_cast<uint8_t*>(malloc(sz));
+      if (!c) return fail(BLOSC2_ERROR_MEMORY_ALLOC);
+      memcpy(c, d.host.u8() + off[k], sz);
+      chunks_out[g0 + k] = c;
+    }
+  }
+  return 0;
+}
+
+// n host chunks (what blosc2_schunk_decompress_chunk would be handed one by one, schunk.c:1481-1530)
+// staged into pinned memory, copied to HBM in one DMA and decoded by one device batch straight into
+// d_dst + i * dst_stride.  Chunks with user-registered filters / codecs run the host-callback pipeline
+// one by one and are copied up afterwards.  A pending blosc2_set_maskout is not applied (it stays
+// for the next blosc2_decompress_ctx).  Returns 0 or the first chunk's error (status[] has them all).
+int ctx_decompress_device(blosc2_context* ctx, const uint8_t* const* chunks, int32_t n, uint8_t* d_dst,
+                          int64_t dst_stride, int32_t dst_cap, int32_t* status) {
+  if (!ctx || (n > 0 && (!chunks || !status || !d_dst))) return BLOSC2_ERROR_NULL_POINTER;
+  if (n < 0 || dst_cap < 0 || (n > 1 && dst_stride < dst_cap)) return BLOSC2_ERROR_INVALID_PARAM;
+  if (ctx->do_compress != 0) return BLOSC2_ERROR_INVALID_PARAM;
+  if (n == 0) return 0;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  Device& d = ctx->dev;
+  if (!d.init()) return BLOSC2_ERROR_FAILURE;
+  std::vector<int32_t> dev_idx, host_idx, nb((size_t)n, 0), cb((size_t)n, 0);
+  std::vector<int64_t> at;
+  int64_t total_c = 0, total_d = 0;
+  for (int32_t i = 0; i < n; i++) {
+    status[i] = 0;
+    const uint8_t* c = chunks[i];
+    if (!c) continue;   // an empty slot decompresses to nothing (schunk.c:1495-1498)
+    int rc = blosc2_cbuffer_sizes(c, &nb[i], &cb[i], nullptr);
+    if (rc < 0) {
+      status[i] = rc;
+      continue;
+    }
+    if (dst_cap < nb[i]) {   // schunk.c:1505-1509
+      status[i] = BLOSC2_ERROR_INVALID_PARAM;
+      continue;
+    }
+    ChunkHdr H;
+    if (read_header(c, cb[i], &H) == 0 && chunk_needs_host(c, H)) {
+      host_idx.push_back(i);
+      continue;
+    }
+    dev_idx.push_back(i);
+    at.push_back(total_c);
+    total_c += ((int64_t)cb[i] + 63) & ~int64_t(63);
+    total_d += std::max(nb[i], 0);
+  }
+  const int32_t m = (int32_t)dev_idx.size();
+  if (m > 0) {
+    const size_t tbytes = (size_t)m * (8 + 8 + 4 + 4);
+    if (!d.host.ensure((size_t)total_c + tbytes) || !d.in.ensure((size_t)total_c) || !d.small.ensure(tbytes + 4 * (size_t)m))
+      return BLOSC2_ERROR_MEMORY_ALLOC;
+    // one SoA table in the small buffer: src ptrs | dst ptrs | srcsizes | dstsizes | status
+    uint8_t* sm = d.small.u8();
+    const uint8_t** h_s = reinterpret_cast<const uint8_t**>(d.host.u8() + total_c);
+    uint8_t** h_o = reinterpret_cast<uint8_t**>(d.host.u8() + total_c + 8 * (size_t)m);
+    int32_t* h_ss = reinterpret_cast<int32_t*>(h_o + m);
+    int32_t* h_ds = h_ss + m;
+    for (int32_t k = 0; k < m; k++) {
+      const int32_t i = dev_idx[k];
+      memcpy(d.host.u8() + at[k], chunks[i], (size_t)cb[i]);
+      h_s[k] = d.in.u8() + at[k];
+      h_o[k] = d_dst + (int64_t)i * dst_stride;
+      h_ss[k] = cb[i];
+      h_ds[k] = dst_cap;
+    }
+    if (hipMemcpyAsync(d.in.p, d.host.p, (size_t)total_c, hipMemcpyHostToDevice, d.stream) != hipSuccess ||
+        hipMemcpyAsync(sm, h_s, tbytes, hipMemcpyHostToDevice, d.stream) != hipSuccess)
+      return BLOSC2_ERROR_FAILURE;
+    const uint8_t* const* d_s = reinterpret_cast<const uint8_t* const*>(sm);
+    uint8_t* const* d_o = reinterpret_cast<uint8_t* const*>(sm + 8 * (size_t)m);
+    const int32_t* d_ss = reinterpret_cast<const int32_t*>(sm + 16 * (size_t)m);
+    const int32_t* d_ds = d_ss + m;
+    int32_t* d_st = const_cast<int32_t*>(d_ds + m);
+    int rc = b2h::decompress_batch(d_s, d_ss, d_o, d_ds, m, total_d, d_st, nullptr, d.stream, d.ws, total_c, 0);
+    if (rc < 0) {
+      TRACE_ERROR("device decompression failed: %s", b2h::last_error());
+      return rc;
+    }
+    std::vector<int32_t> st((size_t)m);
+    if (hipMemcpyAsync(st.data(), d_st, 4 * (size_t)m, hipMemcpyDeviceToHost, d.stream) != hipSuccess ||
+        hipStreamSynchronize(d.stream) != hipSuccess)
+      return BLOSC2_ERROR_FAILURE;
+    for (int32_t k = 0; k < m; k++) {
+      const int32_t i = dev_idx[k];
+      status[i] = st[k] < 0 ? st[k] : (st[k] != nb[i] ? BLOSC2_ERROR_FAILURE : st[k]);   // schunk.c:1511-1517
+    }
+  }
+  std::vector<uint8_t> tmp;
+  for (int32_t i : host_idx) {
+    tmp.resize((size_t)std::max(nb[i], 1));
+    int r = decompress_host(ctx, chunks[i], cb[i], tmp.data(), nb[i], nullptr);
+    if (r >= 0 && r != nb[i]) r = BLOSC2_ERROR_FAILURE;
+    if (r > 0 && hipMemcpy(d_dst + (int64_t)i * dst_stride, tmp.data(), (size_t)r, hipMemcpyHostToDevice) != hipSuccess)
+      r = BLOSC2_ERROR_FAILURE;
+    status[i] = r;
+  }
+  for (int32_t i = 0; i < n; i++)
+    if (status[i] < 0) return status[i];
+  return 0;
+}
+}  // namespace b2h
+
+namespace {
+
 blosc2_context* g_global_cctx = nullptr;
 blosc2_context* g_global_dctx = nullptr;
 
@@ -1164,6 +1414,26 @@ int blosc2_getitem_ctx(blosc2_context* context, const void* src, int32_t srcsize
   if (rc < 0) return rc;
   memcpy(dest, full.data() + sb, (size_t)nib);
   return (int)nib;
+}
+
+// blosc/blosc2.c:4552-4578: byte offsets, checked against the chunk's stored typesize, then getitem.
+int blosc2_getitem_bytes_ctx(blosc2_context* context, const void* src, int32_t srcsize, int32_t start, int32_t nbytes,
+                             void* dest, int32_t destsize) {
+  if (!context) return BLOSC2_ERROR_NULL_POINTER;
+  ChunkHdr H;
+  int rc = read_header(src, srcsize, &H);
+  if (rc < 0) return rc;
+  if (start < 0 || nbytes < 0) {
+    TRACE_ERROR("`start` and `nbytes` must not be negative.");
+    return BLOSC2_ERROR_INVALID_PARAM;
+  }
+  const int32_t ts = H.typesize;
+  if (start % ts != 0 || nbytes % ts != 0) {
+    TRACE_ERROR("`start` (%d) and `nbytes` (%d) must both be multiples of the typesize stored in the chunk (%d).",
+                start, nbytes, ts);
+    return BLOSC2_ERROR_INVALID_PARAM;
+  }
+  return blosc2_getitem_ctx(context, src, srcsize, start / ts, nbytes / ts, dest, destsize);
 }
 
 int blosc2_getitem(const void* src, int32_t srcsize, int start, int nitems, void* dest, int32_t destsize) {

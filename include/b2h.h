@@ -118,6 +118,26 @@ BLOSC_EXPORT int b2h_frame_get_slice(b2h_frame *frame, int64_t start, int64_t st
  * chunksize / blocksize, or sizes that are not multiples of typesize. */
 BLOSC_EXPORT int b2h_frame_get_sparse_buffer(b2h_frame *frame, int64_t ncoords, const int64_t *coords, void *buffer);
 
+/* ---- super-chunk device batches (include/blosc2.h blosc2_schunk, in-memory sparse storage) ----
+ * The reference walks a super-chunk one chunk per call (blosc2_schunk_append_buffer,
+ * blosc/schunk.c:1459-1477; blosc2_schunk_decompress_chunk, 1481-1530; blosc2_schunk_get_slice_buffer,
+ * 1662-1783).  These run many of those calls as one device batch, with the super-chunk's own
+ * contexts, and leave the super-chunk exactly as the serial calls leave it (chunk bytes, nbytes,
+ * cbytes, chunksize, the cctx's sticky blocksize).  Synchronous.
+ *
+ * append: chunk i = d_src + i*src_stride (device), nbytes[i] bytes (HOST array), appended in order.
+ *   Returns the new nchunks or BLOSC2_ERROR_*.  Pipelines with user-registered filters / codecs
+ *   run the serial appends (through host memory).
+ * decompress: chunks [nchunk, nchunk + n) into d_dst + i*dst_stride (device, capacity dst_capacity);
+ *   status[i] (HOST, optional) = blosc2_schunk_decompress_chunk's return for chunk nchunk + i.
+ *   Returns 0 or the first chunk error; BLOSC2_ERROR_INVALID_PARAM for a range outside the schunk.
+ * get_slice: items [start, stop) into device memory d_dst (blosc2_schunk_get_slice_buffer). */
+BLOSC_EXPORT int64_t b2h_schunk_append_device(blosc2_schunk *schunk, const void *d_src, const int32_t *nbytes,
+                                              int32_t n, int64_t src_stride);
+BLOSC_EXPORT int b2h_schunk_decompress_device(blosc2_schunk *schunk, int64_t nchunk, int32_t n, void *d_dst,
+                                              int64_t dst_stride, int32_t dst_capacity, int32_t *status);
+BLOSC_EXPORT int b2h_schunk_get_slice_device(blosc2_schunk *schunk, int64_t start, int64_t stop, void *d_dst);
+
 /* Per-context BloscLZ encoder mode.  Built-in BloscLZ does not read blosc2_cparams.codec_params
  * (reference include/blosc2.h:1207; only user codecs receive it), so a context selects its encoder
  * by pointing codec_params at one of these when it is created (blosc2_create_cctx copies the mode;

@@ -418,6 +418,127 @@ BLOSC_EXPORT int32_t blosc2_unshuffle(int32_t typesize, int32_t blocksize, const
 BLOSC_EXPORT int32_t blosc2_bitshuffle(int32_t typesize, int32_t blocksize, const void *src, void *dest);
 BLOSC_EXPORT int32_t blosc2_bitunshuffle(int32_t typesize, int32_t blocksize, const void *src, void *dest);
 
+/* partial decode by bytes: include/blosc2.h:1735 (blosc2_getitem_bytes_ctx, blosc/blosc2.c:4552-4577):
+ * `start` and `nbytes` count bytes and must be multiples of the chunk's stored typesize. */
+BLOSC_EXPORT int blosc2_getitem_bytes_ctx(blosc2_context *context, const void *src, int32_t srcsize, int32_t start,
+                                          int32_t nbytes, void *dest, int32_t destsize);
+
+/* ---- super-chunks (include/blosc2.h:1740-2362): the container the reference's callers reach the
+ * chunk engine through (blosc/schunk.c).  Structs ABI-identical; the engine keeps IN-MEMORY, SPARSE
+ * super-chunks (storage.contiguous == false, urlpath == NULL): chunks are malloc'd host buffers
+ * indexed by schunk->data, exactly as the reference's frame-less schunk.  Frame-backed storage
+ * (contiguous frames, files, directories) is outside the device engine (DESIGN.md §7;
+ * the read side of contiguous frames is include/b2h.h b2h_frame_*): blosc2_schunk_new returns NULL
+ * for it.  The device-batch forms (b2h_schunk_append_device / b2h_schunk_decompress_device in
+ * include/b2h.h) run one engine launch over many chunks of a super-chunk. ---- */
+enum {   /* include/blosc2.h:994-1005 */
+  BLOSC2_IO_FILESYSTEM = 0,
+  BLOSC2_IO_FILESYSTEM_MMAP = 1,
+  BLOSC_IO_LAST_BLOSC_DEFINED = 2,
+  BLOSC_IO_LAST_REGISTERED = 32,
+};
+enum {
+  BLOSC2_IO_BLOSC_DEFINED = 32,
+  BLOSC2_IO_REGISTERED = 160,
+  BLOSC2_IO_USER_DEFINED = 256
+};
+/* include/blosc2.h:1047-1059 */
+typedef struct {
+  uint8_t id;
+  const char *name;
+  void *params;
+} blosc2_io;
+static const blosc2_io BLOSC2_IO_DEFAULTS = {BLOSC2_IO_FILESYSTEM, "filesystem", NULL};
+
+#define BLOSC2_MAX_METALAYERS 16                  /* include/blosc2.h:1744 */
+#define BLOSC2_METALAYER_NAME_MAXLEN 31
+#define BLOSC2_MAX_VLMETALAYERS (8 * 1024)        /* include/blosc2.h:1750 */
+#define BLOSC2_VLMETALAYERS_NAME_MAXLEN BLOSC2_METALAYER_NAME_MAXLEN
+
+/* include/blosc2.h:1758-1776 */
+typedef struct {
+  bool contiguous;
+  char *urlpath;
+  blosc2_cparams *cparams;
+  blosc2_dparams *dparams;
+  blosc2_io *io;
+} blosc2_storage;
+static const blosc2_storage BLOSC2_STORAGE_DEFAULTS = {false, NULL, NULL, NULL, NULL};
+
+/* defaults getters: include/blosc2.h:1781-1796 (blosc/blosc2.c:6896-6911) */
+BLOSC_EXPORT blosc2_cparams blosc2_get_blosc2_cparams_defaults(void);
+BLOSC_EXPORT blosc2_dparams blosc2_get_blosc2_dparams_defaults(void);
+BLOSC_EXPORT blosc2_storage blosc2_get_blosc2_storage_defaults(void);
+BLOSC_EXPORT blosc2_io blosc2_get_blosc2_io_defaults(void);
+
+typedef struct blosc2_frame_s blosc2_frame;   /* opaque (include/blosc2.h:1803) */
+
+/* include/blosc2.h:1810-1814 */
+typedef struct blosc2_metalayer {
+  char *name;
+  uint8_t *content;
+  int32_t content_len;
+} blosc2_metalayer;
+
+/* include/blosc2.h:1823-1892 */
+typedef struct blosc2_schunk {
+  uint8_t version;
+  uint8_t compcode;
+  uint8_t compcode_meta;
+  uint8_t clevel;
+  uint8_t splitmode;
+  int32_t typesize;
+  int32_t blocksize;
+  int32_t chunksize;
+  uint8_t flags2;
+  uint8_t use_dict;
+  uint8_t filters[BLOSC2_MAX_FILTERS];
+  uint8_t filters_meta[BLOSC2_MAX_FILTERS];
+  int64_t nchunks;
+  int64_t current_nchunk;
+  int64_t nbytes;
+  int64_t cbytes;
+  uint8_t **data;
+  size_t data_len;
+  blosc2_storage *storage;
+  blosc2_frame *frame;
+  blosc2_context *cctx;
+  blosc2_context *dctx;
+  struct blosc2_metalayer *metalayers[BLOSC2_MAX_METALAYERS];
+  uint16_t nmetalayers;
+  struct blosc2_metalayer *vlmetalayers[BLOSC2_MAX_VLMETALAYERS];
+  int16_t nvlmetalayers;
+  void *tuner_params;
+  int tuner_id;
+  int8_t ndim;
+  int64_t *blockshape;
+  bool view;
+  int64_t change_tick;
+} blosc2_schunk;
+
+/* include/blosc2.h:1905 (blosc/schunk.c:163-242) */
+BLOSC_EXPORT blosc2_schunk *blosc2_schunk_new(blosc2_storage *storage);
+/* include/blosc2.h:2088 (blosc/schunk.c:679-729) */
+BLOSC_EXPORT int blosc2_schunk_free(blosc2_schunk *schunk);
+/* include/blosc2.h:2101, 2115, 2129, 2140 (blosc/schunk.c:975-1457) */
+BLOSC_EXPORT int64_t blosc2_schunk_append_chunk(blosc2_schunk *schunk, uint8_t *chunk, bool copy);
+BLOSC_EXPORT int64_t blosc2_schunk_update_chunk(blosc2_schunk *schunk, int64_t nchunk, uint8_t *chunk, bool copy);
+BLOSC_EXPORT int64_t blosc2_schunk_insert_chunk(blosc2_schunk *schunk, int64_t nchunk, uint8_t *chunk, bool copy);
+BLOSC_EXPORT int64_t blosc2_schunk_delete_chunk(blosc2_schunk *schunk, int64_t nchunk);
+/* include/blosc2.h:2152 (blosc/schunk.c:1459-1477) */
+BLOSC_EXPORT int64_t blosc2_schunk_append_buffer(blosc2_schunk *schunk, const void *src, int32_t nbytes);
+/* include/blosc2.h:2171 (blosc/schunk.c:1481-1530) */
+BLOSC_EXPORT int blosc2_schunk_decompress_chunk(blosc2_schunk *schunk, int64_t nchunk, void *dest, int32_t nbytes);
+/* include/blosc2.h:2196, 2236 (blosc/schunk.c:1543-1631) */
+BLOSC_EXPORT int blosc2_schunk_get_chunk(blosc2_schunk *schunk, int64_t nchunk, uint8_t **chunk, bool *needs_free);
+BLOSC_EXPORT int blosc2_schunk_get_lazychunk(blosc2_schunk *schunk, int64_t nchunk, uint8_t **chunk,
+                                             bool *needs_free);
+/* include/blosc2.h:2275 (blosc/schunk.c:1662-1783) */
+BLOSC_EXPORT int blosc2_schunk_get_slice_buffer(blosc2_schunk *schunk, int64_t start, int64_t stop, void *buffer);
+/* include/blosc2.h:2316, 2328 (blosc/schunk.c:70-105) */
+BLOSC_EXPORT int blosc2_schunk_get_cparams(blosc2_schunk *schunk, blosc2_cparams **cparams);
+BLOSC_EXPORT int blosc2_schunk_get_dparams(blosc2_schunk *schunk, blosc2_dparams **dparams);
+
 #ifdef __cplusplus
 }
 #endif

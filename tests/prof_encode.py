@@ -14,7 +14,7 @@ src = gen_f32_device(0, nch * chunk // 4, torch.device("cuda", 0)).view(torch.ui
 stride = chunk + 256
 dst = torch.empty(nch * stride, dtype=torch.uint8, device="cuda")
 cb = torch.zeros(nch, dtype=torch.int32, device="cuda")
-cp = B.cparams(clevel=5, typesize=4)
+cp = B.cparams(clevel=5, typesize=4, lz_mode=int(sys.argv[2]) if len(sys.argv) > 2 else None)
 L = B.lib()
 L.b2h_enable_timing(1)
 for _ in range(2):

@@ -1,0 +1,207 @@
+"""GPU tier: the super-chunk C ABI (include/blosc2.h blosc2_schunk_*, include/b2h.h b2h_schunk_*)
+driving the HIP engine, against the reference build (oracle/_ref, blosc/schunk.c) doing the same
+calls on the host.
+
+Expected, for every pipeline: the same chunks byte for byte and the same counters after serial
+appends (blosc2_schunk_append_buffer, schunk.c:1459-1477) and after ONE batched device append of the
+same buffers (b2h_schunk_append_device) -- including the context's sticky blocksize, checked by one
+more serial append afterwards; decompress_chunk / the batched device decompression restore the
+input with the reference's return codes; get_slice_buffer / the device slice equal the reference's
+slices on ranges that start and end inside chunks, at chunk edges, in the short last chunk.
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "c-blosc2_amd"))
+sys.path.insert(0, HERE)
+
+import blosc2_amd as B  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+CHUNK = 256 * 1024
+PIPES = {
+    "shuffle4": dict(clevel=5, typesize=4, filters=(0, 0, 0, 0, 0, 1)),
+    "delta_shuffle8": dict(clevel=5, typesize=8, filters=(0, 0, 0, 0, 3, 1)),
+    "bitshuffle4_c9": dict(clevel=9, typesize=4, filters=(0, 0, 0, 0, 0, 2)),
+    "lz4_shuffle8": dict(clevel=5, typesize=8, filters=(0, 0, 0, 0, 0, 1), compcode=1),
+    "noshuffle_c1": dict(clevel=1, typesize=2, filters=(0, 0, 0, 0, 0, 0)),
+}
+
+
+def _ref():
+    from oracle_lib import ref
+    R = ref()
+    if R is None:
+        pytest.skip("reference build absent")
+    return B.bind_schunk(R)
+
+
+def _pair(kw):
+    """(product schunk, reference schunk) with the same cparams."""
+    from b2ctypes import cparams as rcp, dparams as rdp
+    R = _ref()
+    a = B.SChunk(B.cparams(**kw), B.dparams())
+    b = B.SChunk(rcp(**kw), rdp(), L=R)
+    return a, b
+
+
+def _data(ts, nchunks, tail):
+    from datagen import gen_f32, int64_ramp
+    n = nchunks * CHUNK + tail
+    a = int64_ramp(3, (n + 7) // 8).view(np.uint8)[:n].copy()
+    f = gen_f32(1, CHUNK // 4).view(np.uint8)
+    for i in range(1, nchunks, 2):   # alternate compressible / noisy chunks
+        a[i * CHUNK:(i + 1) * CHUNK] = f
+    return a, [CHUNK] * nchunks + ([tail] if tail else [])
+
+
+def _chunks(sc):
+    return [sc.chunk(i) for i in range(sc.s.nchunks)]
+
+
+def _assert_same(a, b):
+    assert a.counters() == b.counters()
+    for i, (u, v) in enumerate(zip(_chunks(a), _chunks(b))):
+        assert np.array_equal(u, v), i
+
+
+@pytest.mark.parametrize("pipe", sorted(PIPES))
+def test_append_buffer_serial_matches_reference(pipe):
+    kw = PIPES[pipe]
+    data, sizes = _data(kw["typesize"], 5, 100 * 1024 + 8 * 3)
+    a, b = _pair(kw)
+    try:
+        off = 0
+        for n in sizes:
+            ra, rb = a.append_buffer(data[off:off + n]), b.append_buffer(data[off:off + n])
+            assert ra == rb
+            off += n
+        _assert_same(a, b)
+        for i, n in enumerate(sizes):
+            rc, out = a.decompress_chunk(i, CHUNK)
+            assert rc == n
+            assert np.array_equal(out, data[i * CHUNK:i * CHUNK + n])
+        # too small a destination: the reference's code, before any decompression (schunk.c:1505)
+        assert a.decompress_chunk(0, 100)[0] == b.decompress_chunk(0, 100)[0] == -12
+    finally:
+        a.free()
+        b.free()
+
+
+@pytest.mark.parametrize("pipe", sorted(PIPES))
+def test_append_device_batch_matches_serial_reference(pipe):
+    import torch
+    kw = PIPES[pipe]
+    data, sizes = _data(kw["typesize"], 7, 33 * 1024)
+    dev = torch.from_numpy(data).cuda()
+    a, b = _pair(kw)
+    try:
+        sz = (C.c_int32 * len(sizes))(*sizes)
+        r = a.L.b2h_schunk_append_device(a.p, C.c_void_p(dev.data_ptr()), sz, len(sizes), CHUNK)
+        off = 0
+        for n in sizes:
+            rb = b.append_buffer(data[off:off + n])
+            off += n
+        assert r == rb == len(sizes)
+        _assert_same(a, b)
+        # the cctx's sticky blocksize is where the serial appends leave it
+        extra = data[:CHUNK]
+        assert a.append_buffer(extra) == b.append_buffer(extra)
+        _assert_same(a, b)
+        # batched device decompression of every chunk
+        n = a.s.nchunks
+        out = torch.empty(n * CHUNK, dtype=torch.uint8, device="cuda")
+        st = (C.c_int32 * n)()
+        rc = a.L.b2h_schunk_decompress_device(a.p, 0, n, C.c_void_p(out.data_ptr()), CHUNK, CHUNK, st)
+        torch.cuda.synchronize()
+        assert rc == 0
+        assert list(st) == sizes + [CHUNK]
+        host = out.cpu().numpy()
+        for i, m in enumerate(sizes):
+            assert np.array_equal(host[i * CHUNK:i * CHUNK + m], data[i * CHUNK:i * CHUNK + m]), i
+        assert np.array_equal(host[len(sizes) * CHUNK:], extra)
+        # capacity below a chunk's nbytes: per-chunk INVALID_PARAM, as decompress_chunk returns it
+        st2 = (C.c_int32 * 2)()
+        assert a.L.b2h_schunk_decompress_device(a.p, 0, 2, C.c_void_p(out.data_ptr()), CHUNK, 1000, st2) == -12
+        assert list(st2) == [-12, -12]
+        assert a.L.b2h_schunk_decompress_device(a.p, n - 1, 2, C.c_void_p(out.data_ptr()), CHUNK, CHUNK, st2) == -12
+    finally:
+        a.free()
+        b.free()
+
+
+SLICES = [(0, 10), (5, 70000), (CHUNK // 8 - 3, CHUNK // 8 + 5), (0, 3 * CHUNK // 8), (CHUNK // 8, 3 * CHUNK // 8),
+          (2 * CHUNK // 8 + 1, 5 * CHUNK // 8 + 100 * 128 + 3), (5 * CHUNK // 8 + 17, 5 * CHUNK // 8 + 100 * 128 + 3),
+          (7, 7)]
+
+
+@pytest.mark.parametrize("pipe", ["delta_shuffle8", "lz4_shuffle8"])
+def test_get_slice_matches_reference(pipe):
+    import torch
+    kw = PIPES[pipe]
+    data, sizes = _data(8, 5, 100 * 1024 + 24)
+    a, b = _pair(kw)
+    try:
+        off = 0
+        for n in sizes:
+            a.append_buffer(data[off:off + n])
+            b.append_buffer(data[off:off + n])
+            off += n
+        items = data.view(np.int64)
+        total = len(items)
+        for lo, hi in SLICES + [(total - 9, total), (0, total)]:
+            ra, xa = a.get_slice(lo, hi)
+            rb, xb = b.get_slice(lo, hi)
+            assert ra == rb == 0, (lo, hi)
+            assert np.array_equal(xa, xb), (lo, hi)
+            assert np.array_equal(xa.view(np.int64), items[lo:hi]), (lo, hi)
+            d = torch.zeros(max(hi - lo, 1) * 8, dtype=torch.uint8, device="cuda")
+            assert a.L.b2h_schunk_get_slice_device(a.p, lo, hi, C.c_void_p(d.data_ptr())) == 0
+            torch.cuda.synchronize()
+            assert np.array_equal(d.cpu().numpy()[:(hi - lo) * 8], xa), (lo, hi)
+        # outside the super-chunk: refused (the reference reads past its chunks here)
+        buf = np.zeros(64, np.uint8)
+        assert a.L.blosc2_schunk_get_slice_buffer(a.p, total - 1, total + 1, B._p(buf)) == -12
+        assert a.L.blosc2_schunk_get_slice_buffer(a.p, 5, 3, B._p(buf)) == -12
+    finally:
+        a.free()
+        b.free()
+
+
+def test_decompress_device_mixed_chunks_match_reference():
+    """A variable-chunksize super-chunk of special, golden (blosc1 / blosc2, BloscLZ / LZ4) and
+    engine-made chunks decodes in one batch to the reference's bytes."""
+    import torch
+    from test_schunk_abi import _gold, _special
+    R = _ref()
+    a, b = _pair(dict(clevel=5, typesize=4))
+    try:
+        src = np.arange(300_000, dtype=np.int32)
+        for sc in (a, b):
+            L = sc.L
+            for c in (_special(L, "zeros", 4_000_000), _gold("blosc-blosclz-3.0.0.cdata"),
+                      _gold("blosc-lz4-3.0.0.cdata"), _special(L, "repeat", 40_000),
+                      _gold("blosc-1.14.0-lz4.cdata")):
+                assert sc.append_chunk(c) > 0
+            assert sc.append_buffer(src) > 0
+        _assert_same(a, b)
+        n = a.s.nchunks
+        cap = 4_000_000
+        out = torch.zeros(n * cap, dtype=torch.uint8, device="cuda")
+        st = (C.c_int32 * n)()
+        assert a.L.b2h_schunk_decompress_device(a.p, 0, n, C.c_void_p(out.data_ptr()), cap, cap, st) == 0
+        torch.cuda.synchronize()
+        host = out.cpu().numpy()
+        for i in range(n):
+            rb, xb = b.decompress_chunk(i, cap)
+            assert st[i] == rb, i
+            assert np.array_equal(host[i * cap:i * cap + rb], xb), i
+    finally:
+        a.free()
+        b.free()
