@@ -1685,6 +1685,12 @@ static int fuse_bits() {
   return e ? atoi(e) : 83;
 }
 static bool fuse_enabled() { return (fuse_bits() & 1) != 0; }
+// B2H_FUSE_GRID (tests): cap the fused launch's persistent grid -- a few workgroups then do every
+// shuffle, stream, finalisation and scatter item, the hand-off waits' worst case.
+static int64_t fuse_grid_cap(int64_t slots) {
+  const char* e = getenv("B2H_FUSE_GRID");
+  return e && atoi(e) > 0 ? std::min<int64_t>(slots, atoi(e)) : slots;
+}
 static int fuse_lead() {
   static const int v = [] { const char* e = getenv("B2H_SHUF_LEAD"); return e ? std::max(1, atoi(e)) : 512; }();
   return v;
@@ -1718,7 +1724,7 @@ static int launch_encode_fast_fused_t(Workspace* ws, const CGeom& g, const uint8
     attr_set = true;
   }
   const int slots = resident_slots(fn, lds, 128);
-  const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(ntot, slots));
+  const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(ntot, fuse_grid_cap(slots)));
   if (fuse_prepare(ws, g, ntot, f, st)) return E_MEMORY;
   static int32_t* trace = nullptr;
   static const bool tr = getenv("B2H_FUSE_TRACE") != nullptr;
@@ -1953,7 +1959,8 @@ static int launch_encode_exact_fused(Workspace* ws, const CGeom& g, int hashlog,
     attr_set = true;
   }
   const int slots = resident_slots(fn, lds, 64 * (NL + NG));
-  const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>((ntot + NL + NG - 1) / (NL + NG), slots));
+  const uint32_t grid =
+      (uint32_t)std::max<int64_t>(1, std::min<int64_t>((ntot + NL + NG - 1) / (NL + NG), fuse_grid_cap(slots)));
   if (ws->gtab.ensure(((size_t)grid * NG << hashlog) * sizeof(POS))) return E_MEMORY;
   if (fuse_prepare(ws, g, ntot, f, st)) return E_MEMORY;
   k_encode_fused<POS, NL, NG><<<grid, 64 * (NL + NG), lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot,

@@ -99,14 +99,16 @@ def _index(sizes, stride):
     return cid * stride + pos, offs
 
 
-def pack_chunks(comp, stride, cbytes):
+def pack_chunks(comp, stride, cbytes, total=None):
     """Concatenate the compressed chunks of a batch (chunk i at comp[i*stride:], cbytes[i] bytes)
-    into one contiguous buffer.  Returns (packed uint8, offsets int64[n+1]) on comp's device."""
+    into one contiguous buffer.  Returns (packed uint8, offsets int64[n+1]) on comp's device.
+    `total` (the sum of cbytes, when the caller already knows it on the host) saves a host sync."""
     sizes = cbytes.to(torch.int64)
     n = sizes.numel()
     if comp.is_cuda:
         import blosc2_amd as B
-        total = int(sizes.sum().item())
+        if total is None:
+            total = int(sizes.sum().item())
         out = torch.empty(max(total, 1), dtype=torch.uint8, device=comp.device)
         offs = torch.empty(n + 1, dtype=torch.int64, device=comp.device)
         c32 = cbytes.to(torch.int32).contiguous()
@@ -169,29 +171,40 @@ def scatter_chunks(full, chunk_nbytes, nchunks, device, root=0, group=None):
     return recv
 
 
-def gather_compressed(comp, stride, cbytes, nchunks, root=0, group=None):
+def gather_compressed(comp, stride, cbytes, nchunks, root=0, group=None, failed=False):
     """Collect every rank's compressed chunks on the root, in chunk order ("gatherv").
-    Returns on the root (frame_bytes uint8, offsets int64[nchunks+1]); None elsewhere."""
+    Returns on the root (frame_bytes uint8, offsets int64[nchunks+1]); None elsewhere.
+
+    The per-chunk sizes are all-gathered on the device and read back ONCE per rank: every P2P
+    count, the packing total and the root's frame size come from that one copy (RCCL needs its
+    counts on the host).  The same exchange carries the failure flag: a rank whose compression
+    failed (`failed`, or a chunk of size <= 0) sends -1 sizes, and every rank raises together
+    after the read-back -- no separate agreement round."""
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     dev = comp.device
-    packed, _ = pack_chunks(comp, stride, cbytes)
     mx = _max_shard(nchunks, world)
-    sz = torch.zeros(mx, dtype=torch.int64, device=dev)
+    spans = [shard_range(nchunks, world, q) for q in range(world)]
+    sz = torch.zeros(mx + 1, dtype=torch.int64, device=dev)
     sz[:cbytes.numel()] = cbytes.to(torch.int64)
-    all_sz = _all_gather(sz, group)                     # per-chunk sizes of every rank (fixed count)
-    lens = torch.cat([all_sz[r][:b - a] for r, (a, b) in
-                      enumerate(shard_range(nchunks, world, q) for q in range(world))])
-    offsets = torch.zeros(nchunks + 1, dtype=torch.int64, device=dev)
-    offsets[1:] = torch.cumsum(lens, 0)
+    if failed:
+        sz[:cbytes.numel()] = -1
+    sz[mx] = -1 if failed else 0
+    all_sz = torch.stack(_all_gather(sz, group)).cpu()   # the one host sync
+    lens = torch.cat([all_sz[r, :b - a] for r, (a, b) in enumerate(spans)])
+    bad = [r for r, (a, b) in enumerate(spans) if int(all_sz[r, mx]) < 0 or bool((all_sz[r, :b - a] <= 0).any())]
+    if bad:
+        raise RuntimeError(f"rank {rank}: compression failed on rank(s) {bad}")
+    host_off = [0] + torch.cumsum(lens, 0).tolist()
+    a, b = spans[rank]
+    packed, _ = pack_chunks(comp, stride, cbytes, total=host_off[b] - host_off[a])
     if rank != root:
         _p2p([(packed, root)], [], group)
         return None
-    host_off = offsets.cpu().tolist()
+    offsets = torch.tensor(host_off, dtype=torch.int64).to(dev, non_blocking=True)
     frame = torch.empty(int(host_off[-1]), dtype=torch.uint8, device=dev)
     recvs = []
-    for r in range(world):
-        a, b = shard_range(nchunks, world, r)
-        piece = frame[int(host_off[a]):int(host_off[b])]
+    for r, (a, b) in enumerate(spans):
+        piece = frame[host_off[a]:host_off[b]]
         if r == root:
             piece.copy_(packed)
         else:
@@ -280,17 +293,15 @@ def compress_schunk(full, chunk_nbytes, nchunks, cparams, device, compress_batch
     n = hi - lo
     comp = torch.empty(max(1, n) * stride, dtype=torch.uint8, device=device)
     cbytes = torch.zeros(max(1, n), dtype=torch.int32, device=device)
-    err = None
+    failed = False
     if n:
         try:
             compress_batch(cparams, local, chunk_nbytes, n, comp, stride, cap, cbytes)
-            if not bool((cbytes[:n] > 0).all()):   # 0: did not fit (cannot happen at cap = nbytes + 32)
-                err = f"rank {rank}: a chunk failed to compress: {cbytes[:n].min().item()}"
-        except RuntimeError as e:
-            err = f"rank {rank}: {e}"
-    if not _agree(err is None, group):   # raise on every rank together, before the gather
-        raise RuntimeError(err or f"rank {rank}: another rank failed to compress its chunks")
-    return gather_compressed(comp, stride, cbytes[:n], nchunks, root, group)
+        except RuntimeError:
+            failed = True
+    # a chunk of size <= 0 (did not fit: cannot happen at cap = nbytes + 32) or a failed launch is
+    # seen by every rank in the gather's size exchange, which then raises everywhere together
+    return gather_compressed(comp, stride, cbytes[:n], nchunks, root, group, failed=failed)
 
 
 def decompress_schunk(frame, offsets, chunk_nbytes, nchunks, device, decompress_batch, root=0, group=None):

@@ -350,3 +350,77 @@ def test_gpu_blosclz_mode_per_context_on_threads(fast):
     # a context without codec_params follows the process default
     plain = B.compress(src, clevel=5, typesize=4)
     assert np.array_equal(plain, want[B.FAST] if default == 1 else want[B.EXACT])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lzmode", [1, 0], ids=["fast", "exact"])
+def test_gpu_fused_small_grid_has_no_timeouts(fast, lzmode, monkeypatch):
+    """VERDICT r2 hardening: the fused launch with its persistent grid capped at 1, 2 and 5
+    workgroups (B2H_FUSE_GRID) -- a lone workgroup then runs every shuffle job, stream, chunk
+    finalisation and scatter item, so every hand-off wait has to be met by itself or a peer --
+    writes the separate launches' chunks.  A timed-out wait (sync[4]) would turn every chunk of the
+    batch into E_FAILURE, which the cbytes check catches."""
+    import torch
+    B = fast
+    chunk, n = 4 << 20, 6
+    src = torch.from_numpy(gen_f32(21, n * chunk // 4).view(np.uint8)).cuda()
+    cap = chunk + 64
+    stride = (cap + 255) // 256 * 256
+    cp = B.cparams(clevel=5, typesize=4, lz_mode=lzmode)
+
+    def run():
+        comp = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+        cb = torch.zeros(n, dtype=torch.int32, device="cuda")
+        B.compress_batch(cp, src.data_ptr(), chunk, n, chunk, comp.data_ptr(), stride, cap, cb.data_ptr(), 0)
+        torch.cuda.synchronize()
+        cbh = cb.cpu().numpy()
+        assert (cbh > 0).all(), cbh
+        compb = comp.cpu().numpy().reshape(n, stride)
+        return [compb[i, :cbh[i]].copy() for i in range(n)]
+    monkeypatch.setenv("B2H_FUSE", "0")
+    want = run()
+    monkeypatch.setenv("B2H_FUSE", "83" if lzmode == 1 else "87")
+    for grid in ("1", "2", "5"):
+        monkeypatch.setenv("B2H_FUSE_GRID", grid)
+        got = run()
+        assert all(np.array_equal(a, b) for a, b in zip(got, want)), grid
+
+
+@pytest.mark.gpu
+def test_gpu_fused_launches_on_two_streams_at_once(fast):
+    """Two super-chunks on two host threads append device batches at the same time: two fused
+    launches, each sized for the whole chip, on two contexts' own streams and workspaces, compete
+    for the CUs (part of one launch's grid may wait for the other to leave).  Every chunk equals a
+    lone call's chunk, and no batch reports a failed hand-off wait."""
+    import threading
+    import torch
+    B = fast
+    chunk, n = 4 << 20, 16
+    L = B.lib()
+    host = [gen_f32(s, n * chunk // 4).view(np.uint8) for s in (31, 32)]
+    dev = [torch.from_numpy(h).cuda() for h in host]
+    want = [[B.compress(h[i * chunk:(i + 1) * chunk], clevel=5, typesize=4, lz_mode=B.FAST) for i in range(n)]
+            for h in host]
+    errs = []
+
+    def run(k):
+        try:
+            for _ in range(3):
+                sc = B.SChunk(B.cparams(clevel=5, typesize=4, lz_mode=B.FAST), B.dparams())
+                sizes = (C.c_int32 * n)(*([chunk] * n))
+                r = L.b2h_schunk_append_device(sc.p, C.c_void_p(dev[k].data_ptr()), sizes, n, chunk)
+                if r != n:
+                    errs.append((k, "append", r))
+                for i in range(n):
+                    if not np.array_equal(sc.chunk(i), want[k][i]):
+                        errs.append((k, i))
+                sc.free()
+        except Exception as e:   # noqa: BLE001 -- reported to the main thread
+            errs.append((k, repr(e)))
+    th = [threading.Thread(target=run, args=(k,)) for k in (0, 1)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in th)
+    assert not errs, errs

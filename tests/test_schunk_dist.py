@@ -128,6 +128,8 @@ def _failing_worker(rank, world, port, q):
         _oracle_compress_batch(cparams, src, chunk_nbytes, n, out, stride, cap, cbytes)
         if rank == 1:
             cbytes[0] = 0
+        if rank == 2:
+            raise RuntimeError("b2h_compress_batch: -12")
 
     try:
         full = torch.from_numpy(_data(4)) if rank == 0 else None
@@ -140,16 +142,17 @@ def _failing_worker(rank, world, port, q):
 
 
 def test_schunk_failure_on_one_rank_raises_everywhere():
-    """a rank whose chunk fails must not leave the others blocked in the gather: all
-    ranks agree on the failure (one MIN all-reduce) and raise together, well before any timeout."""
+    """a rank whose chunk fails must not leave the others blocked in the gather: the
+    failure travels in the gather's size exchange and every rank raises together, well before any
+    timeout (rank 1: a chunk of size 0; rank 2: its launch raises)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_failing_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_failing_worker, args=(r, 3, port, q)) for r in range(3)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=120) for _ in range(2))
+    got = dict(q.get(timeout=120) for _ in range(3))
     for p in procs:
         p.join(timeout=60)
-    assert "failed to compress" in got[1], got
-    assert "another rank failed" in got[0], got
+    for r in range(3):
+        assert "compression failed on rank(s) [1, 2]" in got[r], got

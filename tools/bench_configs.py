@@ -199,6 +199,56 @@ def e2e(steps, group_chunks=64, nstreams=3):
             drain(g)
         torch.cuda.synchronize()
 
+    def decompress_group(g, strs, h_from):
+        k = g % nstreams
+        s, b = strs[k], dbuf[k]
+        n = base[g + 1] - base[g]
+        with torch.cuda.stream(s):
+            b["packed"][:n].copy_(h_from[base[g]:base[g + 1]], non_blocking=True)
+            b["off"].copy_(h_off[g], non_blocking=True)
+            B.unpack_chunks(b["packed"].data_ptr(), b["off"].data_ptr(), group_chunks, b["comp"].data_ptr(), stride,
+                            b["cb"].data_ptr(), s.cuda_stream)
+            B.decompress_batch(b["comp"].data_ptr(), stride, b["cb"].data_ptr(), group_chunks, b["raw"].data_ptr(),
+                               chunk, chunk, b["status"].data_ptr(), s.cuda_stream)
+            statuses[g * group_chunks:(g + 1) * group_chunks].copy_(b["status"], non_blocking=True)
+            h_out[g * GN:(g + 1) * GN].copy_(b["raw"], non_blocking=True)
+
+    dstreams = [torch.cuda.Stream() for _ in range(nstreams)]
+
+    def duplex_all(h_from):
+        """Both directions at once: group g compresses (H2D raw, D2H packed) on `streams` while group g
+        of the previous pass's packed bytes decompresses (H2D packed, D2H raw) on `dstreams`, so both
+        PCIe directions carry traffic together (the sequential passes leave one direction idle)."""
+        evs = [None] * G
+        done = [0] * (G + 1)
+
+        def drain(g):
+            evs[g].synchronize()
+            n = int(h_off[g][group_chunks])
+            done[g + 1] = done[g] + n
+            k = g % nstreams
+            with torch.cuda.stream(streams[k]):
+                h_packed[done[g]:done[g] + n].copy_(cbuf[k]["packed"][:n], non_blocking=True)
+        for g in range(G):
+            k = g % nstreams
+            s, b = streams[k], cbuf[k]
+            with torch.cuda.stream(s):
+                b["raw"].copy_(h_src[g * GN:(g + 1) * GN], non_blocking=True)
+                B.compress_batch(cp, b["raw"].data_ptr(), chunk, group_chunks, chunk, b["comp"].data_ptr(), stride, cap,
+                                 b["cb"].data_ptr(), s.cuda_stream)
+                B.pack_chunks(b["comp"].data_ptr(), stride, b["cb"].data_ptr(), group_chunks, b["packed"].data_ptr(),
+                              b["off"].data_ptr(), s.cuda_stream)
+                h_off2[g].copy_(b["off"], non_blocking=True)
+                evs[g] = torch.cuda.Event()
+                evs[g].record(s)
+            decompress_group(g, dstreams, h_from)
+            if g >= nstreams - 1:
+                drain(g - (nstreams - 1))
+        for g in range(max(0, G - (nstreams - 1)), G):
+            drain(g)
+        torch.cuda.synchronize()
+        return done[G]
+
     def decompress_all():
         for g in range(G):
             k = g % nstreams
@@ -234,6 +284,22 @@ def e2e(steps, group_chunks=64, nstreams=3):
     C = base[G]
     exact = bool(torch.equal(h_out, h_src)) and bool((statuses == chunk).all())
     tcm, tdm = float(np.median(tc)), float(np.median(td))
+    # duplex: compress and decompress of the whole workload together (the decompress side reads a
+    # copy of the packed bytes, the compress side rewrites h_packed; the duplex's compressed bytes
+    # and offsets are compared with the sequential pass's afterwards)
+    h_from = h_packed[:C].clone().pin_memory()
+    h_off2 = [torch.zeros(group_chunks + 1, dtype=torch.int64, pin_memory=True) for _ in range(G)]
+    tdup = []
+    dup_exact = True
+    for _ in range(steps):
+        h_out.zero_()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        C2 = duplex_all(h_from)
+        tdup.append(time.perf_counter() - t0)
+        dup_exact = dup_exact and C2 == C and bool(torch.equal(h_out, h_src)) and bool((statuses == chunk).all()) \
+            and bool(torch.equal(h_packed[:C], h_from)) and all(torch.equal(a, b) for a, b in zip(h_off, h_off2))
+    tdupm = float(np.median(tdup))
     mode = "fast" if B.lib().b2h_set_blosclz_mode(-1) == 1 else "exact"
     return {"config": f"E2E: T from/to pinned host memory, {nstreams} streams x groups of {group_chunks} chunks "
                       "(H2D + compress + pack + D2H of the packed bytes; H2D of the packed bytes + unpack + "
@@ -242,7 +308,11 @@ def e2e(steps, group_chunks=64, nstreams=3):
             "compress_GiBps": round(N / GiB / tcm, 3), "decompress_GiBps": round(N / GiB / tdm, 3),
             "GiBps_c_plus_d": round(N / GiB / (tcm + tdm), 3),
             "pcie_bytes_per_s": {"compress": round((N + C) / tcm / 1e9, 2), "decompress": round((N + C) / tdm / 1e9, 2),
-                                 "unit": "GB/s (H2D + D2H bytes / wall)"}}
+                                 "unit": "GB/s (H2D + D2H bytes / wall)"},
+            "duplex": {"what": "compress and decompress of the workload overlapped (both PCIe directions busy)",
+                       "round_trip_exact": dup_exact, "ms": round(tdupm * 1e3, 2),
+                       "GiBps_c_plus_d": round(N / GiB / tdupm, 3),
+                       "pcie_GBps_both_directions": round(2 * (N + C) / tdupm / 1e9, 2)}}
 
 
 def c1(steps, nchunks=67, clevel=5):
