@@ -111,6 +111,8 @@ def bind_schunk(lib):
         "blosc2_schunk_get_chunk": ([sp, i64, C.POINTER(vp), C.POINTER(C.c_bool)], C.c_int),
         "blosc2_schunk_get_lazychunk": ([sp, i64, C.POINTER(vp), C.POINTER(C.c_bool)], C.c_int),
         "blosc2_schunk_get_slice_buffer": ([sp, i64, i64, vp], C.c_int),
+        "blosc2_schunk_set_slice_buffer": ([sp, i64, i64, vp], C.c_int),
+        "b2h_schunk_set_slice_device": ([sp, i64, i64, vp], C.c_int),
         "blosc2_schunk_get_cparams": ([sp, C.POINTER(vp)], C.c_int),
         "blosc2_schunk_get_dparams": ([sp, C.POINTER(vp)], C.c_int),
         "blosc2_getitem_bytes_ctx": ([vp, vp, i32, i32, i32, vp, i32], C.c_int),
@@ -350,6 +352,10 @@ class SChunk:
         out = np.zeros(max((stop - start) * ts, 1), np.uint8)
         rc = self.L.blosc2_schunk_get_slice_buffer(self.p, start, stop, _p(out))
         return (rc, out[:max((stop - start) * ts, 0)])
+
+    def set_slice(self, start, stop, a: np.ndarray):
+        raw = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+        return self.L.blosc2_schunk_set_slice_buffer(self.p, start, stop, _p(raw))
 
     def free(self):
         if self.p:

@@ -588,3 +588,145 @@ int b2h_schunk_get_slice_device(blosc2_schunk* schunk, int64_t start, int64_t st
   }
   return 0;
 }
+
+// ------------------------------------------------------------------------ slice writes ----
+namespace {
+// The chunk walk of blosc2_schunk_set_slice_buffer (schunk.c:2146-2216): chunk k takes the range's
+// bytes [lo, hi) of it; `whole` chunks are compressed straight from the caller's bytes with `n`
+// = the byte count the reference compresses, the others are decompressed, patched and recompressed.
+// Quirk kept: a range that starts a chunk and ends nbytes % chunksize bytes into it counts as a
+// whole chunk of that many bytes, even in the middle of the super-chunk, where the chunk then
+// shrinks (the reference's `chunksize` local, 2165-2172).
+struct SliceStep {
+  int64_t k;
+  int32_t lo, hi, n;
+  bool whole;
+};
+std::vector<SliceStep> slice_walk(const blosc2_schunk* s, int64_t b0, int64_t b1) {
+  std::vector<SliceStep> v;
+  const int64_t cs = s->chunksize;
+  int64_t k = b0 / cs;
+  int32_t lo = (int32_t)(b0 % cs), hi = b1 >= (k + 1) * cs ? (int32_t)cs : (int32_t)(b1 % cs);
+  int32_t csz = (int32_t)cs;
+  for (int64_t done = 0; done < b1 - b0;) {
+    const int32_t tail = (int32_t)(s->nbytes % cs);
+    SliceStep st{k, lo, hi, 0, lo == 0 && (hi == cs || hi == tail)};
+    if (st.whole && hi == tail) csz = hi;
+    st.n = st.whole ? csz : 0;
+    v.push_back(st);
+    done += hi - lo;
+    k++;
+    lo = 0;
+    hi = b1 >= (k + 1) * cs ? (int32_t)cs : (int32_t)(b1 % cs);
+  }
+  return v;
+}
+
+int check_slice(const blosc2_schunk* s, int64_t start, int64_t stop) {
+  const int64_t ts = s->typesize;
+  if (start < 0 || stop < start || ts <= 0 || stop * ts > s->nbytes || s->chunksize <= 0) {
+    TRACE_ERROR("slice [%lld, %lld) is outside the super-chunk (or the super-chunk has no fixed chunksize)",
+                (long long)start, (long long)stop);
+    return BLOSC2_ERROR_INVALID_PARAM;
+  }
+  return 0;
+}
+
+// One chunk of the walk from host bytes `src` (the range's bytes for this chunk).
+int set_one(blosc2_schunk* s, const SliceStep& st, const uint8_t* src, std::vector<uint8_t>& data) {
+  uint8_t* chunk;
+  if (st.whole) {
+    chunk = static_cast<uint8_t*>(malloc((size_t)st.n + BLOSC2_MAX_OVERHEAD));
+    if (!chunk) return BLOSC2_ERROR_MEMORY_ALLOC;
+    if (blosc2_compress_ctx(s->cctx, src, st.n, chunk, st.n + BLOSC2_MAX_OVERHEAD) < 0) {
+      TRACE_ERROR("Cannot compress data of chunk ('%lld').", (long long)st.k);
+      free(chunk);
+      return BLOSC2_ERROR_FAILURE;
+    }
+  } else {
+    data.resize((size_t)s->chunksize);
+    const int got = blosc2_schunk_decompress_chunk(s, st.k, data.data(), s->chunksize);
+    if (got < 0) {
+      TRACE_ERROR("Cannot decompress chunk ('%lld').", (long long)st.k);
+      return BLOSC2_ERROR_FAILURE;
+    }
+    memcpy(data.data() + st.lo, src, (size_t)(st.hi - st.lo));
+    chunk = static_cast<uint8_t*>(malloc((size_t)got + BLOSC2_MAX_OVERHEAD));
+    if (!chunk) return BLOSC2_ERROR_MEMORY_ALLOC;
+    if (blosc2_compress_ctx(s->cctx, data.data(), got, chunk, got + BLOSC2_MAX_OVERHEAD) < 0) {
+      TRACE_ERROR("Cannot compress data of chunk ('%lld').", (long long)st.k);
+      free(chunk);
+      return BLOSC2_ERROR_FAILURE;
+    }
+  }
+  if (blosc2_schunk_update_chunk(s, st.k, chunk, false) != s->nchunks) {
+    TRACE_ERROR("Cannot update chunk ('%lld').", (long long)st.k);
+    free(chunk);
+    return BLOSC2_ERROR_CHUNK_UPDATE;
+  }
+  return 0;
+}
+}  // namespace
+
+int blosc2_schunk_set_slice_buffer(blosc2_schunk* schunk, int64_t start, int64_t stop, void* buffer) {
+  if (!schunk || !buffer) return BLOSC2_ERROR_NULL_POINTER;
+  int rc = check_slice(schunk, start, stop);
+  if (rc < 0) return rc;
+  const uint8_t* src = static_cast<const uint8_t*>(buffer);
+  std::vector<uint8_t> data;
+  for (const SliceStep& st : slice_walk(schunk, start * schunk->typesize, stop * schunk->typesize)) {
+    if ((rc = set_one(schunk, st, src, data)) < 0) return rc;
+    src += st.hi - st.lo;
+  }
+  return BLOSC2_ERROR_SUCCESS;
+}
+
+// The same walk from device bytes: each run of whole chunks is compressed by one device batch on the
+// super-chunk's cctx (ctx_append_device, the sticky blocksize carried as the serial calls carry it),
+// then updated in order; the (at most two) edge chunks go through the host walk above.
+int b2h_schunk_set_slice_device(blosc2_schunk* schunk, int64_t start, int64_t stop, const void* d_src) {
+  if (!schunk || !d_src) return BLOSC2_ERROR_NULL_POINTER;
+  int rc = check_slice(schunk, start, stop);
+  if (rc < 0) return rc;
+  const uint8_t* src = static_cast<const uint8_t*>(d_src);
+  const std::vector<SliceStep> walk = slice_walk(schunk, start * schunk->typesize, stop * schunk->typesize);
+  std::vector<uint8_t> data, piece;
+  int64_t off = 0;
+  for (size_t i = 0; i < walk.size();) {
+    if (!walk[i].whole) {
+      const SliceStep& st = walk[i];
+      piece.resize((size_t)(st.hi - st.lo));
+      if (hipMemcpy(piece.data(), src + off, piece.size(), hipMemcpyDeviceToHost) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+      if ((rc = set_one(schunk, st, piece.data(), data)) < 0) return rc;
+      off += st.hi - st.lo;
+      i++;
+      continue;
+    }
+    size_t j = i;
+    std::vector<int32_t> sizes;
+    for (; j < walk.size() && walk[j].whole; j++) sizes.push_back(walk[j].n);
+    // the whole chunks of a run sit back to back in the range, chunksize apart
+    std::vector<uint8_t*> chunks(sizes.size(), nullptr);
+    rc = b2h::ctx_append_device(schunk->cctx, src + off, sizes.data(), (int32_t)sizes.size(), schunk->chunksize,
+                                chunks.data());
+    if (rc == BLOSC2_ERROR_FILTER_PIPELINE) {   // user filters / codecs: the host walk
+      for (; i < j; i++) {
+        piece.resize((size_t)walk[i].n);
+        if (hipMemcpy(piece.data(), src + off, piece.size(), hipMemcpyDeviceToHost) != hipSuccess)
+          return BLOSC2_ERROR_FAILURE;
+        if ((rc = set_one(schunk, walk[i], piece.data(), data)) < 0) return rc;
+        off += walk[i].hi - walk[i].lo;
+      }
+      continue;
+    }
+    if (rc < 0) return rc;
+    for (size_t q = 0; i < j; i++, q++) {
+      if (blosc2_schunk_update_chunk(schunk, walk[i].k, chunks[q], false) != schunk->nchunks) {
+        for (size_t r = q; r < chunks.size(); r++) free(chunks[r]);
+        return BLOSC2_ERROR_CHUNK_UPDATE;
+      }
+      off += walk[i].hi - walk[i].lo;
+    }
+  }
+  return BLOSC2_ERROR_SUCCESS;
+}

@@ -131,12 +131,16 @@ BLOSC_EXPORT int b2h_frame_get_sparse_buffer(b2h_frame *frame, int64_t ncoords, 
  * decompress: chunks [nchunk, nchunk + n) into d_dst + i*dst_stride (device, capacity dst_capacity);
  *   status[i] (HOST, optional) = blosc2_schunk_decompress_chunk's return for chunk nchunk + i.
  *   Returns 0 or the first chunk error; BLOSC2_ERROR_INVALID_PARAM for a range outside the schunk.
- * get_slice: items [start, stop) into device memory d_dst (blosc2_schunk_get_slice_buffer). */
+ * get_slice: items [start, stop) into device memory d_dst (blosc2_schunk_get_slice_buffer).
+ * set_slice: items [start, stop) from device memory d_src (blosc2_schunk_set_slice_buffer): the chunks
+ *   wholly inside the range are compressed in one device batch, the edge chunks one by one, all in
+ *   the serial calls' order (the cctx's sticky blocksize moves as theirs does). */
 BLOSC_EXPORT int64_t b2h_schunk_append_device(blosc2_schunk *schunk, const void *d_src, const int32_t *nbytes,
                                               int32_t n, int64_t src_stride);
 BLOSC_EXPORT int b2h_schunk_decompress_device(blosc2_schunk *schunk, int64_t nchunk, int32_t n, void *d_dst,
                                               int64_t dst_stride, int32_t dst_capacity, int32_t *status);
 BLOSC_EXPORT int b2h_schunk_get_slice_device(blosc2_schunk *schunk, int64_t start, int64_t stop, void *d_dst);
+BLOSC_EXPORT int b2h_schunk_set_slice_device(blosc2_schunk *schunk, int64_t start, int64_t stop, const void *d_src);
 
 /* Per-context BloscLZ encoder mode.  Built-in BloscLZ does not read blosc2_cparams.codec_params
  * (reference include/blosc2.h:1207; only user codecs receive it), so a context selects its encoder

@@ -535,6 +535,9 @@ BLOSC_EXPORT int blosc2_schunk_get_lazychunk(blosc2_schunk *schunk, int64_t nchu
                                              bool *needs_free);
 /* include/blosc2.h:2275 (blosc/schunk.c:1662-1783) */
 BLOSC_EXPORT int blosc2_schunk_get_slice_buffer(blosc2_schunk *schunk, int64_t start, int64_t stop, void *buffer);
+/* include/blosc2.h:2304 (blosc/schunk.c:2146-2216): items [start, stop) of the super-chunk replaced by
+ * `buffer`, every touched chunk recompressed through the super-chunk's cctx and updated in place. */
+BLOSC_EXPORT int blosc2_schunk_set_slice_buffer(blosc2_schunk *schunk, int64_t start, int64_t stop, void *buffer);
 /* include/blosc2.h:2316, 2328 (blosc/schunk.c:70-105) */
 BLOSC_EXPORT int blosc2_schunk_get_cparams(blosc2_schunk *schunk, blosc2_cparams **cparams);
 BLOSC_EXPORT int blosc2_schunk_get_dparams(blosc2_schunk *schunk, blosc2_dparams **dparams);

@@ -22,7 +22,7 @@ dst = torch.empty(nch * stride, dtype=torch.uint8, device="cuda")
 cb = torch.zeros(nch, dtype=torch.int32, device="cuda")
 out = torch.empty(nch * chunk, dtype=torch.uint8, device="cuda")
 status = torch.zeros(nch, dtype=torch.int32, device="cuda")
-cp = B.cparams(clevel=5, typesize=4)
+cp = B.cparams(clevel=5, typesize=4, lz_mode=int(sys.argv[2]) if len(sys.argv) > 2 else None)
 L = B.lib()
 L.b2h_enable_timing(1)
 B.compress_batch(cp, src.data_ptr(), chunk, nch, chunk, dst.data_ptr(), stride, chunk + 32, cb.data_ptr())
@@ -31,6 +31,8 @@ for _ in range(2):
 torch.cuda.synchronize()
 assert torch.equal(out, src)
 print("times", B.last_times())
+if not os.environ.get("B2H_DECODE_DEBUG"):
+    sys.exit(0)
 ns = nch * 16 * 4
 rec = np.zeros((ns, 2), np.int64)
 L.b2h_debug_decode_cycles.argtypes = [C.c_void_p, C.c_int32]

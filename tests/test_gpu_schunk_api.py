@@ -7,7 +7,8 @@ appends (blosc2_schunk_append_buffer, schunk.c:1459-1477) and after ONE batched 
 same buffers (b2h_schunk_append_device) -- including the context's sticky blocksize, checked by one
 more serial append afterwards; decompress_chunk / the batched device decompression restore the
 input with the reference's return codes; get_slice_buffer / the device slice equal the reference's
-slices on ranges that start and end inside chunks, at chunk edges, in the short last chunk.
+slices on ranges that start and end inside chunks, at chunk edges, in the short last chunk; and
+set_slice_buffer (host and device forms) leaves the same chunks and counters as the reference.
 """
 import ctypes as C
 import os
@@ -65,8 +66,8 @@ def _chunks(sc):
     return [sc.chunk(i) for i in range(sc.s.nchunks)]
 
 
-def _assert_same(a, b):
-    assert a.counters() == b.counters()
+def _assert_same(a, b, what=None):
+    assert a.counters() == b.counters(), (what, a.counters(), b.counters())
     for i, (u, v) in enumerate(zip(_chunks(a), _chunks(b))):
         assert np.array_equal(u, v), i
 
@@ -205,3 +206,45 @@ def test_decompress_device_mixed_chunks_match_reference():
     finally:
         a.free()
         b.free()
+
+
+SET_SLICES = [(24, 136), (0, CHUNK), (CHUNK - 40, 3 * CHUNK + 72), (CHUNK, 4 * CHUNK),
+              (4 * CHUNK + 8, 5 * CHUNK + 100 * 1024 + 24), (5 * CHUNK, 5 * CHUNK + 100 * 1024 + 24)]   # bytes
+
+
+@pytest.mark.parametrize("pipe", ["delta_shuffle8", "shuffle4"])
+def test_set_slice_matches_reference(pipe):
+    """blosc2_schunk_set_slice_buffer (schunk.c:2146-2216) and its device form: the same chunks and
+    counters as the reference after each write, edge chunks patched, whole chunks recompressed
+    (the device form in one batch), the cctx's sticky blocksize moving as the serial calls move it."""
+    import torch
+    kw = PIPES[pipe]
+    ts = kw["typesize"]
+    data, sizes = _data(ts, 5, 100 * 1024 + 24)
+    a, b = _pair(kw)
+    c = B.SChunk(B.cparams(**kw), B.dparams())
+    try:
+        off = 0
+        for n in sizes:
+            for sc in (a, b, c):
+                sc.append_buffer(data[off:off + n])
+            off += n
+        cur = data.copy()
+        for j, (blo, bhi) in enumerate(SET_SLICES):
+            lo, hi = blo // ts, bhi // ts
+            new = np.random.default_rng(j).integers(0, 7, (hi - lo) * ts, dtype=np.uint8)   # compressible
+            assert a.set_slice(lo, hi, new) == b.set_slice(lo, hi, new) == 0, (lo, hi)
+            d = torch.from_numpy(new).cuda()
+            assert c.L.b2h_schunk_set_slice_device(c.p, lo, hi, C.c_void_p(d.data_ptr())) == 0, (lo, hi)
+            cur[lo * ts:hi * ts] = new
+            # counters first: fetching the chunks moves current_nchunk (blosc2_schunk_get_chunk)
+            assert a.counters() == b.counters() == c.counters(), (lo, hi)
+            for i, (x, y, z) in enumerate(zip(_chunks(a), _chunks(b), _chunks(c))):
+                assert np.array_equal(x, y) and np.array_equal(z, y), (lo, hi, i)
+            rc, got = a.get_slice(0, len(cur) // ts, ts)
+            assert rc == 0 and np.array_equal(got, cur), (lo, hi)
+        buf = np.zeros(64, np.uint8)
+        assert a.L.blosc2_schunk_set_slice_buffer(a.p, 10, 5, B._p(buf)) == -12
+    finally:
+        for sc in (a, b, c):
+            sc.free()
