@@ -5,13 +5,14 @@
 // which earlier position a hash bucket offers as a position's candidate.  The reference inserts
 // only the positions its serial walk visits, so every candidate depends on the whole parse before
 // it and the walk is a latency chain (exact mode, b2h_lz.h, ~9 000 cycles per 64 positions on T's
-// smooth plane).  Fast mode inserts positions in TILES of 64, in tile order, independently of the
+// smooth plane).  Fast mode inserts positions in TILES of 128, in tile order, independently of the
 // parse (semantics and their CPU model: tools/fm_model.c): entering tile T, the parse inserts T
 // (if a jump skipped it) and T + 1; tiles a long match jumps over are never inserted.
 //
-//   * one LDS atomic exchange per lane swaps the lane's position into its bucket and returns the
-//     bucket's previous position -- the most recent earlier position with that hash, earlier lanes
-//     of the same tile included (LDS applies the lanes of one instruction in lane order);
+//   * one LDS atomic exchange per lane and half swaps the position into its bucket and returns the
+//     bucket's previous position -- the most recent earlier position with that hash, earlier
+//     positions of the same tile included (LDS applies the lanes of one instruction in lane order,
+//     and the wave's two exchanges in program order);
 //   * so a tile's candidates, their 60-byte compares and match lengths are known before the parse
 //     reaches it.  Two waves of a workgroup share one stream's table: the MATCHER exchanges and
 //     compares tile T + 1 while the PARSER parses tile T with the exact-mode window code (ballot
@@ -25,10 +26,14 @@
 
 namespace b2h {
 
-constexpr int kFastTile = 64;
+// Positions per parse step: two 64-lane HALVES.  The parser's per-step cost is mostly a fixed
+// latency chain (LDS hand-over reads, two DPP scans, ballots, the ring writes, the barrier:
+// measured 1 600 of 3 100 cycles per 64-position step on T's smooth plane, the chain walk the
+// rest), so both halves go through the same instructions and their chains overlap.
+constexpr int kFastTile = 128, kHalf = 64;
 
-// Table exchange of one tile: the lanes with p < loop_end hash in[p..p+3] (v) and swap p into the
-// bucket.  Returns the candidate (the bucket's previous position; 0 for an empty bucket).
+// Table exchange of 64 positions: the lanes with p < loop_end hash in[p..p+3] (v) and swap p into
+// the bucket.  Returns the candidate (the bucket's previous position; 0 for an empty bucket).
 // POS = uint32_t: one ds_wrxchg_rtn_b32.  POS = uint16_t (streams <= 64 KiB, half the LDS, twice
 // the waves per CU): two buckets per dword, exchanged with ds_mskor_rtn_b32 -- the masked-or
 // atomic replaces just the bucket's half ((old & ~mask) | p << sh) and returns the old dword.
@@ -68,26 +73,27 @@ struct RawCmp {
   uint32_t d[kCmpWords + 1];
   uint32_t sh;
 };
-__device__ __forceinline__ void rawc_load(gin_t p, RawCmp& r) {
-  const B2H_GLB uint32_t* q = align4(p);
-  r.sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
-#pragma unroll
-  for (int i = 0; i < kCmpWords + 1; i++) r.d[i] = q[i];
-}
 __device__ __forceinline__ uint32_t rawc_word(const RawCmp& r, int i) { return funnel(r.d[i], r.d[i + 1], r.sh); }
+
+// Hand-over record of one position, matcher -> parser: input byte | (first mismatch + 1) << 8 |
+// candidate distance << 14.  mismatch + 1 == 0: no usable candidate (then the distance is 0); a
+// usable distance is < MAX_FARDISTANCE < 2^17, the mismatch + 1 <= 61 < 2^6.
+__device__ __forceinline__ uint32_t rec_pack(uint32_t byte, int32_t mm1, uint32_t dist) {
+  return (byte & 0xffu) | ((uint32_t)mm1 << 8) | (dist << 14);
+}
+__device__ __forceinline__ int32_t rec_mm(uint32_t w) { return (int32_t)((w >> 8) & 63u) - 1; }
+__device__ __forceinline__ uint32_t rec_dist(uint32_t w) { return w >> 14; }
 
 // ============================================================ matcher / parser workgroup ====
 // One stream per workgroup of two waves (k_encode_fast):
-//   wave 0, the MATCHER: tile exchanges, candidate loads and 60-byte compares -- for each lane of a
-//     tile its candidate distance, first mismatch and input byte, handed over through LDS;
+//   wave 0, the MATCHER: tile exchanges, candidate loads and 60-byte compares -- for each position
+//     of a tile its hand-over record, through LDS;
 //   wave 1, the PARSER: chain walk, token emission, output ring and flushes.
 // Lockstep, one barrier per tile.  A match jumping past tile T + 1 costs one step in which the
 // matcher produces the jump target and the parser waits.  The split keeps each wave within 128
-// VGPRs, so a CU holds 8 streams x 2 waves (measured: the encoder is issue-bound at that
-// occupancy, so a deeper matcher pipeline -- exchange T + 2 while comparing T + 1 -- ran slower).
+// VGPRs, so a CU holds 8 streams x 2 waves.
 struct FastShared {          // per workgroup, after the table and the output ring
-  uint32_t dist[2][64];      // hand-over slots: candidate distance
-  uint32_t aux[2][64];       //   (first mismatch + 1) | input byte << 8 (mismatch + 1 == 0: no candidate)
+  uint32_t rec[2][kFastTile];   // hand-over records, by step parity
   int32_t ctrl[2];           // parser -> matcher: next tile, or -1 (stop); by iteration parity
   int32_t decide[2];         // the stream's probe decision / run verdict (parser -> both)
   int32_t pull;              // the stream index the workgroup pulled
@@ -124,7 +130,7 @@ __device__ __forceinline__ void fast_clear_half(B2H_LDS uint8_t* tab, int tablog
 // the larger of the two, not their sum (one shared loop with a role branch inside kept both roles'
 // state live everywhere and spilled ~170 SGPRs into VGPR lanes).
 //
-// MATCHER: tile exchanges, candidate loads and 60-byte compares -> the hand-over slots.
+// MATCHER: tile exchanges, candidate loads and 60-byte compares -> the hand-over records.
 template <bool PROBE, typename POS>
 __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int32_t length, int probe_hashlog, int tablog,
                                                                B2H_LDS uint8_t* tab, B2H_LDS FastShared* sh) {
@@ -133,60 +139,91 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
   fast_limits<PROBE>(length, probe_hashlog, &limit, &bound, &loop_end);
   (void)bound;
   fast_clear_half<POS>(tab, tablog, true);
-  // ---- matcher: the first input words of tile `ant` (prefetched one step ahead); the other 14
-  // are loaded only when some lane's candidate matches its first 4 bytes, together with the
-  // candidates' words (the same round trip): incompressible tiles issue 4 loads per lane, not 18 ----
-  RawCmp na;
+  // ---- the first two input words of each half of tile `ant` (prefetched one step ahead); the
+  // other 14 are loaded only when some lane's candidate matches its first 4 bytes, together with
+  // the candidates' words (the same round trip): incompressible halves issue 4 loads per lane ----
+  uint32_t na[2][2], nsh[2];
   int32_t ant = -1;
-  auto load_a = [&](int32_t t, RawCmp& a) {
-    const int32_t p = t * kFastTile + lane;
-    gin_t q8 = in + (p < loop_end ? p : 0);
-    const B2H_GLB uint32_t* q = align4(q8);
-    a.sh = (uint32_t)(reinterpret_cast<uintptr_t>(q8) & 3);
-    a.d[0] = q[0];
-    a.d[1] = q[1];
-  };
-  // insert tile t, test every lane's candidate, hand the results over in slot `slot`
-  auto produce = [&](int32_t t, int slot) {
-    RawCmp a;
-    if (t == ant) a = na;
-    else load_a(t, a);
-    const int32_t p = t * kFastTile + lane;
-    const bool valid = p < loop_end;
-    const uint32_t cand = fast_exchange<POS>(rawc_word(a, 0), p, valid, tablog, tab);
-    const bool cok = fast_cand_ok(p, cand, valid);
-    // the candidate's first word decides most tiles: when no lane's 4 bytes match, every first
-    // mismatch lies in word 0 and the other 14 words are neither loaded nor compared
-    gin_t cq = in + (cok ? (int32_t)cand : (valid ? p : 0));
-    const B2H_GLB uint32_t* cw = align4(cq);
-    const uint32_t csh = (uint32_t)(reinterpret_cast<uintptr_t>(cq) & 3);
-    const uint32_t c0 = cw[0], c1 = cw[1];
-    load_a(t + 1, na);   // issued after the candidate loads: the compare waits for those only
-    ant = t + 1;
-    const uint32_t x0 = rawc_word(a, 0) ^ funnel(c0, c1, csh);
-    int32_t mm;
-    if (__ballot(cok && x0 == 0) == 0) {
-      mm = x0 ? (int32_t)(__builtin_ctz(x0) >> 3) : 4;
-    } else {
-      uint32_t c[kCmpWords + 1];
-      c[0] = c0;
-      c[1] = c1;
-      const B2H_GLB uint32_t* aw = align4(in + (p < loop_end ? p : 0));
+  auto load_a = [&](int32_t t, uint32_t (&w)[2][2], uint32_t (&s)[2]) {
 #pragma unroll
-      for (int i = 2; i < kCmpWords + 1; i++) {
-        c[i] = cw[i];
-        a.d[i] = aw[i];
-      }
-      mm = kCmpBytes;
-#pragma unroll
-      for (int i = kCmpWords - 1; i >= 1; i--) {
-        const uint32_t x = rawc_word(a, i) ^ funnel(c[i], c[i + 1], csh);
-        if (x) mm = 4 * i + (__builtin_ctz(x) >> 3);
-      }
-      if (x0) mm = (int32_t)(__builtin_ctz(x0) >> 3);
+    for (int h = 0; h < 2; h++) {
+      const int32_t p = t * kFastTile + h * kHalf + lane;
+      gin_t q8 = in + (p < loop_end ? p : 0);
+      const B2H_GLB uint32_t* q = align4(q8);
+      s[h] = (uint32_t)(reinterpret_cast<uintptr_t>(q8) & 3);
+      w[h][0] = q[0];
+      w[h][1] = q[1];
     }
-    sh->dist[slot][lane] = (uint32_t)(p - (int32_t)cand);
-    sh->aux[slot][lane] = (uint32_t)(cok ? mm + 1 : 0) | ((rawc_word(a, 0) & 0xffu) << 8);
+  };
+  // insert tile t (half 0, then half 1: position order), test every position's candidate, hand
+  // the records over in slot `slot`
+  auto produce = [&](int32_t t, int slot) {
+    uint32_t a0[2][2], ash[2];
+    if (t == ant) {
+#pragma unroll
+      for (int h = 0; h < 2; h++) { a0[h][0] = na[h][0]; a0[h][1] = na[h][1]; ash[h] = nsh[h]; }
+    } else {
+      load_a(t, a0, ash);
+    }
+    int32_t p[2];
+    uint32_t v[2], cand[2];
+    bool valid[2], cok[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      p[h] = t * kFastTile + h * kHalf + lane;
+      valid[h] = p[h] < loop_end;
+      v[h] = funnel(a0[h][0], a0[h][1], ash[h]);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {   // in order: half 1's positions follow half 0's
+      cand[h] = fast_exchange<POS>(v[h], p[h], valid[h], tablog, tab);
+      cok[h] = fast_cand_ok(p[h], cand[h], valid[h]);
+    }
+    // the candidate's first word decides most halves: when no lane's 4 bytes match, every first
+    // mismatch lies in word 0 and the other 14 words are neither loaded nor compared
+    const B2H_GLB uint32_t* cw[2];
+    uint32_t csh[2], c0[2], c1[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      gin_t cq = in + (cok[h] ? (int32_t)cand[h] : (valid[h] ? p[h] : 0));
+      cw[h] = align4(cq);
+      csh[h] = (uint32_t)(reinterpret_cast<uintptr_t>(cq) & 3);
+      c0[h] = cw[h][0];
+      c1[h] = cw[h][1];
+    }
+    load_a(t + 1, na, nsh);   // issued after the candidate loads: the compare waits for those only
+    ant = t + 1;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint32_t x0 = v[h] ^ funnel(c0[h], c1[h], csh[h]);
+      int32_t mm;
+      if (__ballot(cok[h] && x0 == 0) == 0) {
+        mm = x0 ? (int32_t)(__builtin_ctz(x0) >> 3) : 4;
+      } else {
+        RawCmp a;
+        uint32_t c[kCmpWords + 1];
+        a.d[0] = a0[h][0];
+        a.d[1] = a0[h][1];
+        a.sh = ash[h];
+        c[0] = c0[h];
+        c[1] = c1[h];
+        const B2H_GLB uint32_t* aw = align4(in + (valid[h] ? p[h] : 0));
+#pragma unroll
+        for (int i = 2; i < kCmpWords + 1; i++) {
+          c[i] = cw[h][i];
+          a.d[i] = aw[i];
+        }
+        mm = kCmpBytes;
+#pragma unroll
+        for (int i = kCmpWords - 1; i >= 1; i--) {
+          const uint32_t x = rawc_word(a, i) ^ funnel(c[i], c[i + 1], csh[h]);
+          if (x) mm = 4 * i + (__builtin_ctz(x) >> 3);
+        }
+        if (x0) mm = (int32_t)(__builtin_ctz(x0) >> 3);
+      }
+      sh->rec[slot][h * kHalf + lane] =
+          rec_pack(v[h], cok[h] ? mm + 1 : 0, cok[h] ? (uint32_t)(p[h] - (int32_t)cand[h]) : 0u);
+    }
   };
 
   const int32_t pos = PROBE ? 0 : 4;
@@ -218,7 +255,109 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
   }
 }
 
-// PARSER: chain walk, token emission, output ring and flushes, the tail.
+// value of per-half variable x[2] at tile position q (0..127), as a wave-uniform value
+__device__ __forceinline__ int32_t rdq(const int32_t (&x)[2], int32_t q) {
+  return q < kHalf ? rdlane(x[0], q) : rdlane(x[1], q - kHalf);
+}
+
+// Exact length of the match taken at tile position m whose 60-byte compare did not find its end
+// (lenx == -1): lanes at +56, +112 with the same distance carry the next 60 bytes' compares, then
+// 64 lanes x 16 bytes per step from memory.
+__device__ __forceinline__ int32_t fast_match_len(int32_t m, const int32_t (&lenx)[2], const int32_t (&dist)[2],
+                                                  const int32_t (&mmd)[2], int32_t P, int32_t bound, gin_t in) {
+  const int32_t known = rdq(lenx, m);
+  if (known >= 0) return known;
+  const int32_t pm = P + m;
+  const int32_t dm = rdq(dist, m);
+  int32_t L = kCmpBytes, e = -1;
+  for (int32_t j = m + kNbrStride; j < kFastTile; j += kNbrStride) {
+    if (pm + L >= bound) { e = bound; break; }
+    const int32_t mj = rdq(mmd, j);
+    if (mj < 0 || rdq(dist, j) != dm) break;
+    if (mj < kCmpBytes) { e = min(P + j + mj + 1, bound); break; }
+    L = j - m + kCmpBytes;
+  }
+  if (e < 0) e = pm + L >= bound ? bound : wave_match_end(in, pm + L, (uint32_t)dm, bound);
+  return e - 4 - pm;
+}
+
+// One counting step of the probe (get_cratio, blosc/blosclz.c:320-419) over a tile with accepted
+// matches: the chain walk, then every element's output size through two 128-position DPP scans.
+// Returns the next parse position relative to the tile.
+__device__ __forceinline__ int32_t probe_step(const uint64_t (&am)[2], int32_t (&lenx)[2], const int32_t (&dist)[2],
+                                              const int32_t (&mmd)[2], int32_t P, int32_t s0, int32_t lim,
+                                              int32_t bound, gin_t in, int32_t& lit, int32_t& o) {
+  const int lane = lane_id();
+  uint64_t chain[2] = {0, 0};
+  int32_t ser = -1, endc2 = -1;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    if (ser >= 0 || endc2 >= (h + 1) * kHalf) continue;
+    uint64_t rem = endc2 > h * kHalf ? am[h] & (~0ull << (endc2 - h * kHalf)) : am[h];
+    while (rem) {
+      const int32_t m = h * kHalf + __builtin_ctzll(rem);
+      int32_t lm = rdlane(lenx[h], m - h * kHalf);
+      if (lm < 0) {
+        lm = fast_match_len(m, lenx, dist, mmd, P, bound, in);
+        lenx[h] = lane == m - h * kHalf ? lm : lenx[h];
+      }
+      if (lm >= 262) { ser = m; break; }
+      chain[h] |= 1ull << (m - h * kHalf);
+      const int32_t c2 = m + lm + 2;
+      endc2 = c2;
+      if (c2 >= (h + 1) * kHalf) break;
+      rem = am[h] & (~0ull << (c2 - h * kHalf));
+    }
+  }
+  bool ischain[2], islit[2];
+  int32_t c2incl[2], lpos[2], contrib[2], incl[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    ischain[h] = (chain[h] >> lane) & 1ull;
+    c2incl[h] = wave_scan_max(ischain[h] ? h * kHalf + lane + lenx[h] + 2 : -1);
+  }
+  const int32_t carry_c2 = rdlane(c2incl[0], 63);
+  c2incl[1] = max(c2incl[1], carry_c2);
+  const int32_t lit_end = ser >= 0 ? ser : lim;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int32_t q = h * kHalf + lane;
+    int32_t pc2 = __builtin_amdgcn_update_dpp(-1, c2incl[h], 0x138, 0xf, 0xf, false);   // wave_shr:1
+    if (h == 1 && lane == 0) pc2 = carry_c2;
+    const bool hasprev = pc2 >= 0;
+    const int32_t segstart = hasprev ? pc2 : s0;
+    lpos[h] = (hasprev ? 0 : lit) + q - segstart;
+    islit[h] = !ischain[h] && q >= segstart && q < lit_end;
+    const int32_t rr5 = lpos[h] & 31;
+    const bool near = (uint32_t)dist[h] - 1 < kLzNear;
+    const int32_t tok = (uint32_t)lenx[h] < 7 ? (near ? 2 : 4) : (near ? 3 : 5);
+    contrib[h] = 0;
+    if (islit[h]) contrib[h] = 1 + (rr5 == 31 ? 1 : 0);
+    if (ischain[h]) contrib[h] = tok + 1 - (rr5 == 0 ? 1 : 0);
+    incl[h] = wave_scan_add(contrib[h]);
+  }
+  const uint64_t litm0 = __ballot(islit[0]), litm1 = __ballot(islit[1]);
+  const uint64_t elems0 = litm0 | chain[0], elems1 = litm1 | chain[1];
+  if (elems0 | elems1) {
+    const int32_t le = elems1 ? kHalf + 63 - __builtin_clzll(elems1) : 63 - __builtin_clzll(elems0);
+    const bool lelit = le < kHalf ? ((litm0 >> le) & 1ull) : ((litm1 >> (le - kHalf)) & 1ull);
+    lit = lelit ? ((rdq(lpos, le) + 1) & 31) : 0;
+  }
+  o += rdlane(incl[0], 63) + rdlane(incl[1], 63);
+  int32_t next_rel = max(endc2, lim);
+  if (ser >= 0) {   // a match with length-extension bytes
+    const uint32_t sbd = (uint32_t)rdq(dist, ser) - 1;
+    const int32_t lm = rdq(lenx, ser);
+    if (!lit) o--;
+    lit = 0;
+    o += 1 + (int32_t)(((uint32_t)lm - 7) / 255) + (sbd < kLzNear ? 2 : 4) + 1;
+    next_rel = ser + lm + 2;
+  }
+  return next_rel;
+}
+
+// PARSER: chain walk, token emission, output ring and flushes, the tail.  Position q of the tile
+// (0..127) is lane q & 63 of half q >> 6; every per-position value is a pair [half].
 template <bool PROBE, typename POS, bool WT>
 __device__ __forceinline__ LzPassOut lz_pass_fast_parser(gin_t __restrict__ in, int32_t length, int probe_hashlog,
                                                                    int tablog, gout_t __restrict__ out, int32_t maxout,
@@ -263,128 +402,120 @@ __device__ __forceinline__ LzPassOut lz_pass_fast_parser(gin_t __restrict__ in, 
         EPROF_T(t0);
         if (!PROBE && o - F >= 1024) flush(F + 512);   // a tile emits < 512 bytes
         const int32_t P = T * kFastTile;
-        const int32_t p = P + lane;
         const int32_t s0 = pos - P;
         const int32_t lim = min(kFastTile, loop_end - P);
-        const uint32_t dist = sh->dist[cur][lane];
-        const uint32_t ax = sh->aux[cur][lane];
-        const int32_t mmd = (int32_t)(ax & 0xffu) - 1;   // -1: no usable candidate
-        const uint32_t vbyte = (ax >> 8) & 0xffu;
-        bool accept = false;
-        int32_t lenx = 0;
-        if (lane >= s0 && mmd >= 4) {
-          const int32_t e = min(mmd < kCmpBytes ? p + mmd + 1 : 0x7fffffff, bound);
-          const int32_t len = e - 4 - p;
-          accept = len >= 4 && (PROBE || !(len <= 5 && (dist - 1) >= kLzNear));
-          lenx = (mmd < kCmpBytes || p + kCmpBytes + 1 >= bound) ? len : -1;
+        int32_t mmd[2], dist[2], lenx[2];
+        uint32_t vbyte[2];
+        uint64_t am[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          const int32_t q = h * kHalf + lane, p = P + q;
+          const uint32_t w = sh->rec[cur][q];
+          mmd[h] = rec_mm(w);   // -1: no usable candidate
+          dist[h] = (int32_t)rec_dist(w);
+          vbyte[h] = w & 0xffu;
+          bool accept = false;
+          lenx[h] = 0;
+          if (q >= s0 && mmd[h] >= 4) {
+            const int32_t e = min(mmd[h] < kCmpBytes ? p + mmd[h] + 1 : 0x7fffffff, bound);
+            const int32_t len = e - 4 - p;
+            accept = len >= 4 && (PROBE || !(len <= 5 && (uint32_t)(dist[h] - 1) >= kLzNear));
+            lenx[h] = (mmd[h] < kCmpBytes || p + kCmpBytes + 1 >= bound) ? len : -1;
+          }
+          am[h] = __ballot(accept);
         }
-        const uint64_t am = __ballot(accept);
         EPROF_T(t2);
         EPROF_ADD(1, t0, t2);
-        if (PROBE && am == 0) {
-          const int32_t cnt = lim - s0;
-          o += cnt + (lit + cnt) / 32;
-          lit = (lit + cnt) & 31;
-          pos = P + lim;
+        if constexpr (PROBE) {
+          if ((am[0] | am[1]) == 0) {
+            const int32_t cnt = lim - s0;
+            o += cnt + (lit + cnt) / 32;
+            lit = (lit + cnt) & 31;
+            pos = P + lim;
+          } else {
+            pos = P + probe_step(am, lenx, dist, mmd, P, s0, lim, bound, in, lit, o);
+          }
         } else {
-          uint64_t chain = 0;
-          int32_t ser = -1, endc2 = -1;
-          {
-            uint64_t rem = am;
+          // ---- emitting pass: the chain walk emits each element as it takes it (literal runs by
+          // the lanes that hold them, a token by lanes 0..5), so a step costs instructions per
+          // ELEMENT, not per position: on T's smooth plane a 128-position step holds ~10 ----
+          int32_t c = s0, ser = -1, ser_len = 0, endc2 = -1, req = -1;
+          auto emit_lits = [&](int32_t a, int32_t e) {   // literals at tile positions [a, e), a < e
+            const int32_t n = e - a;
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+              if (a < (h + 1) * kHalf && e > h * kHalf) {
+                const int32_t q = h * kHalf + lane, k = q - a;
+                if (q >= a && q < e) {
+                  const int32_t off = o + k + ((lit + k) >> 5);
+                  oring[off & ORM] = (uint8_t)vbyte[h];
+                  if (((lit + k + 1) & 31) == 0) oring[(off + 1) & ORM] = (uint8_t)(kLzMaxCopy - 1);
+                }
+              }
+            }
+            req = o + (n - 1) + ((lit + n - 1) >> 5) + 2;
+            o += n + ((lit + n) >> 5);
+            lit = (lit + n) & 31;
+          };
+          // MATCH_SHORT / MATCH_LONG (+ _FAR) token + the marker opening the next literal run
+          // (blosc/blosclz.c:270-316); the run it ends gets its header (lane 8).
+          auto emit_token = [&](int32_t lm, uint32_t dm) {
+            int32_t at = -1;
+            const uint32_t hdr = (uint32_t)(lit - 1);
+            if (lit) {
+              at = o - lit - 1;
+              if (at == 0) byte0 = hdr;
+            } else {
+              o--;
+            }
+            lit = 0;
+            const uint32_t bd = dm - 1, ulen = (uint32_t)lm, fd = bd - kLzNear;
+            const bool near = bd < kLzNear, lng = ulen >= 7;
+            const uint32_t b0 = (lng ? (7u << 5) : (ulen << 5)) + (near ? (bd >> 8) : 31u);
+            const uint32_t dbytes = near ? (bd & 255u) : (255u | ((fd >> 8) << 8) | ((fd & 255u) << 16));
+            uint64_t rest = (uint64_t)dbytes | (31ull << (near ? 8 : 24));
+            if (lng) rest = (uint64_t)(ulen - 7) | (rest << 8);
+            const uint64_t bytes = (uint64_t)b0 | (rest << 8);
+            const int32_t tok = lng ? (near ? 3 : 5) : (near ? 2 : 4);
+            const bool wr = lane <= tok || (lane == 8 && at >= 0);
+            if (wr) oring[(lane <= tok ? o + lane : at) & ORM] = lane <= tok ? (uint8_t)(bytes >> (8 * lane)) : (uint8_t)hdr;
+            o += tok + 1;
+            req = o;
+          };
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            if (ser >= 0 || c >= (h + 1) * kHalf) continue;
+            uint64_t rem = c > h * kHalf ? am[h] & (~0ull << (c - h * kHalf)) : am[h];
             while (rem) {
-              const int32_t m = __builtin_ctzll(rem);
-              int32_t lm = rdlane(lenx, m);
+              const int32_t m = h * kHalf + __builtin_ctzll(rem);
+              int32_t lm = rdlane(lenx[h], m - h * kHalf);
               if (lm < 0) {
                 EPROF_T(te0);
-                const int32_t pm = P + m;
-                const uint32_t dm = (uint32_t)rdlane((int32_t)dist, m);
-                int32_t L = kCmpBytes, e = -1;
-                for (int32_t j = m + kNbrStride; j < kFastTile; j += kNbrStride) {
-                  if (pm + L >= bound) { e = bound; break; }
-                  const int32_t mj = rdlane(mmd, j);
-                  if (mj < 0 || (uint32_t)rdlane((int32_t)dist, j) != dm) break;
-                  if (mj < kCmpBytes) { e = min(P + j + mj + 1, bound); break; }
-                  L = j - m + kCmpBytes;
-                }
-                if (e < 0) e = pm + L >= bound ? bound : wave_match_end(in, pm + L, dm, bound);
-                lm = e - 4 - pm;
-                lenx = lane == m ? lm : lenx;
+                lm = fast_match_len(m, lenx, dist, mmd, P, bound, in);
                 EPROF_T(te1);
                 EPROF_ADD(5, te0, te1);
               }
-              if (lm >= 262) { ser = m; break; }
-              chain |= 1ull << m;
-              const int32_t c2 = m + lm + 2;
-              endc2 = c2;
-              if (c2 >= kFastTile) break;
-              rem = am & (~0ull << c2);
+              if (lm >= 262) { ser = m; ser_len = lm; break; }
+              if (m > c) emit_lits(c, m);
+              emit_token(lm, (uint32_t)rdlane(dist[h], m - h * kHalf));
+              c = m + lm + 2;
+              endc2 = c;
+              if (c >= (h + 1) * kHalf) break;
+              rem = am[h] & (~0ull << (c - h * kHalf));
             }
+          }
+          const int32_t lit_end = ser >= 0 ? ser : lim;
+          if (c < lit_end) emit_lits(c, lit_end);
+          if (req >= 0) {
+            peak = max(peak, req);
+            if (req > maxout) { fail = true; break; }
           }
           EPROF_T(t3);
           EPROF_ADD(2, t2, t3);
-          const bool ischain = (chain >> lane) & 1ull;
-          const int32_t c2v = lane + lenx + 2;
-          const int32_t c2incl = wave_scan_max(ischain ? c2v : -1);
-          const int32_t pc2 = __builtin_amdgcn_update_dpp(-1, c2incl, 0x138, 0xf, 0xf, false);
-          const bool hasprev = pc2 >= 0;
-          const int32_t segstart = hasprev ? pc2 : s0;
-          const int32_t lpos = (hasprev ? 0 : lit) + lane - segstart;
-          const int32_t lit_end = ser >= 0 ? ser : lim;
-          const bool islit = !ischain && lane >= segstart && lane < lit_end;
-          const int32_t rr5 = lpos & 31;
-          const uint32_t bd = dist - 1;
-          const bool near = bd < kLzNear;
-          const uint32_t ulen = (uint32_t)lenx;
-          const int32_t tok = ulen < 7 ? (near ? 2 : 4) : (near ? 3 : 5);
-          int32_t contrib = 0;
-          if (islit) contrib = 1 + (rr5 == 31 ? 1 : 0);
-          if (ischain) contrib = tok + 1 - (rr5 == 0 ? 1 : 0);
-          const int32_t incl = wave_scan_add(contrib);
-          const int32_t excl = incl - contrib;
-          const uint64_t litm = __ballot(islit);
-          const uint64_t elems = litm | chain;
-          if (elems) {
-            const int32_t le = 63 - __builtin_clzll(elems);
-            const bool lelit = (litm >> le) & 1ull;
-            if (!PROBE) {
-              const int32_t base = o + excl;
-              const int32_t ts = base - (rr5 == 0 ? 1 : 0);
-              const int32_t req = lelit ? rdlane(base, le) + 2 : rdlane(ts + tok + 1, le);
-              peak = max(peak, req);
-              if (req > maxout) { fail = true; break; }
-              // Every element writes a fixed 6-byte slot from its start in DESCENDING byte order: a
-              // position's owner always has the lowest byte index among the elements that touch it
-              // (the others start earlier), so the owner's byte lands last and the bytes past an
-              // element's end need no masks: the next element's first byte replaces a literal's
-              // pending run marker or a token's trailing marker exactly as the reference overwrites it.
-              // Token bytes (MATCH_SHORT/LONG/_FAR, blosc/blosclz.c:270-316) + the marker opening the
-              // next literal run, built without branches.
-              if (islit || ischain) {
-                const uint32_t fd = bd - kLzNear;
-                const bool lng = ulen >= 7;
-                const uint32_t b0 = (lng ? (7u << 5) : (ulen << 5)) + (near ? (bd >> 8) : 31u);
-                const uint32_t dbytes = near ? (bd & 255u) : (255u | ((fd >> 8) << 8) | ((fd & 255u) << 16));
-                uint64_t rest = (uint64_t)dbytes | (31ull << (near ? 8 : 24));
-                if (lng) rest = (uint64_t)(ulen - 7) | (rest << 8);
-                const uint64_t bytes = islit ? (uint64_t)(vbyte | ((uint32_t)(kLzMaxCopy - 1) << 8))
-                                             : ((uint64_t)b0 | (rest << 8));
-                const int32_t start = islit ? base : ts;
-#pragma unroll
-                for (int i = 5; i >= 0; i--) oring[(start + i) & ORM] = (uint8_t)(bytes >> (8 * i));
-              }
-              if (ischain && rr5 > 0) oring[(ts - rr5 - 1) & ORM] = (uint8_t)(rr5 - 1);
-              const uint64_t z = __ballot(ischain && rr5 > 0 && ts - rr5 - 1 == 0);
-              if (z) byte0 = (uint32_t)(rdlane(rr5, __builtin_ctzll(z)) - 1);
-            }
-            lit = lelit ? ((rdlane(lpos, le) + 1) & 31) : 0;
-          }
-          o += rdlane(incl, 63);
-          EPROF_T(t4);
-          EPROF_ADD(3, t3, t4);
           int32_t next_rel = max(endc2, lim);
           if (ser >= 0) {   // a match with length-extension bytes: the scalar token path
-            const uint32_t dm = (uint32_t)rdlane((int32_t)dist, ser);
-            const int32_t lm = rdlane(lenx, ser);
+            const uint32_t dm = (uint32_t)rdq(dist, ser);
+            const int32_t lm = ser_len;
             const uint32_t sbd = dm - 1;
             const uint32_t sulen = (uint32_t)lm;
             const bool snear = sbd < kLzNear;
@@ -392,33 +523,31 @@ __device__ __forceinline__ LzPassOut lz_pass_fast_parser(gin_t __restrict__ in, 
             const uint32_t hdr = (uint32_t)(lit - 1);
             if (lit) {
               at = o - lit - 1;
-              if (!PROBE && at == 0) byte0 = hdr;
+              if (at == 0) byte0 = hdr;
             } else {
               o--;
             }
             lit = 0;
             const int32_t ext = (int32_t)((sulen - 7) / 255);
             const int32_t stok = 1 + ext + (snear ? 2 : 4);
-            if (!PROBE) {
-              peak = max(peak, o + stok + 1);
-              if (o + stok + 1 > maxout) {
-                fail = true;
-              } else {
-                if (lane == 0 && at >= 0) oring[at & ORM] = (uint8_t)hdr;
-                const uint32_t remlen = (sulen - 7) - 255u * (uint32_t)ext;
-                const uint32_t fd = sbd - kLzNear;
-                if (lane == 0) oring[o & ORM] = (uint8_t)((7u << 5) + (snear ? (sbd >> 8) : 31u));
-                for (int32_t i0 = 0; i0 < ext; i0 += 512) {
-                  if (o + 1 + i0 + 512 - F > kOutRing) flush(o + 1 + i0);
-                  for (int32_t i = i0 + lane; i < min(ext, i0 + 512); i += 64) oring[(o + 1 + i) & ORM] = 255;
-                }
-                if (o + 1 + ext + 5 - F > kOutRing) flush(o + 1 + ext);
-                if (lane == 0) {
-                  const int32_t qq = o + 1 + ext;
-                  oring[qq & ORM] = (uint8_t)remlen;
-                  if (snear) { oring[(qq + 1) & ORM] = (uint8_t)(sbd & 255); oring[(qq + 2) & ORM] = (uint8_t)(kLzMaxCopy - 1); }
-                  else { oring[(qq + 1) & ORM] = 255; oring[(qq + 2) & ORM] = (uint8_t)(fd >> 8); oring[(qq + 3) & ORM] = (uint8_t)(fd & 255); oring[(qq + 4) & ORM] = (uint8_t)(kLzMaxCopy - 1); }
-                }
+            peak = max(peak, o + stok + 1);
+            if (o + stok + 1 > maxout) {
+              fail = true;
+            } else {
+              if (lane == 0 && at >= 0) oring[at & ORM] = (uint8_t)hdr;
+              const uint32_t remlen = (sulen - 7) - 255u * (uint32_t)ext;
+              const uint32_t fd = sbd - kLzNear;
+              if (lane == 0) oring[o & ORM] = (uint8_t)((7u << 5) + (snear ? (sbd >> 8) : 31u));
+              for (int32_t i0 = 0; i0 < ext; i0 += 512) {
+                if (o + 1 + i0 + 512 - F > kOutRing) flush(o + 1 + i0);
+                for (int32_t i = i0 + lane; i < min(ext, i0 + 512); i += 64) oring[(o + 1 + i) & ORM] = 255;
+              }
+              if (o + 1 + ext + 5 - F > kOutRing) flush(o + 1 + ext);
+              if (lane == 0) {
+                const int32_t qq = o + 1 + ext;
+                oring[qq & ORM] = (uint8_t)remlen;
+                if (snear) { oring[(qq + 1) & ORM] = (uint8_t)(sbd & 255); oring[(qq + 2) & ORM] = (uint8_t)(kLzMaxCopy - 1); }
+                else { oring[(qq + 1) & ORM] = 255; oring[(qq + 2) & ORM] = (uint8_t)(fd >> 8); oring[(qq + 3) & ORM] = (uint8_t)(fd & 255); oring[(qq + 4) & ORM] = (uint8_t)(kLzMaxCopy - 1); }
               }
             }
             o += stok + 1;

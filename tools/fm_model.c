@@ -6,9 +6,9 @@
  * thing: which earlier position a position's hash bucket offers as its candidate.  The reference
  * inserts only the positions its serial walk visits (literals, match starts, the match-end rehash),
  * so every candidate depends on the whole parse before it.  Fast mode inserts positions in TILES of
- * 64 consecutive positions, in tile order, independently of the parse:
+ * 128 consecutive positions, in tile order, independently of the parse:
  *
- *   insert_tile(t): for lane 0..63 (p = 64 t + lane < loop_end, in lane order):
+ *   insert_tile(t): for i = 0..127 (p = 128 t + i < loop_end, in order):
  *                     cand[p] = tab[hash(in[p..p+3])]; tab[hash] = p
  *
  * and the parse consumes tiles: entering tile T (the one holding the parse position) it inserts T
@@ -26,7 +26,8 @@
 #include <stdlib.h>
 #include <string.h>
 
-enum { LZ_MAX_COPY = 32, LZ_NEAR = 8191, LZ_FAR = 65535 + 8191 - 1, LZ_SHIFT = 4, LZ_MINLEN = 4, TILE = 64 };
+/* TILE = the kernel's parse step: 128 positions, two 64-lane halves exchanged in order */
+enum { LZ_MAX_COPY = 32, LZ_NEAR = 8191, LZ_FAR = 65535 + 8191 - 1, LZ_SHIFT = 4, LZ_MINLEN = 4, TILE = 128 };
 
 static inline uint32_t ld32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
 static inline uint32_t lz_hash(uint32_t seq, int hashlog) { return (seq * 2654435761U) >> (32 - hashlog); }
@@ -41,8 +42,8 @@ static inline int32_t lz_match_end(const uint8_t *in, int32_t p, int32_t r, int3
 }
 
 static void insert_tile(const uint8_t *in, int32_t t, int32_t loop_end, int tablog, uint32_t *tab, int32_t *cand) {
-  for (int32_t lane = 0; lane < TILE; lane++) {
-    const int32_t p = t * TILE + lane;
+  for (int32_t i = 0; i < TILE; i++) {
+    const int32_t p = t * TILE + i;
     if (p >= loop_end) break;
     const uint32_t h = lz_hash(ld32(in + p), tablog);
     cand[p] = (int32_t)tab[h];
