@@ -75,14 +75,18 @@ struct RawCmp {
 };
 __device__ __forceinline__ uint32_t rawc_word(const RawCmp& r, int i) { return funnel(r.d[i], r.d[i + 1], r.sh); }
 
-// Hand-over record of one position, matcher -> parser: input byte | (first mismatch + 1) << 8 |
-// candidate distance << 14.  mismatch + 1 == 0: no usable candidate (then the distance is 0); a
-// usable distance is < MAX_FARDISTANCE < 2^17, the mismatch + 1 <= 61 < 2^6.
-__device__ __forceinline__ uint32_t rec_pack(uint32_t byte, int32_t mm1, uint32_t dist) {
-  return (byte & 0xffu) | ((uint32_t)mm1 << 8) | (dist << 14);
+// Hand-over record of one position, matcher -> parser: the match the serial loop would take there
+// (L: 0 none, 4..57 its length, 127 longer than the 60-byte compare shows) | input byte << 7 |
+// candidate distance << 15.  The matcher decides the position-local rules (distance range,
+// minimum length, the far short-match rule, blosc/blosclz.c:516-540); the parser only masks the
+// positions before its parse position.  A usable distance is < MAX_FARDISTANCE < 2^17.
+constexpr int32_t kRecLong = 127;
+__device__ __forceinline__ uint32_t rec_pack(int32_t L, uint32_t byte, uint32_t dist) {
+  return (uint32_t)L | ((byte & 0xffu) << 7) | (dist << 15);
 }
-__device__ __forceinline__ int32_t rec_mm(uint32_t w) { return (int32_t)((w >> 8) & 63u) - 1; }
-__device__ __forceinline__ uint32_t rec_dist(uint32_t w) { return w >> 14; }
+__device__ __forceinline__ int32_t rec_len(uint32_t w) { return (int32_t)(w & 127u); }
+__device__ __forceinline__ uint32_t rec_byte(uint32_t w) { return (w >> 7) & 0xffu; }
+__device__ __forceinline__ uint32_t rec_dist(uint32_t w) { return w >> 15; }
 
 // ============================================================ matcher / parser workgroup ====
 // One stream per workgroup of two waves (k_encode_fast):
@@ -137,7 +141,6 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
   const int lane = lane_id();
   int32_t limit, bound, loop_end;
   fast_limits<PROBE>(length, probe_hashlog, &limit, &bound, &loop_end);
-  (void)bound;
   fast_clear_half<POS>(tab, tablog, true);
   // ---- the first two input words of each half of tile `ant` (prefetched one step ahead); the
   // other 14 are loaded only when some lane's candidate matches its first 4 bytes, together with
@@ -221,8 +224,12 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
         }
         if (x0) mm = (int32_t)(__builtin_ctz(x0) >> 3);
       }
-      sh->rec[slot][h * kHalf + lane] =
-          rec_pack(v[h], cok[h] ? mm + 1 : 0, cok[h] ? (uint32_t)(p[h] - (int32_t)cand[h]) : 0u);
+      const uint32_t d = cok[h] ? (uint32_t)(p[h] - (int32_t)cand[h]) : 0u;
+      const int32_t e = min(mm < kCmpBytes ? p[h] + mm + 1 : 0x7fffffff, bound);
+      const int32_t len = e - 4 - p[h];
+      const bool acc = cok[h] && mm >= 4 && len >= 4 && (PROBE || !(len <= 5 && d - 1 >= kLzNear));
+      const bool known = mm < kCmpBytes || p[h] + kCmpBytes + 1 >= bound;
+      sh->rec[slot][h * kHalf + lane] = rec_pack(acc ? (known ? len : kRecLong) : 0, v[h], d);
     }
   };
 
@@ -261,10 +268,11 @@ __device__ __forceinline__ int32_t rdq(const int32_t (&x)[2], int32_t q) {
 }
 
 // Exact length of the match taken at tile position m whose 60-byte compare did not find its end
-// (lenx == -1): lanes at +56, +112 with the same distance carry the next 60 bytes' compares, then
-// 64 lanes x 16 bytes per step from memory.
+// (lenx == -1): the positions at +56, +112 at the same distance carry the next 60 bytes' compares
+// (lenx -1: they match on; a known length: the match ends where theirs does), then 64 lanes x 16
+// bytes per step from memory.
 __device__ __forceinline__ int32_t fast_match_len(int32_t m, const int32_t (&lenx)[2], const int32_t (&dist)[2],
-                                                  const int32_t (&mmd)[2], int32_t P, int32_t bound, gin_t in) {
+                                                  int32_t P, int32_t bound, gin_t in) {
   const int32_t known = rdq(lenx, m);
   if (known >= 0) return known;
   const int32_t pm = P + m;
@@ -272,9 +280,9 @@ __device__ __forceinline__ int32_t fast_match_len(int32_t m, const int32_t (&len
   int32_t L = kCmpBytes, e = -1;
   for (int32_t j = m + kNbrStride; j < kFastTile; j += kNbrStride) {
     if (pm + L >= bound) { e = bound; break; }
-    const int32_t mj = rdq(mmd, j);
-    if (mj < 0 || rdq(dist, j) != dm) break;
-    if (mj < kCmpBytes) { e = min(P + j + mj + 1, bound); break; }
+    const int32_t lj = rdq(lenx, j);
+    if (lj == 0 || rdq(dist, j) != dm) break;
+    if (lj > 0) { e = P + j + 4 + lj; break; }
     L = j - m + kCmpBytes;
   }
   if (e < 0) e = pm + L >= bound ? bound : wave_match_end(in, pm + L, (uint32_t)dm, bound);
@@ -285,7 +293,7 @@ __device__ __forceinline__ int32_t fast_match_len(int32_t m, const int32_t (&len
 // matches: the chain walk, then every element's output size through two 128-position DPP scans.
 // Returns the next parse position relative to the tile.
 __device__ __forceinline__ int32_t probe_step(const uint64_t (&am)[2], int32_t (&lenx)[2], const int32_t (&dist)[2],
-                                              const int32_t (&mmd)[2], int32_t P, int32_t s0, int32_t lim,
+                                              int32_t P, int32_t s0, int32_t lim,
                                               int32_t bound, gin_t in, int32_t& lit, int32_t& o) {
   const int lane = lane_id();
   uint64_t chain[2] = {0, 0};
@@ -298,7 +306,7 @@ __device__ __forceinline__ int32_t probe_step(const uint64_t (&am)[2], int32_t (
       const int32_t m = h * kHalf + __builtin_ctzll(rem);
       int32_t lm = rdlane(lenx[h], m - h * kHalf);
       if (lm < 0) {
-        lm = fast_match_len(m, lenx, dist, mmd, P, bound, in);
+        lm = fast_match_len(m, lenx, dist, P, bound, in);
         lenx[h] = lane == m - h * kHalf ? lm : lenx[h];
       }
       if (lm >= 262) { ser = m; break; }
@@ -404,25 +412,18 @@ __device__ __forceinline__ LzPassOut lz_pass_fast_parser(gin_t __restrict__ in, 
         const int32_t P = T * kFastTile;
         const int32_t s0 = pos - P;
         const int32_t lim = min(kFastTile, loop_end - P);
-        int32_t mmd[2], dist[2], lenx[2];
+        int32_t dist[2], lenx[2];
         uint32_t vbyte[2];
         uint64_t am[2];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
-          const int32_t q = h * kHalf + lane, p = P + q;
+          const int32_t q = h * kHalf + lane;
           const uint32_t w = sh->rec[cur][q];
-          mmd[h] = rec_mm(w);   // -1: no usable candidate
+          const int32_t L = rec_len(w);
+          vbyte[h] = rec_byte(w);
           dist[h] = (int32_t)rec_dist(w);
-          vbyte[h] = w & 0xffu;
-          bool accept = false;
-          lenx[h] = 0;
-          if (q >= s0 && mmd[h] >= 4) {
-            const int32_t e = min(mmd[h] < kCmpBytes ? p + mmd[h] + 1 : 0x7fffffff, bound);
-            const int32_t len = e - 4 - p;
-            accept = len >= 4 && (PROBE || !(len <= 5 && (uint32_t)(dist[h] - 1) >= kLzNear));
-            lenx[h] = (mmd[h] < kCmpBytes || p + kCmpBytes + 1 >= bound) ? len : -1;
-          }
-          am[h] = __ballot(accept);
+          lenx[h] = L == kRecLong ? -1 : L;
+          am[h] = __ballot(q >= s0 && L != 0);
         }
         EPROF_T(t2);
         EPROF_ADD(1, t0, t2);
@@ -433,7 +434,7 @@ __device__ __forceinline__ LzPassOut lz_pass_fast_parser(gin_t __restrict__ in, 
             lit = (lit + cnt) & 31;
             pos = P + lim;
           } else {
-            pos = P + probe_step(am, lenx, dist, mmd, P, s0, lim, bound, in, lit, o);
+            pos = P + probe_step(am, lenx, dist, P, s0, lim, bound, in, lit, o);
           }
         } else {
           // ---- emitting pass: the chain walk emits each element as it takes it (literal runs by
@@ -491,7 +492,7 @@ __device__ __forceinline__ LzPassOut lz_pass_fast_parser(gin_t __restrict__ in, 
               int32_t lm = rdlane(lenx[h], m - h * kHalf);
               if (lm < 0) {
                 EPROF_T(te0);
-                lm = fast_match_len(m, lenx, dist, mmd, P, bound, in);
+                lm = fast_match_len(m, lenx, dist, P, bound, in);
                 EPROF_T(te1);
                 EPROF_ADD(5, te0, te1);
               }
