@@ -118,6 +118,10 @@ int bitshuffle_dev(int32_t typesize, int32_t nbytes, const uint8_t* d_src, uint8
 // BloscLZ encoder mode, process-wide default: 0 exact (default), 1 fast.  Returns the previous
 // mode.  A plan's own lz_mode (a context's cparams.codec_params, see include/b2h.h) overrides it.
 int set_blosclz_mode(int mode);
+// Fused launches (k_encode_fast_fused / k_encode_fused) off for the calling host thread: a caller
+// that saw a fused launch's hand-off wait time out (BLOSC2_ERROR_FAILURE for the whole batch, e.g.
+// on a time-sliced GPU) re-runs the batch with the separate shuffle / encode / layout launches.
+void set_fuse_disabled(bool off);
 // The BloscLZ mode a cparams.codec_params selects (b2h_codec_params), or -1 (none / not ours).
 int codec_params_lz_mode(const void* codec_params);
 

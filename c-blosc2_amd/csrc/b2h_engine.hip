@@ -1684,7 +1684,10 @@ static int fuse_bits() {
   const char* e = getenv("B2H_FUSE");
   return e ? atoi(e) : 83;
 }
-static bool fuse_enabled() { return (fuse_bits() & 1) != 0; }
+// Per host thread: the fused launches off (set around a retry after a hand-off timeout).
+static thread_local bool t_fuse_off = false;
+void set_fuse_disabled(bool off) { t_fuse_off = off; }
+static bool fuse_enabled() { return !t_fuse_off && (fuse_bits() & 1) != 0; }
 // B2H_FUSE_GRID (tests): cap the fused launch's persistent grid -- a few workgroups then do every
 // shuffle, stream, finalisation and scatter item, the hand-off waits' worst case.
 static int64_t fuse_grid_cap(int64_t slots) {
@@ -1707,6 +1710,9 @@ static int fuse_prepare(Workspace* ws, const CGeom& g, int64_t ntot, EncFuse& f,
   f.mode_bits = fuse_bits();
   f.trace = nullptr;
   HIPCHK(hipMemsetAsync(f.sync, 0, sync_bytes, st));
+  // B2H_FUSE_SIMULATE_TIMEOUT (tests): the launch starts with its timeout flag set, as if a
+  // hand-off wait had run out -- the batch fails and the synchronous entry points retry unfused
+  if (getenv("B2H_FUSE_SIMULATE_TIMEOUT")) HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(f.sync + 4), 1, 1, st));
   return 0;
 }
 

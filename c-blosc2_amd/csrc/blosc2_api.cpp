@@ -272,14 +272,21 @@ int compress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void* d
   if (srcsize && hipMemcpyAsync(d.in.p, src, (size_t)srcsize, hipMemcpyHostToDevice, d.stream) != hipSuccess)
     return BLOSC2_ERROR_FAILURE;
   int32_t* d_cb = reinterpret_cast<int32_t*>(d.small.p);
-  rc = b2h::compress_batch(plan, d.in.u8(), 0, 1, d.out.u8(), 0, d_cb, d.stream, d.ws);
-  if (rc < 0) {
-    TRACE_ERROR("device compression failed: %s", b2h::last_error());
-    return rc;
-  }
   int32_t cb = 0;
-  if (hipMemcpyAsync(&cb, d_cb, 4, hipMemcpyDeviceToHost, d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
-  if (hipStreamSynchronize(d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+  // a fused launch whose hand-off wait timed out fails the batch with FAILURE: run it once more
+  // with the separate launches (the chunk bytes are the same either way)
+  for (int attempt = 0; attempt < 2; attempt++) {
+    b2h::set_fuse_disabled(attempt > 0);
+    rc = b2h::compress_batch(plan, d.in.u8(), 0, 1, d.out.u8(), 0, d_cb, d.stream, d.ws);
+    b2h::set_fuse_disabled(false);
+    if (rc < 0) {
+      TRACE_ERROR("device compression failed: %s", b2h::last_error());
+      return rc;
+    }
+    if (hipMemcpyAsync(&cb, d_cb, 4, hipMemcpyDeviceToHost, d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+    if (hipStreamSynchronize(d.stream) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+    if (cb != BLOSC2_ERROR_FAILURE) break;
+  }
   const int32_t ncopy = cb > 0 ? cb : (destsize < plan.overhead ? destsize : plan.overhead);
   if (hipMemcpy(dest, d.out.p, (size_t)ncopy, hipMemcpyDeviceToHost) != hipSuccess) return BLOSC2_ERROR_FAILURE;
   return cb;

@@ -424,3 +424,35 @@ def test_gpu_fused_launches_on_two_streams_at_once(fast):
         t.join(timeout=100)
     assert not any(t.is_alive() for t in th)
     assert not errs, errs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lzmode", [1, 0], ids=["fast", "exact"])
+def test_gpu_fused_timeout_falls_back_to_separate_launches(fast, lzmode, monkeypatch):
+    """a fused launch whose hand-off wait times out (simulated: B2H_FUSE_SIMULATE_TIMEOUT
+    starts it with the timeout flag set) fails its whole batch with BLOSC2_ERROR_FAILURE on the
+    asynchronous batch API (documented), while blosc2_compress_ctx, which synchronises anyway,
+    re-runs the chunk with the separate launches and returns the normal chunk."""
+    import torch
+    B = fast
+    L = B.lib()
+    src = gen_f32(23, 1 << 20)
+    monkeypatch.setenv("B2H_FUSE", "83" if lzmode == 1 else "87")
+    want = B.compress(src, clevel=5, typesize=4, lz_mode=lzmode)
+    monkeypatch.setenv("B2H_FUSE_SIMULATE_TIMEOUT", "1")
+    ctx = L.blosc2_create_cctx(B.cparams(clevel=5, typesize=4, lz_mode=lzmode))
+    try:
+        got = B.compress_ctx(ctx, src)
+    finally:
+        L.blosc2_free_ctx(ctx)
+    assert np.array_equal(got, want)
+    assert np.array_equal(oracle_decompress(got, src.nbytes), src.view(np.uint8))
+    chunk, n = 4 << 20, 3
+    dsrc = torch.from_numpy(gen_f32(29, n * chunk // 4).view(np.uint8)).cuda()
+    stride = chunk + 256
+    comp = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+    cb = torch.zeros(n, dtype=torch.int32, device="cuda")
+    B.compress_batch(B.cparams(clevel=5, typesize=4, lz_mode=lzmode), dsrc.data_ptr(), chunk, n, chunk,
+                     comp.data_ptr(), stride, chunk + 64, cb.data_ptr(), 0)
+    torch.cuda.synchronize()
+    assert (cb.cpu().numpy() == -1).all()   # BLOSC2_ERROR_FAILURE for every chunk of the batch
