@@ -454,9 +454,14 @@ struct EncArgs {
   int32_t nstreams_total, pad;
 };
 
-template <typename TAB>
-__device__ __forceinline__ void encode_loop(const B2H_LDS EncArgs* A, TAB htab, B2H_LDS uint32_t* dbits,
-                                            B2H_LDS uint8_t* oring) {
+// Where the 144 bytes would cost a workgroup per CU (u32 positions -- streams > 64 KiB -- fill
+// exactly 80 KiB per workgroup at hashlog 14: 2 per CU) the loop reads the kernel argument.
+template <typename T>
+__device__ __forceinline__ T arg_uniform(const B2H_LDS T* p) { return lds_uniform(p); }
+template <typename T>
+__device__ __forceinline__ T arg_uniform(const T* p) { return *p; }
+template <typename TAB, typename AP>
+__device__ __forceinline__ void encode_loop(AP A, TAB htab, B2H_LDS uint32_t* dbits, B2H_LDS uint8_t* oring) {
   for (;;) {
     // branch-free grab: every lane takes part (lane 0 adds 1, the others 0), so no divergent
     // region sits between the atomic and the broadcast -- with a lane-0 branch the structurizer
@@ -465,21 +470,21 @@ __device__ __forceinline__ void encode_loop(const B2H_LDS EncArgs* A, TAB htab, 
     // through the generic pointer read back from LDS it issued 64 flat atomics per grab, and
     // ~4 M serialised RMWs on the one counter doubled the T encode)
     const int32_t i = __builtin_amdgcn_readfirstlane(__hip_atomic_fetch_add(
-        (B2H_GLB int32_t*)lds_uniform(&A->next), lane_id() == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const int32_t ntot = lds_uniform(&A->nstreams_total);
+        (B2H_GLB int32_t*)arg_uniform(&A->next), lane_id() == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const int32_t ntot = arg_uniform(&A->nstreams_total);
     if (i >= ntot) return;
     int32_t s, len, clevel;
     gin_t in;
     gout_t out;
     bool runs;
     {
-      const CGeom g = lds_uniform(&A->g);
-      s = __builtin_amdgcn_readfirstlane(pull_to_stream(g, lds_uniform(&A->porder), g.front, i, ntot));
+      const CGeom g = arg_uniform(&A->g);
+      s = __builtin_amdgcn_readfirstlane(pull_to_stream(g, arg_uniform(&A->porder), g.front, i, ntot));
       const int32_t c = s / g.nsc, l = s - c * g.nsc;
       int32_t off, blk;
       stream_locate(g, l, &off, &len, &blk);
-      in = (gin_t)(lds_uniform(&A->filt) + (int64_t)c * g.wstride + off);
-      out = (gout_t)(lds_uniform(&A->sbuf) + (int64_t)c * g.wstride + off);
+      in = (gin_t)(arg_uniform(&A->filt) + (int64_t)c * g.wstride + off);
+      out = (gout_t)(arg_uniform(&A->sbuf) + (int64_t)c * g.wstride + off);
       clevel = g.clevel;
       runs = g.overhead == kHdrExt;
     }
@@ -489,48 +494,44 @@ __device__ __forceinline__ void encode_loop(const B2H_LDS EncArgs* A, TAB htab, 
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     if (TAB::kGlobal) r.windows |= 1 << 30;   // diagnostics: the stream ran on a global-table wave
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
-    if (lane_id() == 0) lds_uniform(&A->res)[s] = r;
+    if (lane_id() == 0) arg_uniform(&A->res)[s] = r;
   }
 }
 
 __host__ __device__ constexpr size_t enc_wave_lds(int hashlog) { return ((size_t(1) << hashlog) >> 3) + kOutRing; }
+// EncArgs staged in LDS: u16 positions (see encode_loop)
+template <typename POS>
+__host__ __device__ constexpr bool enc_args_lds() { return sizeof(POS) == 2; }
 template <typename POS>
 __host__ __device__ constexpr size_t enc_wg_lds(int hashlog, int nlds, int nglb) {
   return (size_t)nlds * (sizeof(POS) << hashlog) + (size_t)(nlds + nglb) * enc_wave_lds(hashlog) +
-         ((sizeof(EncArgs) + 15) & ~size_t(15));
+         (enc_args_lds<POS>() ? ((sizeof(EncArgs) + 15) & ~size_t(15)) : 0);
 }
 
 template <typename POS, int NLDS, int NGLB>
-__global__ __launch_bounds__(64 * (NLDS + NGLB)) void k_encode(CGeom g, const uint8_t* __restrict__ filt,
-                                                               uint8_t* __restrict__ sbuf, StreamResult* __restrict__ res,
-                                                               int32_t nstreams_total, int32_t* __restrict__ next,
-                                                               POS* __restrict__ gtab, const int32_t* __restrict__ porder) {
+__global__ __launch_bounds__(64 * (NLDS + NGLB)) void k_encode(EncArgs args, POS* __restrict__ gtab) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
+  const int hashlog = args.g.clevel == 1 ? 12 : (args.g.clevel == 2 ? 13 : 14);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const size_t tabsz = sizeof(POS) << hashlog;
   B2H_LDS EncArgs* A = (B2H_LDS EncArgs*)(smem + NLDS * tabsz + (NLDS + NGLB) * enc_wave_lds(hashlog));
-  if (threadIdx.x == 0) {
-    lds_store(&A->g, g);
-    A->filt = filt;
-    A->sbuf = sbuf;
-    A->res = res;
-    A->next = next;
-    A->porder = porder;
-    A->nstreams_total = nstreams_total;
+  if (enc_args_lds<POS>()) {
+    if (threadIdx.x == 0) lds_store(A, args);
+    __syncthreads();
   }
-  __syncthreads();
   B2H_LDS uint8_t* mine = (B2H_LDS uint8_t*)(smem + NLDS * tabsz + w * enc_wave_lds(hashlog));
   B2H_LDS uint32_t* dbits = (B2H_LDS uint32_t*)mine;
   B2H_LDS uint8_t* oring = mine + ((size_t(1) << hashlog) >> 3);
   if (NLDS > 0 && w < NLDS) {
     LdsTab<POS> t;
     t.t = (volatile B2H_LDS POS*)(smem + w * tabsz);
-    encode_loop(A, t, dbits, oring);
+    if (enc_args_lds<POS>()) encode_loop(static_cast<const B2H_LDS EncArgs*>(A), t, dbits, oring);
+    else encode_loop(static_cast<const EncArgs*>(&args), t, dbits, oring);
   } else if (NGLB > 0) {
     GlbTab<POS> t;
     t.t = (B2H_GLB POS*)(gtab + (((size_t)blockIdx.x * NGLB + (w - NLDS)) << hashlog));
-    encode_loop(A, t, dbits, oring);
+    if (enc_args_lds<POS>()) encode_loop(static_cast<const B2H_LDS EncArgs*>(A), t, dbits, oring);
+    else encode_loop(static_cast<const EncArgs*>(&args), t, dbits, oring);
   }
 }
 
@@ -2139,7 +2140,16 @@ static int launch_encode_shape(Workspace* ws, const CGeom& g, int hashlog, const
     if (ws->gtab.ensure(((size_t)grid * NG << hashlog) * sizeof(POS))) return E_MEMORY;
     gt = ws->gtab.as<POS>();
   }
-  k_encode<POS, NL, NG><<<grid, 64 * (NL + NG), lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, gt, porder);
+  EncArgs args;
+  args.g = g;
+  args.filt = filt;
+  args.sbuf = ws->sbuf.as<uint8_t>();
+  args.res = res;
+  args.next = next;
+  args.porder = porder;
+  args.nstreams_total = (int32_t)ntot;
+  args.pad = 0;
+  k_encode<POS, NL, NG><<<grid, 64 * (NL + NG), lds, st>>>(args, gt);
   HIPCHK(hipGetLastError());
   return 0;
 }
