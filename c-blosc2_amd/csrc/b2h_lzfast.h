@@ -460,6 +460,10 @@ __device__ __forceinline__ LzPassOut lz_pass_fast_parser(gin_t __restrict__ in, 
           };
           // MATCH_SHORT / MATCH_LONG (+ _FAR) token + the marker opening the next literal run
           // (blosc/blosclz.c:270-316); the run it ends gets its header (lane 8).
+          // A token's place in the output is known in the walk (a scalar chain); its bytes are
+          // written afterwards by one lane per token, all tokens of the step at once (the walk
+          // records start, length, distance and the header it closes into lane k of e_*).
+          int32_t nel = 0, e_ts = 0, e_len = 0, e_dist = 0, e_at = -1, e_hdr = 0;
           auto emit_token = [&](int32_t lm, uint32_t dm) {
             int32_t at = -1;
             const uint32_t hdr = (uint32_t)(lit - 1);
@@ -470,16 +474,15 @@ __device__ __forceinline__ LzPassOut lz_pass_fast_parser(gin_t __restrict__ in, 
               o--;
             }
             lit = 0;
-            const uint32_t bd = dm - 1, ulen = (uint32_t)lm, fd = bd - kLzNear;
-            const bool near = bd < kLzNear, lng = ulen >= 7;
-            const uint32_t b0 = (lng ? (7u << 5) : (ulen << 5)) + (near ? (bd >> 8) : 31u);
-            const uint32_t dbytes = near ? (bd & 255u) : (255u | ((fd >> 8) << 8) | ((fd & 255u) << 16));
-            uint64_t rest = (uint64_t)dbytes | (31ull << (near ? 8 : 24));
-            if (lng) rest = (uint64_t)(ulen - 7) | (rest << 8);
-            const uint64_t bytes = (uint64_t)b0 | (rest << 8);
-            const int32_t tok = lng ? (near ? 3 : 5) : (near ? 2 : 4);
-            const bool wr = lane <= tok || (lane == 8 && at >= 0);
-            if (wr) oring[(lane <= tok ? o + lane : at) & ORM] = lane <= tok ? (uint8_t)(bytes >> (8 * lane)) : (uint8_t)hdr;
+            const uint32_t bd = dm - 1;
+            const int32_t tok = (uint32_t)lm >= 7 ? (bd < kLzNear ? 3 : 5) : (bd < kLzNear ? 2 : 4);
+            const bool me = lane == nel;
+            e_ts = me ? o : e_ts;
+            e_len = me ? lm : e_len;
+            e_dist = me ? (int32_t)dm : e_dist;
+            e_at = me ? at : e_at;
+            e_hdr = me ? (int32_t)hdr : e_hdr;
+            nel++;
             o += tok + 1;
             req = o;
           };
@@ -507,6 +510,25 @@ __device__ __forceinline__ LzPassOut lz_pass_fast_parser(gin_t __restrict__ in, 
           }
           const int32_t lit_end = ser >= 0 ? ser : lim;
           if (c < lit_end) emit_lits(c, lit_end);
+          if (nel) {
+            // the step's tokens (MATCH_SHORT / MATCH_LONG + _FAR, blosc/blosclz.c:270-316) + the
+            // marker opening the next literal run, in DESCENDING byte order: a token right after
+            // a marker (no literal between) overwrites it at its byte 0, written last; then the
+            // headers of the literal runs the tokens close
+            const bool el = lane < nel;
+            const uint32_t bd = (uint32_t)e_dist - 1, ulen = (uint32_t)e_len, fd = bd - kLzNear;
+            const bool near = bd < kLzNear, lng = ulen >= 7;
+            const uint32_t b0 = (lng ? (7u << 5) : (ulen << 5)) + (near ? (bd >> 8) : 31u);
+            const uint32_t dbytes = near ? (bd & 255u) : (255u | ((fd >> 8) << 8) | ((fd & 255u) << 16));
+            uint64_t rest = (uint64_t)dbytes | (31ull << (near ? 8 : 24));
+            if (lng) rest = (uint64_t)(ulen - 7) | (rest << 8);
+            const uint64_t bytes = (uint64_t)b0 | (rest << 8);
+            const int32_t tok = lng ? (near ? 3 : 5) : (near ? 2 : 4);
+#pragma unroll
+            for (int i = 5; i >= 0; i--)
+              if (el && i <= tok) oring[(e_ts + i) & ORM] = (uint8_t)(bytes >> (8 * i));
+            if (el && e_at >= 0) oring[e_at & ORM] = (uint8_t)e_hdr;
+          }
           if (req >= 0) {
             peak = max(peak, req);
             if (req > maxout) { fail = true; break; }
