@@ -70,6 +70,8 @@ struct Scratch {
     cap = n;
     static const bool poison = getenv("B2H_POISON") != nullptr;   // debug: expose unwritten bytes
     if (poison) (void)hipMemset(p, 0xA5, n);
+    static const bool trace = getenv("B2H_TRACE_ALLOC") != nullptr;   // debug: where each buffer lives
+    if (trace) fprintf(stderr, "b2h scratch %p + %zu\n", p, n);
     return 0;
   }
   void release() {
@@ -536,44 +538,47 @@ __global__ __launch_bounds__(64 * (NLDS + NGLB)) void k_encode(EncArgs args, POS
 }
 
 // ------------------------------------------------------------------ BloscLZ fast mode ----
-// One stream per workgroup of two waves: wave 0 matches, wave 1 parses (b2h_lzfast.h);
-// persistent, pulling streams like k_encode.  LDS per workgroup: table + output ring + hand-over
-// slots.
+// One stream per workgroup of four waves (b2h_lzfast.h: exchanges, checks, segment-parallel
+// walk, emission); persistent, pulling streams like k_encode.
 __host__ __device__ constexpr size_t fast_lds(size_t pos_bytes, int tablog) {
-  return (pos_bytes << tablog) + kOutRing + ((sizeof(FastShared) + 15) & ~size_t(15));
+  return pos_bytes == 2 ? fm_lds_bytes<uint16_t>(tablog) : fm_lds_bytes<uint32_t>(tablog);
 }
 template <typename POS>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4, 8)))   // <= 128 VGPRs: 16 waves per CU
+__global__ __launch_bounds__(kFmThreads) __attribute__((amdgpu_waves_per_eu(4, 8)))   // <= 128 VGPRs
 void k_encode_fast(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
                    StreamResult* __restrict__ res, int32_t nstreams_total, int32_t* __restrict__ next, int tablog,
                    const int32_t* __restrict__ porder) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  B2H_LDS uint8_t* tab = (B2H_LDS uint8_t*)smem;
-  B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + (sizeof(POS) << tablog));
-  B2H_LDS FastShared* sh = (B2H_LDS FastShared*)(smem + (sizeof(POS) << tablog) + kOutRing);
-  const bool matcher = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
-  if (!matcher) __builtin_amdgcn_s_setprio(2);   // the parser issues first (see k_encode_fast_fused)
+  const FmBufs B = fm_bufs<POS>((B2H_LDS uint8_t*)smem);
   for (;;) {
-    if (threadIdx.x == 0) sh->pull = atomicAdd(next, 1);
+    if (threadIdx.x == 0) B.sh->pull = atomicAdd(next, 1);
     __syncthreads();
-    const int32_t i = __builtin_amdgcn_readfirstlane(sh->pull);
+    const int32_t i = __builtin_amdgcn_readfirstlane(B.sh->pull);
     __syncthreads();
     if (i >= nstreams_total) return;
     const int32_t s = __builtin_amdgcn_readfirstlane(pull_to_stream(g, porder, g.front, i, nstreams_total));
     const int32_t c = s / g.nsc, l = s - c * g.nsc;
     int32_t off, len, blk;
     stream_locate(g, l, &off, &len, &blk);
+    if (!FM_OK(s >= 0 && s < nstreams_total && off >= 0 && len >= 0 && off + len <= g.wstride, 8, s, off, len)) continue;
     gin_t in = (gin_t)(filt + (int64_t)c * g.wstride + off);
     gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
-    StreamResult r = encode_stream_fast<POS>(in, len, g.clevel, out, tab, tablog, oring, sh, g.overhead == kHdrExt,
-                                             matcher);
+    StreamResult r = encode_stream_fast<POS>(in, len, g.clevel, out, B, tablog, g.overhead == kHdrExt);
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
-    if (!matcher && lane_id() == 0) res[s] = r;
+    if (threadIdx.x == 0) res[s] = r;
   }
 }
+
+#ifdef B2H_FM_CHECK
+extern "C" __attribute__((visibility("default"))) int b2h_fm_debug(int64_t* out) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fm_bad), 8 * sizeof(int64_t)) != hipSuccess) return -1;
+  return 0;
+}
+#endif
 
 // BloscLZ encoder mode: exact (default, byte-identical to the reference) or fast (round-trip
 // identical, same grammar and decisions, parse-independent candidates).  Process-wide; also
@@ -612,9 +617,11 @@ static int launch_encode_fast_t(Workspace* ws, const CGeom& g, const uint8_t* fi
     HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  const int slots = resident_slots(fn, lds, 128);
+  static const int grid_env = [] { const char* e = getenv("B2H_FAST_GRID"); return e ? atoi(e) : 0; }();   // debug
+  const int slots = grid_env > 0 ? grid_env : resident_slots(fn, lds, kFmThreads);
   const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(ntot, slots));
-  k_encode_fast<POS><<<grid, 128, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog, porder);
+  k_encode_fast<POS><<<grid, kFmThreads, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog,
+                                                    porder);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1421,15 +1428,15 @@ __host__ __device__ constexpr size_t fused_lds(size_t pos_bytes, int tablog) {
 #undef FUSE_TRACE_PTR
 #define FUSE_TRACE_PTR lds_uniform(&A->f.trace)
 template <typename POS>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4, 8)))   // as k_encode_fast
+__global__ __launch_bounds__(kFmThreads) __attribute__((amdgpu_waves_per_eu(4, 8)))   // as k_encode_fast
 void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint8_t* __restrict__ sbuf_arg,
                          StreamResult* __restrict__ res_arg, int32_t nstreams_total_arg, int32_t* __restrict__ next_arg,
                          int tablog_arg, const int32_t* __restrict__ porder_arg, EncFuse f_arg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tablog0 = tablog_arg;
-  B2H_LDS uint8_t* tab = (B2H_LDS uint8_t*)smem;
-  B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + (sizeof(POS) << tablog0));
-  B2H_LDS FastShared* sh = (B2H_LDS FastShared*)(smem + (sizeof(POS) << tablog0) + kOutRing);
+  const FmBufs Bf = fm_bufs<POS>((B2H_LDS uint8_t*)smem);
+  B2H_LDS uint8_t* tab = Bf.tab;
+  B2H_LDS FmShared* sh = Bf.sh;
   B2H_LDS FusedArgs* A = (B2H_LDS FusedArgs*)(smem + fast_lds(sizeof(POS), tablog0));
   if (threadIdx.x == 0) {
     lds_store(&A->g, g_arg);
@@ -1443,10 +1450,9 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
     A->tablog = tablog_arg;
   }
   __syncthreads();
-  const bool matcher = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
-  // wave priority (B2H_FUSE bit 64, default): the parser -- the tile's latency chain -- issues
-  // ahead of the matchers sharing its SIMD (T encode 18.0 -> 17.6 ms; the matcher first: 19.3)
-  if ((lds_uniform(&A->f.mode_bits) & 64) && !matcher) __builtin_amdgcn_s_setprio(2);
+  // wave priority (B2H_FUSE bit 64, default): wave 0 -- the exchanges and the walk, the stream's
+  // latency chain -- issues ahead of the other waves sharing its SIMD
+  if ((lds_uniform(&A->f.mode_bits) & 64) && threadIdx.x < 64) __builtin_amdgcn_s_setprio(2);
   // lane 0 of the workgroup computes v, everyone gets it
   auto bcast = [&](int32_t v) -> int32_t {
     if (threadIdx.x == 0) sh->bcast = v;
@@ -1479,7 +1485,7 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
     const int32_t c = v - 1;
     if (__builtin_amdgcn_readfirstlane(f2.mode[c]) != 0) return;
     uint8_t* d = f2.dst + (int64_t)c * g2.dst_stride;
-    const int32_t wv = threadIdx.x >> 6;
+    const int32_t wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
     for (int32_t l = j0; l < min(j0 + kFuseSpi, g2.nsc); l++) {
       const int32_t s = c * g2.nsc + l;
       Place pl;
@@ -1495,7 +1501,7 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
       }
       if (pl.csize <= 0) continue;
       const uint8_t* src = (pl.csize == len ? filt : sbuf) + (int64_t)c * g2.wstride + off;
-      const int32_t q = ((pl.csize + 1) / 2 + 15) & ~15;
+      const int32_t q = ((pl.csize + nwv - 1) / nwv + 15) & ~15;
       const int32_t a = min(pl.csize, wv * q), b = min(pl.csize, a + q);
       if (b > a) {
         if ((f2.mode_bits & 32) || !aligned16(src + a)) wave_copy((gout_t)(d + pl.off + a), (gin_t)(src + a), b - a);
@@ -1588,10 +1594,10 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
     FUSE_TRACE(6, s);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
-    StreamResult r = encode_stream_fast<POS, true>(in, len, clevel, out, tab, tablog, oring, sh, runs, matcher);
+    StreamResult r = encode_stream_fast<POS, true>(in, len, clevel, out, Bf, tablog, runs);
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
-    if (!matcher && lane_id() == 0) {
+    if (threadIdx.x == 0) {
       int32_t* fin = lds_uniform(&A->f.fin);
       lds_uniform(&A->res)[s] = r;
       st_agent(fin + 3 * s, r.kind);
@@ -1730,7 +1736,7 @@ static int launch_encode_fast_fused_t(Workspace* ws, const CGeom& g, const uint8
     HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  const int slots = resident_slots(fn, lds, 128);
+  const int slots = resident_slots(fn, lds, kFmThreads);
   const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(ntot, fuse_grid_cap(slots)));
   if (fuse_prepare(ws, g, ntot, f, st)) return E_MEMORY;
   static int32_t* trace = nullptr;
@@ -1738,7 +1744,7 @@ static int launch_encode_fast_fused_t(Workspace* ws, const CGeom& g, const uint8
   if (tr && !trace) HIPCHK(hipHostMalloc(&trace, 4 << 20, hipHostMallocCoherent));
   f.trace = tr ? trace : nullptr;
   if (tr) memset(trace, 0xff, 4 * (size_t)grid);
-  k_encode_fast_fused<POS><<<grid, 128, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog,
+  k_encode_fast_fused<POS><<<grid, kFmThreads, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog,
                                                    porder, f);
   HIPCHK(hipGetLastError());
   if (tr) {   // debug watchdog: report where the workgroups are if the launch has not ended after 5 s

@@ -90,9 +90,9 @@ __device__ __forceinline__ void st8(gout_t base, __amdgpu_buffer_rsrc_t r, int32
 // byte is its output offset mod kOutRing, so a 16-aligned output offset is a 16-aligned ring
 // offset when `out` is 16-aligned), bytes at the ends; WT: write-through (`sc1`) stores, for
 // streams another workgroup copies inside the same launch (k_encode_fast_fused).
-template <bool WT>
-__device__ __forceinline__ void ring_flush(gout_t out, const B2H_LDS uint8_t* oring, int32_t F, int32_t to) {
-  constexpr int32_t ORM = kOutRing - 1;
+template <bool WT, int32_t RING = kOutRing>
+__device__ __forceinline__ void ring_flush_n(gout_t out, const B2H_LDS uint8_t* oring, int32_t F, int32_t to) {
+  constexpr int32_t ORM = RING - 1;
   const int lane = lane_id();
   const __amdgpu_buffer_rsrc_t r = wt_rsrc(out);
   if ((reinterpret_cast<uintptr_t>(out) & 15) != 0 || to - F < 32) {
@@ -104,6 +104,10 @@ __device__ __forceinline__ void ring_flush(gout_t out, const B2H_LDS uint8_t* or
   if (lane < to - b) st8<WT>(out, r, b + lane, oring[(b + lane) & ORM]);
   for (int32_t y = a + 16 * lane; y < b; y += 1024)
     st16<WT>(out, r, y, *reinterpret_cast<const B2H_LDS u32x4*>(oring + (y & ORM)));
+}
+template <bool WT>
+__device__ __forceinline__ void ring_flush(gout_t out, const B2H_LDS uint8_t* oring, int32_t F, int32_t to) {
+  ring_flush_n<WT, kOutRing>(out, oring, F, to);
 }
 
 
@@ -311,7 +315,10 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t __restrict__ in, int32_t leng
     pos = 0;
   } else {
     pos = 4;
-    if (lane < 5) oring[lane] = lane == 0 ? (uint8_t)(kLzMaxCopy - 1) : in[lane - 1];
+    if (lane < 5) {   // marker + four literals; the load index never negative (in[-1] lies outside the image)
+      const uint8_t b = in[lane > 0 ? lane - 1 : 0];
+      oring[lane] = lane == 0 ? (uint8_t)(kLzMaxCopy - 1) : b;
+    }
   }
   int32_t peak = 0;
   bool fail = false;

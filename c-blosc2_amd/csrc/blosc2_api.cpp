@@ -977,11 +977,25 @@ int ctx_append_device(blosc2_context* ctx, const uint8_t* d_src, const int32_t* 
     }
     return rc;
   };
+  std::vector<int32_t> cbh((size_t)group);
   for (int32_t g0 = 0; g0 < n; g0 += group) {
     const int32_t m = std::min(group, n - g0);
-    int rc = compress_device_locked(ctx, d_src + (int64_t)g0 * src_stride, nbytes + g0, m, src_stride, d.out.u8(),
-                                    dst_stride, d_cb);
-    if (rc < 0) return fail(rc);
+    // a fused launch whose hand-off wait timed out fails its whole batch with FAILURE (b2h.h): the
+    // group runs once more with the separate launches, from the sticky blocksize it started with,
+    // so every chunk is still the serial blosc2_schunk_append_buffer's
+    const int32_t blocksize0 = ctx->blocksize;
+    for (int attempt = 0; attempt < 2; attempt++) {
+      ctx->blocksize = blocksize0;
+      b2h::set_fuse_disabled(attempt > 0);
+      int rc = compress_device_locked(ctx, d_src + (int64_t)g0 * src_stride, nbytes + g0, m, src_stride, d.out.u8(),
+                                      dst_stride, d_cb);
+      b2h::set_fuse_disabled(false);
+      if (rc < 0) return fail(rc);
+      if (hipMemcpyAsync(cbh.data(), d_cb, 4 * (size_t)m, hipMemcpyDeviceToHost, d.stream) != hipSuccess ||
+          hipStreamSynchronize(d.stream) != hipSuccess)
+        return fail(BLOSC2_ERROR_FAILURE);
+      if (std::find(cbh.begin(), cbh.begin() + m, (int32_t)BLOSC2_ERROR_FAILURE) == cbh.begin() + m) break;
+    }
     if (b2h::pack_chunks(d.out.u8(), dst_stride, d_cb, m, d.in.u8(), d_off, d.stream) < 0) return fail(BLOSC2_ERROR_FAILURE);
     if (hipMemcpyAsync(off.data(), d_off, 8 * ((size_t)m + 1), hipMemcpyDeviceToHost, d.stream) != hipSuccess ||
         hipStreamSynchronize(d.stream) != hipSuccess)

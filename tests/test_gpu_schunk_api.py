@@ -248,3 +248,50 @@ def test_set_slice_matches_reference(pipe):
     finally:
         for sc in (a, b, c):
             sc.free()
+
+
+@pytest.mark.parametrize("lzmode", [0, 1], ids=["exact", "fast"])
+def test_device_batches_survive_fused_timeout(lzmode, monkeypatch):
+    """VERDICT r3 item 8 / ADVICE r3: a fused launch whose hand-off wait times out (simulated with
+    B2H_FUSE_SIMULATE_TIMEOUT: the launch starts with its timeout flag set) fails its batch; the
+    super-chunk batch forms (b2h_schunk_append_device, b2h_schunk_set_slice_device, both through
+    ctx_append_device) re-run the group with the separate launches from the same sticky blocksize.
+    Exact mode (fused with B2H_FUSE bit 4): chunks and counters equal the reference's serial calls;
+    fast mode: equal to the same calls without the simulated timeout."""
+    import torch
+    kw = dict(PIPES["shuffle4"])
+    data, sizes = _data(4, 5, 100 * 1024 + 8)
+    dev = torch.from_numpy(data).cuda()
+    sz = (C.c_int32 * len(sizes))(*sizes)
+    lo, hi = (CHUNK - 40) // 4, (3 * CHUNK + 72) // 4
+    new = np.random.default_rng(5).integers(0, 7, (hi - lo) * 4, dtype=np.uint8)
+    dnew = torch.from_numpy(new).cuda()
+
+    def run():
+        a = B.SChunk(B.cparams(**kw, lz_mode=lzmode), B.dparams())
+        assert a.L.b2h_schunk_append_device(a.p, C.c_void_p(dev.data_ptr()), sz, len(sizes), CHUNK) == len(sizes)
+        assert a.L.b2h_schunk_set_slice_device(a.p, lo, hi, C.c_void_p(dnew.data_ptr())) == 0
+        torch.cuda.synchronize()
+        return a
+
+    monkeypatch.setenv("B2H_FUSE", "87" if lzmode == 0 else "83")
+    want = run()
+    monkeypatch.setenv("B2H_FUSE_SIMULATE_TIMEOUT", "1")
+    got = run()
+    try:
+        _assert_same(got, want)
+        if lzmode == 0:
+            from b2ctypes import cparams as rcp, dparams as rdp
+            b = B.SChunk(rcp(**kw), rdp(), L=_ref())
+            try:
+                off = 0
+                for n in sizes:
+                    b.append_buffer(data[off:off + n])
+                    off += n
+                assert b.set_slice(lo, hi, new) == 0
+                _assert_same(got, b)
+            finally:
+                b.free()
+    finally:
+        got.free()
+        want.free()
