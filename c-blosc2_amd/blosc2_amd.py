@@ -119,6 +119,12 @@ def bind_schunk(lib):
         "b2h_schunk_append_device": ([sp, vp, vp, i32, i64], i64),
         "b2h_schunk_decompress_device": ([sp, i64, i32, vp, i64, i32, vp], C.c_int),
         "b2h_schunk_get_slice_device": ([sp, i64, i64, vp], C.c_int),
+        "blosc2_schunk_from_buffer": ([vp, i64, C.c_bool], sp),
+        "blosc2_schunk_open": ([C.c_char_p], sp),
+        "blosc2_schunk_open_offset": ([C.c_char_p, i64], sp),
+        "blosc2_schunk_to_buffer": ([sp, C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_bool)], i64),
+        "blosc2_meta_add": ([sp, C.c_char_p, vp, i32], C.c_int),
+        "blosc2_vlmeta_add": ([sp, C.c_char_p, vp, i32, vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name, None)
@@ -310,6 +316,13 @@ class SChunk:
         self.p = self.L.blosc2_schunk_new(C.byref(st))
         if not self.p:
             raise RuntimeError("blosc2_schunk_new failed")
+
+    @classmethod
+    def wrap(cls, p, L):
+        """Take ownership of a super-chunk pointer `p` of library `L` (blosc2_schunk_open & co.)."""
+        self = cls.__new__(cls)
+        self.L, self._keep, self.p = L, None, p
+        return self
 
     @property
     def s(self):

@@ -5,7 +5,7 @@ set -e
 H=$(cd $(dirname $0) && pwd)
 D=$H/${1:-lib_dbg}
 mkdir -p $D
-F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -fvisibility=hidden -mcode-object-version=5 -I$H/../include -DB2H_FM_CHECK ${2:-}"
+F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -fvisibility=hidden -mcode-object-version=5 -I$H/../include ${2--DB2H_FM_CHECK}"
 for f in b2h_engine.hip blosc2_api.cpp b2h_frame.cpp b2h_schunk.cpp; do
   /opt/rocm/bin/hipcc $F -c -x hip $H/csrc/$f -o $D/${f%.*}.o &
 done

@@ -544,7 +544,10 @@ __host__ __device__ constexpr size_t fast_lds(size_t pos_bytes, int tablog) {
   return pos_bytes == 2 ? fm_lds_bytes<uint16_t>(tablog) : fm_lds_bytes<uint32_t>(tablog);
 }
 template <typename POS>
-__global__ __launch_bounds__(kFmThreads) __attribute__((amdgpu_waves_per_eu(4, 8)))   // <= 128 VGPRs
+#ifndef B2H_FM_WPE
+#define B2H_FM_WPE 4   // waves per SIMD the fast encoder is compiled for (diagnostic builds vary it)
+#endif
+__global__ __launch_bounds__(kFmThreads) __attribute__((amdgpu_waves_per_eu(B2H_FM_WPE, 8)))   // <= 128 VGPRs
 void k_encode_fast(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
                    StreamResult* __restrict__ res, int32_t nstreams_total, int32_t* __restrict__ next, int tablog,
                    const int32_t* __restrict__ porder) {
@@ -563,14 +566,32 @@ void k_encode_fast(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restric
     if (!FM_OK(s >= 0 && s < nstreams_total && off >= 0 && len >= 0 && off + len <= g.wstride, 8, s, off, len)) continue;
     gin_t in = (gin_t)(filt + (int64_t)c * g.wstride + off);
     gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
+    FM_TRACE(0, s);
+    FM_TRACE(1, len);
+    FM_TRACE(2, off);
+    FM_TRACE(11, i);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
     StreamResult r = encode_stream_fast<POS>(in, len, g.clevel, out, B, tablog, g.overhead == kHdrExt);
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
     if (threadIdx.x == 0) res[s] = r;
+    FM_TRACE(12, r.size);
+    FM_TRACE(6, 9);
   }
 }
+
+#ifdef B2H_FM_TRACE
+extern "C" __attribute__((visibility("default"))) void* b2h_fm_trace_alloc(int32_t words) {
+  void* h = nullptr;
+  if (hipHostMalloc(&h, (size_t)words * 4, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return nullptr;
+  memset(h, 0xff, (size_t)words * 4);
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) return nullptr;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_fm_trace), &d, sizeof d) != hipSuccess) return nullptr;
+  return h;
+}
+#endif
 
 #ifdef B2H_FM_CHECK
 extern "C" __attribute__((visibility("default"))) int b2h_fm_debug(int64_t* out) {
@@ -1428,7 +1449,7 @@ __host__ __device__ constexpr size_t fused_lds(size_t pos_bytes, int tablog) {
 #undef FUSE_TRACE_PTR
 #define FUSE_TRACE_PTR lds_uniform(&A->f.trace)
 template <typename POS>
-__global__ __launch_bounds__(kFmThreads) __attribute__((amdgpu_waves_per_eu(4, 8)))   // as k_encode_fast
+__global__ __launch_bounds__(kFmThreads) __attribute__((amdgpu_waves_per_eu(B2H_FM_WPE, 8)))   // as k_encode_fast
 void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint8_t* __restrict__ sbuf_arg,
                          StreamResult* __restrict__ res_arg, int32_t nstreams_total_arg, int32_t* __restrict__ next_arg,
                          int tablog_arg, const int32_t* __restrict__ porder_arg, EncFuse f_arg) {

@@ -535,3 +535,203 @@ int b2h_frame_get_sparse_buffer(b2h_frame* f, int64_t ncoords, const int64_t* co
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------ frame -> super-chunk ----
+namespace {
+
+// One metalayer index (msgpack): be16 idx_size, 0xde map16 (be16 count), then per layer a fixstr
+// name and 0xd2 + be32 offset of its content (0xc6 bin32: be32 length, bytes), offsets from `base`.
+// Header metalayers: get_meta_from_header (blosc/frame.c:2388-2500), index at FRAME_IDX_SIZE (89);
+// trailer vlmetalayers: get_vlmeta_from_trailer (2591-2720), index at FRAME_TRAILER_VLMETALAYERS + 2.
+int read_layers(const uint8_t* base, int64_t len, int64_t idx, int max, blosc2_metalayer** out, int* count) {
+  int64_t pos = idx + 2 + 1 + 2;
+  if (len < pos) return BLOSC2_ERROR_READ_BUFFER;
+  const uint8_t* p = base + idx + 2;
+  if (p[0] != 0xde) return BLOSC2_ERROR_DATA;
+  const int n = (int)be(p + 1, 2);
+  p += 3;
+  if (n > max) return BLOSC2_ERROR_DATA;
+  for (int k = 0; k < n; k++) {
+    if (len < ++pos) return BLOSC2_ERROR_READ_BUFFER;
+    if ((*p & 0xe0u) != 0xa0u) return BLOSC2_ERROR_DATA;
+    const int nslen = *p & 0x1f;
+    p++;
+    if (len < (pos += nslen)) return BLOSC2_ERROR_READ_BUFFER;
+    blosc2_metalayer* m = static_cast<blosc2_metalayer*>(calloc(1, sizeof(blosc2_metalayer)));
+    if (!m) return BLOSC2_ERROR_MEMORY_ALLOC;
+    out[k] = m;
+    *count = k + 1;
+    m->name = static_cast<char*>(malloc((size_t)nslen + 1));
+    if (!m->name) return BLOSC2_ERROR_MEMORY_ALLOC;
+    memcpy(m->name, p, (size_t)nslen);
+    m->name[nslen] = '\0';
+    p += nslen;
+    if (len < (pos += 1 + 4)) return BLOSC2_ERROR_READ_BUFFER;
+    if (*p != 0xd2) return BLOSC2_ERROR_DATA;
+    const int64_t off = be(p + 1, 4);
+    p += 5;
+    if (off < 0 || off >= len) return BLOSC2_ERROR_DATA;
+    if (len < off + 5) return BLOSC2_ERROR_READ_BUFFER;
+    if (base[off] != 0xc6) return BLOSC2_ERROR_DATA;
+    const int64_t clen = be(base + off + 1, 4);
+    if (clen < 0) return BLOSC2_ERROR_DATA;
+    if (len < off + 5 + clen) return BLOSC2_ERROR_READ_BUFFER;
+    m->content_len = (int32_t)clen;
+    m->content = static_cast<uint8_t*>(malloc(clen > 0 ? (size_t)clen : 1));
+    if (!m->content) return BLOSC2_ERROR_MEMORY_ALLOC;
+    if (clen > 0) memcpy(m->content, base + off + 5, (size_t)clen);
+  }
+  return 0;
+}
+
+// frame_to_schunk (blosc/frame.c:2941-3245): header fields -> cparams, every chunk into the
+// in-memory index (special offsets become 32-byte special chunks, frame_special_chunk 3321-3365),
+// counters, metalayers and vlmetalayers.  `copy` selects the reference's two flavours: a copy
+// (storage not contiguous, cbytes = sum of the chunks, blocksize = the chunks' common one) or a
+// frame-attached handle (contiguous, header cbytes and blocksize).  Either way the chunks live in
+// host memory here; writes to the handle do not go back to the frame.
+blosc2_schunk* schunk_from_frame(b2h_frame* f, bool copy, const char* urlpath) {
+  const uint8_t* h = f->host;
+  blosc2_cparams cp = BLOSC2_CPARAMS_DEFAULTS;
+  cp.typesize = f->typesize;
+  cp.clevel = f->clevel;
+  cp.compcode = f->compcode == BLOSC_UDCODEC_FORMAT ? h[77] : f->compcode;   // FRAME_UDCODEC
+  cp.compcode_meta = h[78];                                                    // FRAME_CODEC_META
+  cp.splitmode = (h[28] & 0x03) + 1;                                           // FRAME_OTHER_FLAGS
+  cp.use_dict = h[85] & 1;                                                     // FRAME_OTHER_FLAGS2
+  cp.blocksize = f->blocksize;
+  memcpy(cp.filters, f->filters, 6);
+  memcpy(cp.filters_meta, f->filters_meta, 6);
+  blosc2_dparams dp = BLOSC2_DPARAMS_DEFAULTS;
+  blosc2_storage st = BLOSC2_STORAGE_DEFAULTS;
+  st.contiguous = false;
+  st.urlpath = nullptr;
+  st.cparams = &cp;
+  st.dparams = &dp;
+  blosc2_schunk* s = blosc2_schunk_new(&st);
+  if (!s) return nullptr;
+  int rc = 0;
+  int32_t common_bs = 0;
+  for (int64_t i = 0; i < f->nchunks && rc >= 0; i++) {
+    uint8_t special[BLOSC_EXTENDED_HEADER_LENGTH];
+    uint8_t* c;
+    if (f->offsets[i] >= 0) {
+      c = f->host + f->header_len + f->offsets[i];
+      const int32_t cb = le32(c + 12);
+      if (cb < BLOSC_EXTENDED_HEADER_LENGTH || f->offsets[i] + cb > f->cbytes) rc = BLOSC2_ERROR_INVALID_HEADER;
+    } else {
+      blosc2_cparams scp = BLOSC2_CPARAMS_DEFAULTS;
+      scp.typesize = f->typesize;
+      scp.blocksize = f->blocksize;
+      const uint64_t v = (uint64_t)f->offsets[i];
+      const int32_t nb = chunk_nbytes(f, i);
+      if (v & ((uint64_t)BLOSC2_SPECIAL_ZERO << 56)) rc = blosc2_chunk_zeros(scp, nb, special, sizeof special);
+      else if (v & ((uint64_t)BLOSC2_SPECIAL_UNINIT << 56)) rc = blosc2_chunk_uninit(scp, nb, special, sizeof special);
+      else if (v & ((uint64_t)BLOSC2_SPECIAL_NAN << 56)) rc = blosc2_chunk_nans(scp, nb, special, sizeof special);
+      else rc = BLOSC2_ERROR_DATA;
+      c = special;
+    }
+    if (rc < 0) break;
+    const int32_t bs = le32(c + 8);
+    common_bs = i == 0 ? bs : (common_bs == bs ? bs : 0);
+    const int64_t r = blosc2_schunk_append_chunk(s, c, true);
+    if (r < 0) rc = (int)r;
+  }
+  if (rc >= 0 && s->nbytes != f->nbytes) rc = BLOSC2_ERROR_INVALID_HEADER;
+  if (rc >= 0 && f->nchunks > 0) s->flags2 = s->data[0][BLOSC2_CHUNK_BLOSC2_FLAGS2];
+  s->current_nchunk = 0;
+  if (rc >= 0) {
+    s->chunksize = f->chunksize;
+    if (copy) {
+      s->blocksize = common_bs;   // cbytes: the appended chunks' sum already
+    } else {
+      s->cbytes = f->cbytes;
+      s->blocksize = f->blocksize;
+      s->storage->contiguous = true;
+      if (urlpath) s->storage->urlpath = strdup(urlpath);
+    }
+  }
+  int nm = 0;
+  if (rc >= 0) {
+    rc = read_layers(h, f->header_len, 89, BLOSC2_MAX_METALAYERS, s->metalayers, &nm);   // FRAME_IDX_SIZE
+    s->nmetalayers = (uint16_t)nm;
+  }
+  if (rc >= 0 && f->len >= 25) {   // the trailer (frame_from_cframe, frame.c:1893-1910)
+    const uint8_t* t = h + f->len - 25;   // FRAME_TRAILER_MINLEN
+    const int64_t tlen = t[25 - 22 - 1] == 0xce ? be(t + 25 - 22, 4) : -1;
+    if (tlen < 25 || tlen > f->len - kHeaderMin) {
+      rc = BLOSC2_ERROR_READ_BUFFER;
+    } else {
+      const int64_t toff = f->nbytes > 0 ? f->len - tlen : f->header_len;   // get_trailer_offset
+      if (toff < BLOSC_EXTENDED_HEADER_LENGTH || toff + tlen > f->len) {
+        rc = BLOSC2_ERROR_READ_BUFFER;
+      } else {
+        int nv = 0;
+        rc = read_layers(h + toff, tlen, 2, BLOSC2_MAX_VLMETALAYERS, s->vlmetalayers, &nv);   // FRAME_TRAILER_VLMETALAYERS
+        s->nvlmetalayers = (int16_t)nv;
+      }
+    }
+  }
+  if (rc < 0) {
+    blosc2_schunk_free(s);
+    return nullptr;
+  }
+  return s;
+}
+
+std::vector<uint8_t> read_file(const char* path, int64_t offset, int* err) {
+  std::vector<uint8_t> v;
+  FILE* fp = path ? fopen(path, "rb") : nullptr;
+  if (!fp) { *err = BLOSC2_ERROR_FILE_OPEN; return v; }
+  int64_t len = -1;
+  if (fseek(fp, 0, SEEK_END) == 0) len = (int64_t)ftell(fp);
+  if (len <= offset || offset < 0 || fseek(fp, (long)offset, SEEK_SET) != 0) {
+    *err = BLOSC2_ERROR_FILE_READ;
+  } else {
+    v.resize((size_t)(len - offset));
+    if (fread(v.data(), 1, v.size(), fp) != v.size()) { *err = BLOSC2_ERROR_FILE_READ; v.clear(); }
+  }
+  fclose(fp);
+  return v;
+}
+
+}  // namespace
+
+extern "C" {
+
+// blosc2_schunk_from_buffer (blosc/schunk.c:731-750): a contiguous frame in memory.
+blosc2_schunk* blosc2_schunk_from_buffer(uint8_t* cframe, int64_t len, bool copy) {
+  if (!cframe || len < kHeaderMin || memcmp(cframe + kMagic, "b2frame", 8) != 0) return nullptr;
+  int err = 0;
+  b2h_frame* f = b2h_frame_from_buffer(cframe, len, &err);
+  if (!f) return nullptr;
+  blosc2_schunk* s = schunk_from_frame(f, copy, nullptr);
+  frame_release(f);
+  return s;
+}
+
+// blosc2_schunk_open_offset_udio (blosc/schunk.c:405-470) for the filesystem backend: the frame
+// starting `offset` bytes into the file, attached (contiguous, urlpath kept).
+blosc2_schunk* blosc2_schunk_open_offset_udio(const char* urlpath, int64_t offset, const blosc2_io* udio) {
+  if (!urlpath) return nullptr;
+  if (udio && udio->id != BLOSC2_IO_FILESYSTEM) return nullptr;   // user I/O backends: not in the engine
+  int err = 0;
+  std::vector<uint8_t> bytes = read_file(urlpath, offset, &err);
+  if (err || bytes.size() < (size_t)kHeaderMin) return nullptr;
+  b2h_frame* f = b2h_frame_from_buffer(bytes.data(), (int64_t)bytes.size(), &err);
+  if (!f) return nullptr;
+  blosc2_schunk* s = schunk_from_frame(f, false, urlpath);
+  frame_release(f);
+  return s;
+}
+blosc2_schunk* blosc2_schunk_open_udio(const char* urlpath, const blosc2_io* udio) {   // schunk.c:371-373
+  return blosc2_schunk_open_offset_udio(urlpath, 0, udio);
+}
+blosc2_schunk* blosc2_schunk_open_offset(const char* urlpath, int64_t offset) {
+  return blosc2_schunk_open_offset_udio(urlpath, offset, &BLOSC2_IO_DEFAULTS);
+}
+blosc2_schunk* blosc2_schunk_open(const char* urlpath) {
+  return blosc2_schunk_open_offset_udio(urlpath, 0, &BLOSC2_IO_DEFAULTS);
+}
+
+}  // extern "C"

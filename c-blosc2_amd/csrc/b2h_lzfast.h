@@ -53,6 +53,11 @@ constexpr int32_t kFmOpen = 0x7fffffff;     // walk exit inside a match whose en
 // position of an L run, where its match ends (e - p, kFmEoffLong: past the compare cap) in 17..31
 constexpr uint32_t kFmDMask = 0x1ffffu;
 constexpr int32_t kFmEoffLong = 0x7fff;
+// A pass that runs longer than this (s_memrealtime, 100 MHz) gives up at the next super-tile: the
+// stream is stored raw (a valid chunk either way) and the result carries kFmLateBit in `windows`.
+// Streams take well under a millisecond; the watchdog bounds every workgroup's time on the card.
+constexpr uint64_t kFmWatchdogTicks = 50000000;   // 0.5 s
+constexpr int32_t kFmLateBit = 1 << 29;
 static_assert(kFmS % 64 == 0 && kFmS / 64 % kFmWaves == 0, "whole tiles per wave");
 static_assert(kFmWalk <= 64 && kFmHist == kFmSeg, "one walking lane per map word");
 static_assert(kFmH >= 2 * kFmS + kFmAhead + kFmHist, "ring holds the window while the next one loads");
@@ -197,6 +202,18 @@ __device__ __forceinline__ void fm_flush(__amdgpu_buffer_rsrc_t r, bool al16, co
   for (int32_t y = a + 16 * lane; y < b; y += 1024)
     __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const B2H_LDS u32x4*>(oring + (y & ORM)), r, y, 0, kAux);
 }
+
+#ifdef B2H_FM_TRACE   // diagnostics build only: per-workgroup progress words in host-coherent memory
+__device__ int32_t* g_fm_trace;
+#define FM_TRACE(slot, v)                                                                                     \
+  do {                                                                                                        \
+    if (threadIdx.x == 0 && g_fm_trace)                                                                       \
+      __hip_atomic_store(&g_fm_trace[blockIdx.x * 16 + (slot)], (int32_t)(v), __ATOMIC_RELAXED,               \
+                         __HIP_MEMORY_SCOPE_SYSTEM);                                                          \
+  } while (0)
+#else
+#define FM_TRACE(slot, v)
+#endif
 
 __device__ __forceinline__ uint32_t fm_from(int32_t lo) { return lo >= 32 ? 0u : (~0u << lo); }
 __device__ __forceinline__ uint32_t fm_below(int32_t hi) { return hi >= 32 ? ~0u : ((1u << hi) - 1u); }
@@ -439,13 +456,19 @@ __device__ __forceinline__ LzPassOut fm_pass(gin_t __restrict__ in_ptr, int32_t 
   __syncthreads();   // the ring is clear
   stage(0, kFmS + kFmAhead, 0, kFmThreads);
   __syncthreads();
+  FM_TRACE(3, PROBE ? 1 : 2);
+  FM_TRACE(9, loop_end);
+  const uint64_t t_begin = __builtin_amdgcn_s_memrealtime();
   for (int32_t P = 0; P - kFmHist < loop_end; P += kFmS) {
     EPROF_T(tb0);
+    FM_TRACE(4, P);
     const int32_t W = P - kFmHist;
     const int32_t rlo = P + kFmS + kFmAhead - kFmH;   // the ring holds [rlo, P + kFmS + kFmAhead)
     windows++;
     const int32_t entry0 = __builtin_amdgcn_readfirstlane(B.sh->entry);
     const bool has_open = entry0 == kFmOpen;
+    FM_TRACE(5, entry0);
+    FM_TRACE(6, 1);
     // ---- B: the history records move to the window's front; the exchanges of [P, P + kFmS) in
     // position order (wave 0)
     if (wave == 0) {
@@ -483,6 +506,7 @@ __device__ __forceinline__ LzPassOut fm_pass(gin_t __restrict__ in_ptr, int32_t 
     }
     EPROF_T(tb1);
     EPROF_ADD(1, tb0, tb1);
+    FM_TRACE(6, 2);
     __syncthreads();
     EPROF_T(tc0);
     // ---- C: 4-byte checks and chain bits of [P, P + kFmS); every load of a wave's tiles issued
@@ -551,6 +575,7 @@ __device__ __forceinline__ LzPassOut fm_pass(gin_t __restrict__ in_ptr, int32_t 
     }
     EPROF_T(tc1);
     EPROF_ADD(2, tc0, tc1);
+    FM_TRACE(6, 3);
     __syncthreads();
     EPROF_T(td0);
     EPROF_ADD(7, tc1, td0);
@@ -582,6 +607,7 @@ __device__ __forceinline__ LzPassOut fm_pass(gin_t __restrict__ in_ptr, int32_t 
       }
       EPROF_T(td1);
       EPROF_ADD(3, td0, td1);
+      FM_TRACE(6, 4);
       // fixpoint: every lane's entry follows the exit of the lane below until nothing moves
       int32_t rounds = 0;
       for (;;) {
@@ -602,6 +628,8 @@ __device__ __forceinline__ LzPassOut fm_pass(gin_t __restrict__ in_ptr, int32_t 
       }
       EPROF_T(td2);
       EPROF_ADD(4, td1, td2);
+      FM_TRACE(6, 5);
+      FM_TRACE(8, rounds);
       FM_CNT(PROBE ? 4 : 0, rounds);
       FM_CNT(PROBE ? 5 : 1, 1);
       const uint32_t LITS = VIS & ~MS;
@@ -794,15 +822,27 @@ __device__ __forceinline__ LzPassOut fm_pass(gin_t __restrict__ in_ptr, int32_t 
       if (lane == 0 && stop) B.sh->stop = stop;
       EPROF_T(td4);
       EPROF_ADD(6, td3, td4);
+      FM_TRACE(7, o_out);
+      FM_TRACE(6, 6);
+    }
+    FM_TRACE(6, 7);
+    // the watchdog: one thread decides, every wave reads the verdict after the barrier
+    if (threadIdx.x == 0 && __builtin_amdgcn_s_memrealtime() - t_begin > kFmWatchdogTicks) {
+      B.sh->stop = PROBE ? 2 : 1;
+      B.sh->fail = kFmLateBit;
+      FM_TRACE(13, P);
+      FM_TRACE(14, loop_end);
     }
     __syncthreads();
     const int32_t stop = __builtin_amdgcn_readfirstlane(B.sh->stop);
     const int32_t ent = __builtin_amdgcn_readfirstlane(B.sh->entry);
+    FM_TRACE(10, windows);
     if (stop || (ent != kFmOpen && ent >= loop_end)) break;
   }
   if (wave == 0) {
     EPROF_FLUSH;
   }
+  FM_TRACE(6, 8);
   LzPassOut r;
   const int32_t stop = __builtin_amdgcn_readfirstlane(B.sh->stop);
   r.fail = stop == 1;
@@ -811,7 +851,7 @@ __device__ __forceinline__ LzPassOut fm_pass(gin_t __restrict__ in_ptr, int32_t 
   r.pos = __builtin_amdgcn_readfirstlane(B.sh->pos);
   r.o = __builtin_amdgcn_readfirstlane(B.sh->o);
   r.peak = __builtin_amdgcn_readfirstlane(B.sh->peak);
-  r.windows = windows;
+  r.windows = windows | (__builtin_amdgcn_readfirstlane(B.sh->fail) & kFmLateBit);
   if (!PROBE) {
     if (!r.fail && wave == 0) {
       // tail literals [pos, bound] (blosc/blosclz.c:595-604), then the last run's header

@@ -426,10 +426,12 @@ BLOSC_EXPORT int blosc2_getitem_bytes_ctx(blosc2_context *context, const void *s
 /* ---- super-chunks (include/blosc2.h:1740-2362): the container the reference's callers reach the
  * chunk engine through (blosc/schunk.c).  Structs ABI-identical; the engine keeps IN-MEMORY, SPARSE
  * super-chunks (storage.contiguous == false, urlpath == NULL): chunks are malloc'd host buffers
- * indexed by schunk->data, exactly as the reference's frame-less schunk.  Frame-backed storage
- * (contiguous frames, files, directories) is outside the device engine (DESIGN.md §7;
- * the read side of contiguous frames is include/b2h.h b2h_frame_*): blosc2_schunk_new returns NULL
- * for it.  The device-batch forms (b2h_schunk_append_device / b2h_schunk_decompress_device in
+ * indexed by schunk->data, exactly as the reference's frame-less schunk.  New frame-backed storage
+ * (contiguous frames, files, directories) is outside the device engine:
+ * blosc2_schunk_new returns NULL for it.  Existing contiguous frames OPEN through the reference's
+ * entry points (blosc2_schunk_open / _from_buffer below): their chunks are read into an in-memory
+ * super-chunk with the frame's header fields, counters and (vl)metalayers; the offsets index is
+ * decoded on the device (include/b2h.h b2h_frame_*).  The device-batch forms (b2h_schunk_append_device / b2h_schunk_decompress_device in
  * include/b2h.h) run one engine launch over many chunks of a super-chunk. ---- */
 enum {   /* include/blosc2.h:994-1005 */
   BLOSC2_IO_FILESYSTEM = 0,
@@ -520,6 +522,17 @@ typedef struct blosc2_schunk {
 BLOSC_EXPORT blosc2_schunk *blosc2_schunk_new(blosc2_storage *storage);
 /* include/blosc2.h:2088 (blosc/schunk.c:679-729) */
 BLOSC_EXPORT int blosc2_schunk_free(blosc2_schunk *schunk);
+/* include/blosc2.h:1934 (blosc/schunk.c:731-750, frame_to_schunk frame.c:2941-3245): a contiguous
+ * frame in memory; `copy` false gives the frame-attached flavour (storage.contiguous, the header's
+ * cbytes and blocksize), true the copy (sum of the chunks' cbytes, their common blocksize).  The
+ * chunks are host copies either way: writes to the handle do not reach the frame. */
+BLOSC_EXPORT blosc2_schunk *blosc2_schunk_from_buffer(uint8_t *cframe, int64_t len, bool copy);
+/* include/blosc2.h:2008, 2019, 2030, 2043 (blosc/schunk.c:366-470): a contiguous frame file (at
+ * `offset`), filesystem backend only (another udio->id returns NULL). */
+BLOSC_EXPORT blosc2_schunk *blosc2_schunk_open(const char *urlpath);
+BLOSC_EXPORT blosc2_schunk *blosc2_schunk_open_offset(const char *urlpath, int64_t offset);
+BLOSC_EXPORT blosc2_schunk *blosc2_schunk_open_udio(const char *urlpath, const blosc2_io *udio);
+BLOSC_EXPORT blosc2_schunk *blosc2_schunk_open_offset_udio(const char *urlpath, int64_t offset, const blosc2_io *udio);
 /* include/blosc2.h:2101, 2115, 2129, 2140 (blosc/schunk.c:975-1457) */
 BLOSC_EXPORT int64_t blosc2_schunk_append_chunk(blosc2_schunk *schunk, uint8_t *chunk, bool copy);
 BLOSC_EXPORT int64_t blosc2_schunk_update_chunk(blosc2_schunk *schunk, int64_t nchunk, uint8_t *chunk, bool copy);
