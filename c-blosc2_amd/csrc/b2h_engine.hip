@@ -210,42 +210,62 @@ static int resident_slots(const void* fn, size_t lds, int block = 64) {
   return slots;
 }
 
-// Per-phase HIP events of every batch call since timing was enabled (a pool of event pairs,
-// reused from the start by each enable_timing(true)).  Recording never waits on the host: the
-// elapsed times are read only when asked for (last_times / mean_times), after the timed loop.
+// Per-phase HIP events of the batch calls since timing was enabled: a ring of at most kEvRing
+// event pairs per phase (the oldest reused once full; mean over the ring), guarded by one mutex
+// (contexts on several host threads time into the same rings).  Recording never waits on the
+// host: the elapsed times are read only when asked for (last_times / mean_times).
+static std::mutex g_ev_mu;
+constexpr size_t kEvRing = 256;
 struct EvPair {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> rec;
-  size_t used = 0;
+  size_t n = 0;   // pairs recorded since the reset (slot = n % kEvRing)
   bool open = false;
   void start(hipStream_t s) {
     if (!g_timing) return;
-    if (used == rec.size()) {
+    std::lock_guard<std::mutex> g(g_ev_mu);
+    const size_t k = n % kEvRing;
+    if (k == rec.size()) {
       hipEvent_t a = nullptr, b = nullptr;
-      if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+      if (hipEventCreate(&a) != hipSuccess) return;
+      if (hipEventCreate(&b) != hipSuccess) {
+        (void)hipEventDestroy(a);
+        return;
+      }
       rec.push_back({a, b});
     }
-    (void)hipEventRecord(rec[used].first, s);
+    (void)hipEventRecord(rec[k].first, s);
     open = true;
   }
   void stop(hipStream_t s) {
-    if (!g_timing || !open) return;
-    (void)hipEventRecord(rec[used].second, s);
-    used++;
+    if (!g_timing) return;
+    std::lock_guard<std::mutex> g(g_ev_mu);
+    if (!open) return;
+    (void)hipEventRecord(rec[n % kEvRing].second, s);
+    n++;
     open = false;
   }
-  float elapsed(size_t i) {
+  float elapsed(size_t k) {
     float t = 0.f;
-    (void)hipEventSynchronize(rec[i].second);
-    (void)hipEventElapsedTime(&t, rec[i].first, rec[i].second);
+    (void)hipEventSynchronize(rec[k].second);
+    (void)hipEventElapsedTime(&t, rec[k].first, rec[k].second);
     return t;
   }
-  float last() { return used ? elapsed(used - 1) : 0.f; }
-  float mean() {
-    double t = 0;
-    for (size_t i = 0; i < used; i++) t += elapsed(i);
-    return used ? (float)(t / (double)used) : 0.f;
+  float last() {
+    std::lock_guard<std::mutex> g(g_ev_mu);
+    return n ? elapsed((n - 1) % kEvRing) : 0.f;
   }
-  void reset() { used = 0; open = false; }
+  float mean() {
+    std::lock_guard<std::mutex> g(g_ev_mu);
+    const size_t m = std::min(n, kEvRing);
+    double t = 0;
+    for (size_t k = 0; k < m; k++) t += elapsed(k);
+    return m ? (float)(t / (double)m) : 0.f;
+  }
+  void reset() {
+    std::lock_guard<std::mutex> g(g_ev_mu);
+    n = 0;
+    open = false;
+  }
 };
 static EvPair ev_filter, ev_encode, ev_final, ev_decode, ev_unfilter;
 void enable_timing(bool on) {

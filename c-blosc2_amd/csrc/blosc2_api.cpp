@@ -946,6 +946,10 @@ int ctx_compress_device(blosc2_context* ctx, const uint8_t* d_src, const int32_t
 // packed on the device (pack_chunks) and brought back in ONE copy through pinned memory, then split
 // into malloc'd chunks of exactly cbytes bytes (the shrunk chunk blosc2_schunk_append_chunk keeps,
 // blosc/schunk.c:1055-1058).  On failure nothing is returned (every chunk produced so far is freed).
+// The context's sticky blocksize advances over all n chunks here; when the caller's append of
+// chunk i then fails (b2h_schunk_append_device), the context's blocksize is the one after chunk
+// n-1, not after chunk i as in the serial walk: after a failed device append the context state is
+// unspecified (include/b2h.h).
 int ctx_append_device(blosc2_context* ctx, const uint8_t* d_src, const int32_t* nbytes, int32_t n,
                       int64_t src_stride, uint8_t** chunks_out) {
   if (!ctx || (n > 0 && (!nbytes || !d_src || !chunks_out))) return BLOSC2_ERROR_NULL_POINTER;
@@ -1077,9 +1081,15 @@ int ctx_decompress_device(blosc2_context* ctx, const uint8_t* const* chunks, int
       h_ss[k] = cb[i];
       h_ds[k] = dst_cap;
     }
+    // every early return below drains the stream first: the copies read the pinned staging
+    // buffer, which the next call on this context rewrites (or frees when it grows)
+    auto drained = [&](int rc) {
+      (void)hipStreamSynchronize(d.stream);
+      return rc;
+    };
     if (hipMemcpyAsync(d.in.p, d.host.p, (size_t)total_c, hipMemcpyHostToDevice, d.stream) != hipSuccess ||
         hipMemcpyAsync(sm, h_s, tbytes, hipMemcpyHostToDevice, d.stream) != hipSuccess)
-      return BLOSC2_ERROR_FAILURE;
+      return drained(BLOSC2_ERROR_FAILURE);
     const uint8_t* const* d_s = reinterpret_cast<const uint8_t* const*>(sm);
     uint8_t* const* d_o = reinterpret_cast<uint8_t* const*>(sm + 8 * (size_t)m);
     const int32_t* d_ss = reinterpret_cast<const int32_t*>(sm + 16 * (size_t)m);
@@ -1088,7 +1098,7 @@ int ctx_decompress_device(blosc2_context* ctx, const uint8_t* const* chunks, int
     int rc = b2h::decompress_batch(d_s, d_ss, d_o, d_ds, m, total_d, d_st, nullptr, d.stream, d.ws, total_c, 0);
     if (rc < 0) {
       TRACE_ERROR("device decompression failed: %s", b2h::last_error());
-      return rc;
+      return drained(rc);
     }
     std::vector<int32_t> st((size_t)m);
     if (hipMemcpyAsync(st.data(), d_st, 4 * (size_t)m, hipMemcpyDeviceToHost, d.stream) != hipSuccess ||

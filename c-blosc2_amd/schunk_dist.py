@@ -65,21 +65,17 @@ def _agree(ok, group):
     return bool(flag.item())
 
 
-_P2P_READY = set()
-
-
 def _p2p(sends, recvs, group):
     """Grouped point-to-point exchange: sends = [(tensor, dst)], recvs = [(tensor, src)].  Empty
     tensors are skipped (both sides know every size).  Receives land in the given tensors.
 
-    Every rank of the group calls this (possibly with nothing to exchange: an empty shard), so the
-    first call on a group runs a barrier first -- a batch_isend_irecv that is a group's first
-    collective must be joined by all its ranks (torch.distributed), and a rank with nothing to
-    send or receive makes no such call."""
-    key = id(group) if group is not None else None
-    if key not in _P2P_READY:
-        dist.barrier(group=group)
-        _P2P_READY.add(key)
+    Every rank of the group calls this (possibly with nothing to exchange: an empty shard), so
+    every call starts with a barrier -- a batch_isend_irecv that is a group's first collective must
+    be joined by all its ranks (torch.distributed), and a rank with nothing to send or receive makes
+    no such call.  (A per-group "first call done" cache keyed by id(group) would go stale when a
+    process group is destroyed and a new one reuses the id; one barrier per exchange is cheap
+    next to the chunk payloads it precedes.)"""
+    dist.barrier(group=group)
     ops, back = [], []
     for t, peer in sends:
         if t.numel():

@@ -127,7 +127,9 @@ BLOSC_EXPORT int b2h_frame_get_sparse_buffer(b2h_frame *frame, int64_t ncoords, 
  *
  * append: chunk i = d_src + i*src_stride (device), nbytes[i] bytes (HOST array), appended in order.
  *   Returns the new nchunks or BLOSC2_ERROR_*.  Pipelines with user-registered filters / codecs
- *   run the serial appends (through host memory).
+ *   run the serial appends (through host memory).  On an error return the chunks appended before
+ *   the failing one stay, and the cctx's sticky blocksize is unspecified (it has advanced over all
+ *   n chunks, the serial walk's only up to the failing one).
  * decompress: chunks [nchunk, nchunk + n) into d_dst + i*dst_stride (device, capacity dst_capacity);
  *   status[i] (HOST, optional) = blosc2_schunk_decompress_chunk's return for chunk nchunk + i.
  *   Returns 0 or the first chunk error; BLOSC2_ERROR_INVALID_PARAM for a range outside the schunk.
