@@ -573,35 +573,39 @@ void k_encode_fast(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restric
                    const int32_t* __restrict__ porder) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const FmBufs B = fm_bufs<POS>((B2H_LDS uint8_t*)smem);
-  for (;;) {
+  // the pull is the loop's last statement and its broadcast result the loop's only exit test: a
+  // loop that holds barriers with lane-0 code before a mid-body exit can be structurized into an
+  // exec-masked nest whose waves meet different barriers (see encode_stream_fast)
+  auto pull = [&]() {
     if (threadIdx.x == 0) B.sh->pull = atomicAdd(next, 1);
     __syncthreads();
-    const int32_t i = __builtin_amdgcn_readfirstlane(B.sh->pull);
+    const int32_t v = __builtin_amdgcn_readfirstlane(B.sh->pull);
     __syncthreads();
-    if (i >= nstreams_total) return;
+    return v;
+  };
+  for (int32_t i = pull(); i < nstreams_total; i = pull()) {
     const int32_t s = __builtin_amdgcn_readfirstlane(pull_to_stream(g, porder, g.front, i, nstreams_total));
     const int32_t c = s / g.nsc, l = s - c * g.nsc;
     int32_t off, len, blk;
     stream_locate(g, l, &off, &len, &blk);
-    if (!FM_OK(s >= 0 && s < nstreams_total && off >= 0 && len >= 0 && off + len <= g.wstride, 8, s, off, len)) continue;
     gin_t in = (gin_t)(filt + (int64_t)c * g.wstride + off);
     gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
-    FM_TRACE(0, s);
-    FM_TRACE(1, len);
-    FM_TRACE(2, off);
-    FM_TRACE(11, i);
+    FM_TRACE_S(0, s);
+    FM_TRACE_S(1, len);
+    FM_TRACE_S(2, off);
+    FM_TRACE_S(11, i);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
     StreamResult r = encode_stream_fast<POS>(in, len, g.clevel, out, B, tablog, g.overhead == kHdrExt);
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
     if (threadIdx.x == 0) res[s] = r;
-    FM_TRACE(12, r.size);
-    FM_TRACE(6, 9);
+    FM_TRACE_S(12, r.size);
+    FM_TRACE_S(6, 9);
   }
 }
 
-#ifdef B2H_FM_TRACE
+#if defined(B2H_FM_TRACE) || defined(B2H_FM_TRACE_LITE)
 extern "C" __attribute__((visibility("default"))) void* b2h_fm_trace_alloc(int32_t words) {
   void* h = nullptr;
   if (hipHostMalloc(&h, (size_t)words * 4, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return nullptr;

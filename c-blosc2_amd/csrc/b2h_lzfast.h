@@ -203,14 +203,20 @@ __device__ __forceinline__ void fm_flush(__amdgpu_buffer_rsrc_t r, bool al16, co
     __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const B2H_LDS u32x4*>(oring + (y & ORM)), r, y, 0, kAux);
 }
 
-#ifdef B2H_FM_TRACE   // diagnostics build only: per-workgroup progress words in host-coherent memory
+#if defined(B2H_FM_TRACE) || defined(B2H_FM_TRACE_LITE)   // diagnostics builds only: per-workgroup progress
+                                                          // words in host-coherent memory
 __device__ int32_t* g_fm_trace;
-#define FM_TRACE(slot, v)                                                                                     \
+#define FM_TRACE_S(slot, v)                                                                                   \
   do {                                                                                                        \
     if (threadIdx.x == 0 && g_fm_trace)                                                                       \
       __hip_atomic_store(&g_fm_trace[blockIdx.x * 16 + (slot)], (int32_t)(v), __ATOMIC_RELAXED,               \
                          __HIP_MEMORY_SCOPE_SYSTEM);                                                          \
   } while (0)
+#else
+#define FM_TRACE_S(slot, v)
+#endif
+#ifdef B2H_FM_TRACE   // the pass-internal points (the lite build keeps only the stream-level ones)
+#define FM_TRACE(slot, v) FM_TRACE_S(slot, v)
 #else
 #define FM_TRACE(slot, v)
 #endif
@@ -459,7 +465,9 @@ __device__ __forceinline__ LzPassOut fm_pass(gin_t __restrict__ in_ptr, int32_t 
   FM_TRACE(3, PROBE ? 1 : 2);
   FM_TRACE(9, loop_end);
   const uint64_t t_begin = __builtin_amdgcn_s_memrealtime();
-  for (int32_t P = 0; P - kFmHist < loop_end; P += kFmS) {
+  // one exit, decided last from broadcast values (see encode_stream_fast on uniform branches)
+  bool more = -kFmHist < loop_end;
+  for (int32_t P = 0; more; P += kFmS) {
     EPROF_T(tb0);
     FM_TRACE(4, P);
     const int32_t W = P - kFmHist;
@@ -837,7 +845,7 @@ __device__ __forceinline__ LzPassOut fm_pass(gin_t __restrict__ in_ptr, int32_t 
     const int32_t stop = __builtin_amdgcn_readfirstlane(B.sh->stop);
     const int32_t ent = __builtin_amdgcn_readfirstlane(B.sh->entry);
     FM_TRACE(10, windows);
-    if (stop || (ent != kFmOpen && ent >= loop_end)) break;
+    more = !stop && (ent == kFmOpen || ent < loop_end) && P + kFmS - kFmHist < loop_end;
   }
   if (wave == 0) {
     EPROF_FLUSH;
@@ -936,7 +944,10 @@ __device__ __forceinline__ StreamResult encode_stream_fast(gin_t __restrict__ in
     else if (wave == 1) half_run = wave_is_run_from(in, h, n, in[0]);
     if (wave < 2 && lane_id() == 0) B.sh->decide[wave] = half_run ? 1 : 0;
     __syncthreads();
-    const bool run = B.sh->decide[0] && B.sh->decide[1];
+    // readfirstlane: a branch the compiler must see as uniform (a divergent-looking branch around the
+    // passes' barriers gets structurized into exec-masked paths that run s_barrier a different
+    // number of times per wave -- the stream loop then hangs or reads a stale stream index)
+    const bool run = (__builtin_amdgcn_readfirstlane(B.sh->decide[0]) & __builtin_amdgcn_readfirstlane(B.sh->decide[1])) != 0;
     __syncthreads();   // both read before the next write
     if (run) {
       res.size = in[0];
@@ -950,13 +961,17 @@ __device__ __forceinline__ StreamResult encode_stream_fast(gin_t __restrict__ in
   if (clevel < 2) maxlen /= 8;
   else if (clevel < 4) maxlen /= 4;
   else if (clevel < 7) maxlen /= 2;
+  FM_TRACE_S(6, 20);
   const LzPassOut pr = fm_pass<true, POS, WT>(in + (n - maxlen), maxlen, hashlog, tl, out, 0, B, clevel);
+  FM_TRACE_S(6, 21);
   res.windows = pr.windows;
   const double ratio = (double)pr.pos / (double)pr.o;
   const double thr = clevel == 1 ? 2.0 : clevel == 2 ? 1.5 : clevel <= 6 ? 1.2 : clevel == 7 ? 1.15 : clevel == 8 ? 1.1 : 1.0;
   const bool go = !(pr.early || (!pr.sure && ratio < thr) || n < 66);
   if (!go) return res;
+  FM_TRACE_S(6, 22);
   const LzPassOut em = fm_pass<false, POS, WT>(in, n, hashlog, tl, out, n, B, clevel);
+  FM_TRACE_S(6, 23);
   res.windows += em.windows;
   if (em.fail) return res;
   res.kind = kStreamLz;
