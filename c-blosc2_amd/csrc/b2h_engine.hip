@@ -558,28 +558,31 @@ __global__ __launch_bounds__(64 * (NLDS + NGLB)) void k_encode(EncArgs args, POS
 }
 
 // ------------------------------------------------------------------ BloscLZ fast mode ----
-// One stream per workgroup of four waves (b2h_lzfast.h: exchanges, checks, segment-parallel
-// walk, emission); persistent, pulling streams like k_encode.
+// One stream per workgroup of two waves: wave 0 matches, wave 1 parses (b2h_lzfast.h);
+// persistent, pulling streams like k_encode.  LDS per workgroup: table + output ring + hand-over
+// slots.
 __host__ __device__ constexpr size_t fast_lds(size_t pos_bytes, int tablog) {
-  return pos_bytes == 2 ? fm_lds_bytes<uint16_t>(tablog) : fm_lds_bytes<uint32_t>(tablog);
+  return (pos_bytes << tablog) + kOutRing + ((sizeof(FastShared) + 15) & ~size_t(15));
 }
 template <typename POS>
-#ifndef B2H_FM_WPE
-#define B2H_FM_WPE 4   // waves per SIMD the fast encoder is compiled for (diagnostic builds vary it)
-#endif
-__global__ __launch_bounds__(kFmThreads) __attribute__((amdgpu_waves_per_eu(B2H_FM_WPE, 8)))   // <= 128 VGPRs
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4, 8)))   // <= 128 VGPRs: 16 waves per CU
 void k_encode_fast(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
                    StreamResult* __restrict__ res, int32_t nstreams_total, int32_t* __restrict__ next, int tablog,
                    const int32_t* __restrict__ porder) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const FmBufs B = fm_bufs<POS>((B2H_LDS uint8_t*)smem);
+  B2H_LDS uint8_t* tab = (B2H_LDS uint8_t*)smem;
+  B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + (sizeof(POS) << tablog));
+  B2H_LDS FastShared* sh = (B2H_LDS FastShared*)(smem + (sizeof(POS) << tablog) + kOutRing);
+  const bool matcher = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
+  if (!matcher) __builtin_amdgcn_s_setprio(2);   // the parser issues first (see k_encode_fast_fused)
   // the pull is the loop's last statement and its broadcast result the loop's only exit test: a
   // loop that holds barriers with lane-0 code before a mid-body exit can be structurized into an
-  // exec-masked nest whose waves meet different barriers (see encode_stream_fast)
+  // exec-masked nest whose waves meet different barriers (seen in round 4: a hang, or a stale
+  // stream index and an illegal address)
   auto pull = [&]() {
-    if (threadIdx.x == 0) B.sh->pull = atomicAdd(next, 1);
+    if (threadIdx.x == 0) sh->pull = atomicAdd(next, 1);
     __syncthreads();
-    const int32_t v = __builtin_amdgcn_readfirstlane(B.sh->pull);
+    const int32_t v = __builtin_amdgcn_readfirstlane(sh->pull);
     __syncthreads();
     return v;
   };
@@ -590,40 +593,15 @@ void k_encode_fast(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restric
     stream_locate(g, l, &off, &len, &blk);
     gin_t in = (gin_t)(filt + (int64_t)c * g.wstride + off);
     gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
-    FM_TRACE_S(0, s);
-    FM_TRACE_S(1, len);
-    FM_TRACE_S(2, off);
-    FM_TRACE_S(11, i);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
-    StreamResult r = encode_stream_fast<POS>(in, len, g.clevel, out, B, tablog, g.overhead == kHdrExt);
+    StreamResult r = encode_stream_fast<POS>(in, len, g.clevel, out, tab, tablog, oring, sh, g.overhead == kHdrExt,
+                                             matcher);
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
-    if (threadIdx.x == 0) res[s] = r;
-    FM_TRACE_S(12, r.size);
-    FM_TRACE_S(6, 9);
+    if (!matcher && lane_id() == 0) res[s] = r;
   }
 }
-
-#if defined(B2H_FM_TRACE) || defined(B2H_FM_TRACE_LITE)
-extern "C" __attribute__((visibility("default"))) void* b2h_fm_trace_alloc(int32_t words) {
-  void* h = nullptr;
-  if (hipHostMalloc(&h, (size_t)words * 4, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return nullptr;
-  memset(h, 0xff, (size_t)words * 4);
-  void* d = nullptr;
-  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) return nullptr;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_fm_trace), &d, sizeof d) != hipSuccess) return nullptr;
-  return h;
-}
-#endif
-
-#ifdef B2H_FM_CHECK
-extern "C" __attribute__((visibility("default"))) int b2h_fm_debug(int64_t* out) {
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fm_bad), 8 * sizeof(int64_t)) != hipSuccess) return -1;
-  return 0;
-}
-#endif
 
 // BloscLZ encoder mode: exact (default, byte-identical to the reference) or fast (round-trip
 // identical, same grammar and decisions, parse-independent candidates).  Process-wide; also
@@ -662,11 +640,9 @@ static int launch_encode_fast_t(Workspace* ws, const CGeom& g, const uint8_t* fi
     HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  static const int grid_env = [] { const char* e = getenv("B2H_FAST_GRID"); return e ? atoi(e) : 0; }();   // debug
-  const int slots = grid_env > 0 ? grid_env : resident_slots(fn, lds, kFmThreads);
+  const int slots = resident_slots(fn, lds, 128);
   const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(ntot, slots));
-  k_encode_fast<POS><<<grid, kFmThreads, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog,
-                                                    porder);
+  k_encode_fast<POS><<<grid, 128, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog, porder);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1473,15 +1449,15 @@ __host__ __device__ constexpr size_t fused_lds(size_t pos_bytes, int tablog) {
 #undef FUSE_TRACE_PTR
 #define FUSE_TRACE_PTR lds_uniform(&A->f.trace)
 template <typename POS>
-__global__ __launch_bounds__(kFmThreads) __attribute__((amdgpu_waves_per_eu(B2H_FM_WPE, 8)))   // as k_encode_fast
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4, 8)))   // as k_encode_fast
 void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint8_t* __restrict__ sbuf_arg,
                          StreamResult* __restrict__ res_arg, int32_t nstreams_total_arg, int32_t* __restrict__ next_arg,
                          int tablog_arg, const int32_t* __restrict__ porder_arg, EncFuse f_arg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tablog0 = tablog_arg;
-  const FmBufs Bf = fm_bufs<POS>((B2H_LDS uint8_t*)smem);
-  B2H_LDS uint8_t* tab = Bf.tab;
-  B2H_LDS FmShared* sh = Bf.sh;
+  B2H_LDS uint8_t* tab = (B2H_LDS uint8_t*)smem;
+  B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + (sizeof(POS) << tablog0));
+  B2H_LDS FastShared* sh = (B2H_LDS FastShared*)(smem + (sizeof(POS) << tablog0) + kOutRing);
   B2H_LDS FusedArgs* A = (B2H_LDS FusedArgs*)(smem + fast_lds(sizeof(POS), tablog0));
   if (threadIdx.x == 0) {
     lds_store(&A->g, g_arg);
@@ -1495,9 +1471,10 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
     A->tablog = tablog_arg;
   }
   __syncthreads();
-  // wave priority (B2H_FUSE bit 64, default): wave 0 -- the exchanges and the walk, the stream's
-  // latency chain -- issues ahead of the other waves sharing its SIMD
-  if ((lds_uniform(&A->f.mode_bits) & 64) && threadIdx.x < 64) __builtin_amdgcn_s_setprio(2);
+  const bool matcher = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
+  // wave priority (B2H_FUSE bit 64, default): the parser -- the tile's latency chain -- issues
+  // ahead of the matchers sharing its SIMD (T encode 18.0 -> 17.6 ms; the matcher first: 19.3)
+  if ((lds_uniform(&A->f.mode_bits) & 64) && !matcher) __builtin_amdgcn_s_setprio(2);
   // lane 0 of the workgroup computes v, everyone gets it
   auto bcast = [&](int32_t v) -> int32_t {
     if (threadIdx.x == 0) sh->bcast = v;
@@ -1530,7 +1507,7 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
     const int32_t c = v - 1;
     if (__builtin_amdgcn_readfirstlane(f2.mode[c]) != 0) return;
     uint8_t* d = f2.dst + (int64_t)c * g2.dst_stride;
-    const int32_t wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    const int32_t wv = threadIdx.x >> 6;
     for (int32_t l = j0; l < min(j0 + kFuseSpi, g2.nsc); l++) {
       const int32_t s = c * g2.nsc + l;
       Place pl;
@@ -1546,7 +1523,7 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
       }
       if (pl.csize <= 0) continue;
       const uint8_t* src = (pl.csize == len ? filt : sbuf) + (int64_t)c * g2.wstride + off;
-      const int32_t q = ((pl.csize + nwv - 1) / nwv + 15) & ~15;
+      const int32_t q = ((pl.csize + 1) / 2 + 15) & ~15;
       const int32_t a = min(pl.csize, wv * q), b = min(pl.csize, a + q);
       if (b > a) {
         if ((f2.mode_bits & 32) || !aligned16(src + a)) wave_copy((gout_t)(d + pl.off + a), (gin_t)(src + a), b - a);
@@ -1639,10 +1616,10 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
     FUSE_TRACE(6, s);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
-    StreamResult r = encode_stream_fast<POS, true>(in, len, clevel, out, Bf, tablog, runs);
+    StreamResult r = encode_stream_fast<POS, true>(in, len, clevel, out, tab, tablog, oring, sh, runs, matcher);
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
-    if (threadIdx.x == 0) {
+    if (!matcher && lane_id() == 0) {
       int32_t* fin = lds_uniform(&A->f.fin);
       lds_uniform(&A->res)[s] = r;
       st_agent(fin + 3 * s, r.kind);
@@ -1781,7 +1758,7 @@ static int launch_encode_fast_fused_t(Workspace* ws, const CGeom& g, const uint8
     HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  const int slots = resident_slots(fn, lds, kFmThreads);
+  const int slots = resident_slots(fn, lds, 128);
   const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(ntot, fuse_grid_cap(slots)));
   if (fuse_prepare(ws, g, ntot, f, st)) return E_MEMORY;
   static int32_t* trace = nullptr;
@@ -1789,7 +1766,7 @@ static int launch_encode_fast_fused_t(Workspace* ws, const CGeom& g, const uint8
   if (tr && !trace) HIPCHK(hipHostMalloc(&trace, 4 << 20, hipHostMallocCoherent));
   f.trace = tr ? trace : nullptr;
   if (tr) memset(trace, 0xff, 4 * (size_t)grid);
-  k_encode_fast_fused<POS><<<grid, kFmThreads, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog,
+  k_encode_fast_fused<POS><<<grid, 128, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog,
                                                    porder, f);
   HIPCHK(hipGetLastError());
   if (tr) {   // debug watchdog: report where the workgroups are if the launch has not ended after 5 s

@@ -541,8 +541,9 @@ namespace {
 
 // One metalayer index (msgpack): be16 idx_size, 0xde map16 (be16 count), then per layer a fixstr
 // name and 0xd2 + be32 offset of its content (0xc6 bin32: be32 length, bytes), offsets from `base`.
-// Header metalayers: get_meta_from_header (blosc/frame.c:2388-2500), index at FRAME_IDX_SIZE (89);
-// trailer vlmetalayers: get_vlmeta_from_trailer (2591-2720), index at FRAME_TRAILER_VLMETALAYERS + 2.
+// `idx` is where idx_size sits: FRAME_IDX_SIZE (89) for the header metalayers (get_meta_from_header,
+// blosc/frame.c:2388-2500), FRAME_TRAILER_VLMETALAYERS + 2 (4) for the trailer's vlmetalayers
+// (get_vlmeta_from_trailer, 2591-2720).
 int read_layers(const uint8_t* base, int64_t len, int64_t idx, int max, blosc2_metalayer** out, int* count) {
   int64_t pos = idx + 2 + 1 + 2;
   if (len < pos) return BLOSC2_ERROR_READ_BUFFER;
@@ -667,7 +668,7 @@ blosc2_schunk* schunk_from_frame(b2h_frame* f, bool copy, const char* urlpath) {
         rc = BLOSC2_ERROR_READ_BUFFER;
       } else {
         int nv = 0;
-        rc = read_layers(h + toff, tlen, 2, BLOSC2_MAX_VLMETALAYERS, s->vlmetalayers, &nv);   // FRAME_TRAILER_VLMETALAYERS
+        rc = read_layers(h + toff, tlen, 4, BLOSC2_MAX_VLMETALAYERS, s->vlmetalayers, &nv);   // FRAME_TRAILER_VLMETALAYERS + 2
         s->nvlmetalayers = (int16_t)nv;
       }
     }

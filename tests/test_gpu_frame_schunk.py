@@ -87,7 +87,9 @@ def _same(a, b):
 def _from_buffer(L, buf, copy):
     p = L.blosc2_schunk_from_buffer(buf.ctypes.data, buf.nbytes, copy)
     assert p, "blosc2_schunk_from_buffer returned NULL"
-    return B.SChunk.wrap(p, L)
+    sc = B.SChunk.wrap(p, L)
+    sc._keep = buf   # a frame-attached super-chunk reads the caller's buffer for its lifetime
+    return sc
 
 
 @pytest.mark.parametrize("copy", [False, True], ids=["attached", "copy"])

@@ -278,20 +278,24 @@ def test_device_batches_survive_fused_timeout(lzmode, monkeypatch):
     want = run()
     monkeypatch.setenv("B2H_FUSE_SIMULATE_TIMEOUT", "1")
     got = run()
+    b = None
     try:
-        _assert_same(got, want)
         if lzmode == 0:
             from b2ctypes import cparams as rcp, dparams as rdp
             b = B.SChunk(rcp(**kw), rdp(), L=_ref())
-            try:
-                off = 0
-                for n in sizes:
-                    b.append_buffer(data[off:off + n])
-                    off += n
-                assert b.set_slice(lo, hi, new) == 0
-                _assert_same(got, b)
-            finally:
-                b.free()
+            off = 0
+            for n in sizes:
+                b.append_buffer(data[off:off + n])
+                off += n
+            assert b.set_slice(lo, hi, new) == 0
+            # counters before any chunk is fetched (blosc2_schunk_get_chunk moves current_nchunk)
+            assert got.counters() == b.counters(), (got.counters(), b.counters())
+        _assert_same(got, want)
+        if b is not None:
+            for i, (u, v) in enumerate(zip(_chunks(got), _chunks(b))):
+                assert np.array_equal(u, v), i
     finally:
+        if b is not None:
+            b.free()
         got.free()
         want.free()

@@ -1,7 +1,7 @@
-// Fast-mode encoder micro-benchmark (diagnostics only): encode one stream per two-wave workgroup
-// with the product encode_stream_fast (matcher + parser), many workgroups, and report cycles per
-// stream and the parser's per-phase sums.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../c-blosc2_amd/csrc fast_micro.hip -o fast_micro
+// Fast-mode encoder micro-benchmark (diagnostics only): encode one stream per four-wave workgroup
+// with the product encode_stream_fast, many workgroups, and report cycles per stream and wave 0's
+// per-phase sums (b2h_lzfast.h EPROF points).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I. -I../../c-blosc2_amd/csrc fm2_micro.hip -o fm2_micro
 //   ./fast_micro plane.bin [clevel] [tablog]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -11,23 +11,19 @@
 #define B2H_ENC_PROF 1
 #ifndef FM_POS
 #define FM_POS uint16_t
-#define FM_POSB 2
 #endif
-#include "b2h_lzfast.h"
+#include "b2h_lzfast_fm2.h"
 using namespace b2h;
 
-__global__ __launch_bounds__(128) void k_enc(const uint8_t* in, int32_t n, int clevel, int tablog, uint8_t* out,
-                                             int64_t* cycles, StreamResult* res) {
+__global__ __launch_bounds__(kFmThreads) __attribute__((amdgpu_waves_per_eu(4, 8)))
+void k_enc(const uint8_t* in, int32_t n, int clevel, int tablog, uint8_t* out, int64_t* cycles, StreamResult* res) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  B2H_LDS uint8_t* tab = (B2H_LDS uint8_t*)smem;
-  B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + ((size_t)FM_POSB << tablog));
-  B2H_LDS FastShared* sh = (B2H_LDS FastShared*)(smem + ((size_t)FM_POSB << tablog) + kOutRing);
-  const bool matcher = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
+  const FmBufs B = fm_bufs<FM_POS>((B2H_LDS uint8_t*)smem);
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
-  StreamResult r = encode_stream_fast<FM_POS>((gin_t)in, n, clevel, (gout_t)(out + (size_t)blockIdx.x * (n + 64)), tab,
-                                              tablog, oring, sh, true, matcher);
+  StreamResult r = encode_stream_fast<FM_POS>((gin_t)in, n, clevel, (gout_t)(out + (size_t)blockIdx.x * (n + 64)), B,
+                                              tablog, true);
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
-  if (threadIdx.x == 64) { cycles[blockIdx.x] = (int64_t)(t1 - t0); res[blockIdx.x] = r; }
+  if (threadIdx.x == 0) { cycles[blockIdx.x] = (int64_t)(t1 - t0); res[blockIdx.x] = r; }
 }
 
 static std::vector<uint8_t> slurp(const char* f) {
@@ -55,14 +51,15 @@ int main(int argc, char** argv) {
   hipMalloc(&dout, (size_t)maxblk * (n + 64));
   int64_t* dc; StreamResult* dr;
   hipMalloc(&dc, maxblk * 8); hipMalloc(&dr, maxblk * sizeof(StreamResult));
-  const size_t lds = ((size_t)FM_POSB << tablog) + kOutRing + ((sizeof(FastShared) + 15) & ~size_t(15));
+  const size_t lds = fm_lds_bytes<FM_POS>(tablog);
   hipFuncSetAttribute(reinterpret_cast<const void*>(&k_enc), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   for (int nblk : {1, 256, 1024, 4096}) {
     uint64_t z[16] = {0};
     hipMemcpyToSymbol(HIP_SYMBOL(g_enc_prof), z, sizeof z);
+    hipMemcpyToSymbol(HIP_SYMBOL(g_fm_cnt), z, 8 * sizeof(uint64_t));
     hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
     hipEventRecord(a);
-    k_enc<<<nblk, 128, lds>>>(din, n, clevel, tablog, dout, dc, dr);
+    k_enc<<<nblk, kFmThreads, lds>>>(din, n, clevel, tablog, dout, dc, dr);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms = 0; hipEventElapsedTime(&ms, a, b);
@@ -71,14 +68,20 @@ int main(int argc, char** argv) {
     hipMemcpy(c.data(), dc, nblk * 8, hipMemcpyDeviceToHost);
     hipMemcpy(r.data(), dr, nblk * sizeof(StreamResult), hipMemcpyDeviceToHost);
     double mean = 0; for (auto x : c) mean += x; mean /= nblk;
-    printf("blocks %5d: %.3f ms, cycles/stream %.0f, kind %d size %d tiles %d (%.0f cycles/tile)\n", nblk, ms, mean,
-           r[0].kind, r[0].size, r[0].windows, mean / (r[0].windows ? r[0].windows : 1));
-    uint64_t pr[16];
+    printf("blocks %5d: %.3f ms, cycles/stream %.0f, kind %d size %d super-tiles %d (%.0f cycles each)\n", nblk, ms,
+           mean, r[0].kind, r[0].size, r[0].windows, mean / (r[0].windows ? r[0].windows : 1));
+    uint64_t pr[16], cn[8];
     hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_enc_prof), sizeof pr);
-    const char* nm[8] = {"M: produce", "P: compare", "P: chain walk", "P: emit", "M: barrier", "P: (match ext)", "P: barrier", "-"};
+    hipMemcpyFromSymbol(cn, HIP_SYMBOL(g_fm_cnt), sizeof cn);
+    const char* nm[8] = {"-", "B exchange", "C + C2", "D walk", "D fixpoint", "E scan", "E emit+flush",
+                         "C2 barrier"};
     for (int pass = 1; pass >= 0; pass--)
-      for (int i = 0; i < 7; i++)
-        printf("   %s %-12s %10.0f cycles/stream\n", pass ? "probe" : "main ", nm[i], pr[8 * pass + i] / (double)nblk);
+      for (int i = 0; i < 8; i++)
+        printf("   %s %-14s %10.0f cycles/stream\n", pass ? "probe" : "main ", nm[i], pr[8 * pass + i] / (double)nblk);
+    printf("   main: fixpoint rounds %.1f / super-tile (%.0f super-tiles); probe %.1f (%.0f); "
+           "long match ends/stream %.1f (%.1f)\n",
+           cn[1] ? (double)cn[0] / cn[1] : 0.0, (double)cn[1] / nblk, cn[5] ? (double)cn[4] / cn[5] : 0.0,
+           (double)cn[5] / nblk, (double)cn[2] / nblk, (double)cn[3] / nblk);
   }
   return 0;
 }

@@ -4,7 +4,7 @@
 // lane-order dependences on the CPU, where a fault costs nothing.  The LDS arrays start filled
 // with garbage (seeded) the way a workgroup finds them after a previous stream or kernel.
 //
-//   g++ -O2 -shared -fPIC -o tools/libfm_emu.so tools/fm_emu.cpp
+//   g++ -O2 -shared -fPIC -o tools/fm2/libfm_emu.so tools/fm2/fm_emu.cpp
 //   int fm_emu_stream(in, n, avail, clevel, out, tablog, u16, seed, int64_t diag[8]) -> size (0 raw)
 #include <stdint.h>
 #include <string.h>
