@@ -2680,6 +2680,16 @@ __global__ void k_dplan_chunks(const uint8_t* const* __restrict__ srcs, const in
     const int32_t ts = d.filters_meta[i] ? d.filters_meta[i] : d.typesize;
     d.fuse_unshuffle = d.filters[i] == kShuffle && ts == 4 && (mode & 8) == 0;
   }
+  // (DELTA, SHUFFLE) at typesize 2 / 4 / 8 over whole quads (the C4 pipeline): undone inside the
+  // decode launch as well -- block 0's completing wave un-shuffles and XOR-scans it, every other
+  // block once block 0 is final (finish_block); not with block masks (a masked block 0 never
+  // completes) nor for the self-referencing getitem semantics
+  if (K == 2 && d.ferr == 0 && (mode & (8 | 16)) == 0 && !d.delta_self && d.filters[5] == kShuffle &&
+      d.filters[4] == kDelta) {
+    const int32_t ts = d.typesize;
+    d.fuse_ds = (d.filters_meta[5] == 0 || d.filters_meta[5] == ts) && (ts == 2 || ts == 4 || ts == 8) &&
+                d.blocksize % (4 * ts) == 0 && d.leftover % (4 * ts) == 0;
+  }
   ch[c] = d;
 }
 
@@ -2709,10 +2719,10 @@ __global__ __launch_bounds__(1024) void k_dscan(DChunk* __restrict__ ch, int32_t
     a += ch[i].nstreams ? ch[i].nbytes : 0;
     bk += ch[i].nblocks;
     st += ch[i].nstreams;
-    dl |= ch[i].has_delta ? 0x100 : 0;
+    dl |= (ch[i].has_delta && !ch[i].fuse_ds) ? 0x100 : 0;
     dl |= (ch[i].nstreams == 0 && ch[i].nbytes != 0) ? 0x200 : 0;   // k_dspecial's chunks
     for (int f = 0; f < 6; f++)
-      if (!bwd_noop(ch[i].filters[f]) && !ch[i].fuse_unshuffle) dl |= 1 << f;
+      if (!bwd_noop(ch[i].filters[f]) && !ch[i].fuse_unshuffle && !ch[i].fuse_ds) dl |= 1 << f;
     mf = max(mf, (int32_t)ch[i].nfilters_bwd);
   }
   sb[threadIdx.x] = a; sbk[threadIdx.x] = bk; sst[threadIdx.x] = st; sdl[threadIdx.x] = dl; smf[threadIdx.x] = mf;
@@ -2975,6 +2985,212 @@ __device__ __forceinline__ void unshuffle4_wave_lds(const uint8_t* __restrict__ 
   for (int32_t i = n * 4 + lane; i < bsize; i += 64) dst[i] = src[i];
 }
 
+// One (DELTA, SHUFFLE) block by one wave, stage -> dst: block 0 un-shuffled and XOR-scanned over
+// its elements, the others un-shuffled and XORed with the final block 0 (the bytes of k_dfilter's
+// fused slot, b2h_filters.h unshuffle_scan_fast / unshuffle_xor_fast).  One wave moves a whole
+// block, so it keeps rows in flight as unshuffle4_wave_lds does: a row is 1024 elements, every
+// plane's 1 KiB of it loaded by one 16-byte lane-linear instruction, the next row's loads issued
+// before this row is transposed through the decoder's idle LDS ring (TS KiB); each lane then
+// owns 16 consecutive elements (16 * TS contiguous output bytes).  Block 0's row scan: lane
+// totals scanned over the wave, then each lane's elements with its exclusive prefix.  The quads
+// after the whole rows (and images whose planes are not 16-byte aligned) take the quad loop.
+template <int TS>
+__device__ __forceinline__ int32_t ds_wave_rows(const uint8_t* __restrict__ src, const uint8_t* __restrict__ ref,
+                                                uint8_t* __restrict__ dst, int32_t n, B2H_LDS uint8_t* lds,
+                                                uint64_t& carry) {
+  const int lane = lane_id();
+  const int32_t rows = n / 1024;
+  if (rows == 0) return 0;
+  u32x4 v[TS], nx[TS];
+#pragma unroll
+  for (int p = 0; p < TS; p++) v[p] = *reinterpret_cast<const u32x4*>(src + (int64_t)p * n + 16 * lane);
+#pragma unroll 1
+  for (int32_t r = 0; r < rows; r++) {
+#pragma unroll
+    for (int p = 0; p < TS; p++) *reinterpret_cast<B2H_LDS u32x4*>(lds + p * 1024 + 16 * lane) = v[p];
+    if (r + 1 < rows) {
+#pragma unroll
+      for (int p = 0; p < TS; p++)
+        nx[p] = *reinterpret_cast<const u32x4*>(src + (int64_t)p * n + (int64_t)(r + 1) * 1024 + 16 * lane);
+    }
+    asm volatile("" ::: "memory");   // the row's LDS writes before any lane reads it back
+    const int64_t e0 = (int64_t)r * 1024 + 16 * lane;   // this lane's first element
+    // element quad j of the lane: TS plane dwords -> TS element-order words
+    auto quad = [&](int j, uint32_t (&w)[TS]) {
+      uint32_t pl[TS];
+#pragma unroll
+      for (int p = 0; p < TS; p++) pl[p] = *reinterpret_cast<const B2H_LDS uint32_t*>(lds + p * 1024 + 16 * lane + 4 * j);
+      planes_to_words<TS>(pl, w);
+    };
+    if (ref) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        uint32_t w[TS], rw[TS];
+        quad(j, w);
+        load_words<TS>(ref, (int32_t)(e0 / 4) + j, rw);
+#pragma unroll
+        for (int k = 0; k < TS; k++) w[k] ^= rw[k];
+        store_words<TS>(dst, (int32_t)(e0 / 4) + j, w);
+      }
+    } else {
+      constexpr int K = TS / 2;   // u64 words per element quad
+      uint64_t tot = 0;           // XOR of the lane's 16 elements (replicated per element width)
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        uint32_t w[TS];
+        quad(j, w);
+#pragma unroll
+        for (int k = 0; k < K; k++) tot ^= (uint64_t)w[2 * k] | ((uint64_t)w[2 * k + 1] << 32);
+      }
+      tot = xor_last_word64(xor_prefix64(tot, TS), TS);   // the XOR of every element, replicated
+      uint64_t sc = tot;
+#pragma unroll
+      for (int dd = 1; dd < 64; dd <<= 1) {
+        const uint64_t y = shfl_up64(sc, dd);
+        if (lane >= dd) sc ^= y;
+      }
+      uint64_t run = carry ^ sc ^ tot;   // every element before this lane's first
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        uint32_t w[TS];
+        quad(j, w);
+        uint64_t x[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) x[k] = (uint64_t)w[2 * k] | ((uint64_t)w[2 * k + 1] << 32);
+        x[0] = xor_prefix64(x[0], TS);
+#pragma unroll
+        for (int k = 1; k < K; k++) x[k] = xor_prefix64(x[k], TS) ^ xor_last_word64(x[k - 1], TS);
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+          const uint64_t o = x[k] ^ run;
+          w[2 * k] = (uint32_t)o;
+          w[2 * k + 1] = (uint32_t)(o >> 32);
+        }
+        run ^= xor_last_word64(x[K - 1], TS);
+        store_words<TS>(dst, (int32_t)(e0 / 4) + j, w);
+      }
+      carry ^= (uint64_t)__shfl((long long)sc, 63);
+    }
+    asm volatile("" ::: "memory");   // every lane's LDS reads before the next row's writes
+#pragma unroll
+    for (int p = 0; p < TS; p++) v[p] = nx[p];
+  }
+  return rows * 256;   // quads done
+}
+template <int TS>
+__device__ __forceinline__ void ds_wave_rest(const uint8_t* __restrict__ src, const uint8_t* __restrict__ ref,
+                                             uint8_t* __restrict__ dst, int32_t n, int32_t q0) {
+  const int32_t quads = n / 4;
+  for (int32_t q = q0 + lane_id(); q < quads; q += 64) {
+    uint32_t p[TS], r[TS], w[TS];
+    load_planes<TS>(src, q, n, p);
+    load_words<TS>(ref, q, r);
+    planes_to_words<TS>(p, w);
+#pragma unroll
+    for (int k = 0; k < TS; k++) w[k] ^= r[k];
+    store_words<TS>(dst, q, w);
+  }
+}
+template <int TS>
+__device__ __forceinline__ void ds_wave_first(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t n,
+                                              int32_t q0, uint64_t carry) {
+  constexpr int K = TS / 2;   // u64 words per quad
+  const int lane = lane_id();
+  const int32_t quads = n / 4;
+  for (int32_t base = q0; base < quads; base += 64) {
+    const int32_t q = base + lane;
+    uint32_t p[TS], w[TS];
+    if (q < quads) {
+      load_planes<TS>(src, q, n, p);
+    } else {
+#pragma unroll
+      for (int k = 0; k < TS; k++) p[k] = 0u;
+    }
+    planes_to_words<TS>(p, w);
+    uint64_t x[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) x[k] = (uint64_t)w[2 * k] | ((uint64_t)w[2 * k + 1] << 32);
+    // the quad's own inclusive scan, then the lanes' totals scanned over the wave
+    x[0] = xor_prefix64(x[0], TS);
+#pragma unroll
+    for (int k = 1; k < K; k++) x[k] = xor_prefix64(x[k], TS) ^ xor_last_word64(x[k - 1], TS);
+    const uint64_t t = xor_last_word64(x[K - 1], TS);
+    uint64_t sc = t;
+#pragma unroll
+    for (int dd = 1; dd < 64; dd <<= 1) {
+      const uint64_t y = shfl_up64(sc, dd);
+      if (lane >= dd) sc ^= y;
+    }
+    const uint64_t ex = carry ^ sc ^ t;   // the elements before this quad
+    if (q < quads) {
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        const uint64_t o = x[k] ^ ex;
+        w[2 * k] = (uint32_t)o;
+        w[2 * k + 1] = (uint32_t)(o >> 32);
+      }
+      store_words<TS>(dst, q, w);
+    }
+    carry ^= (uint64_t)__shfl((long long)sc, 63);
+  }
+}
+// (templated on the decoder's ring size: one copy per k_decode instantiation, which then takes
+// that kernel's register budget instead of its own)
+template <int RLOG>
+__device__ __noinline__ void ds_finish_block(const DChunk& d, int32_t c, int32_t blk, uint8_t* const* __restrict__ dsts,
+                                             uint8_t* __restrict__ stage, B2H_LDS uint8_t* ring) {
+  const bool lo = (blk == d.nblocks - 1) && d.leftover;
+  const int32_t bsize = lo ? d.leftover : d.blocksize, ts = d.typesize, ne = bsize / ts;
+  const int64_t off = (int64_t)blk * d.blocksize;
+  const uint8_t* src = stage + d.stage_off + off;
+  uint8_t* dst = dsts[c] + off;
+  const uint8_t* ref = dsts[c];
+  if (aligned16(src) && aligned16(dst) && aligned16(ref)) {
+    // whole rows through the LDS ring when it holds TS KiB and every plane starts 16-byte aligned
+    const bool rows = (1 << RLOG) >= ts * 1024 && ne % 16 == 0;
+    const uint8_t* r = blk == 0 ? nullptr : ref;
+    uint64_t carry = 0;
+    int32_t q0 = 0;
+    if (ts == 4) {
+      if (rows) q0 = ds_wave_rows<4>(src, r, dst, ne, ring, carry);
+      if (blk == 0) ds_wave_first<4>(src, dst, ne, q0, carry);
+      else ds_wave_rest<4>(src, ref, dst, ne, q0);
+    } else if (ts == 8) {
+      if (rows) q0 = ds_wave_rows<8>(src, r, dst, ne, ring, carry);
+      if (blk == 0) ds_wave_first<8>(src, dst, ne, q0, carry);
+      else ds_wave_rest<8>(src, ref, dst, ne, q0);
+    } else {
+      if (rows) q0 = ds_wave_rows<2>(src, r, dst, ne, ring, carry);
+      if (blk == 0) ds_wave_first<2>(src, dst, ne, q0, carry);
+      else ds_wave_rest<2>(src, ref, dst, ne, q0);
+    }
+    return;
+  }
+  // unaligned images: the element loop (lane i gathers element base + i from the planes)
+  const int lane = lane_id();
+  uint64_t carry = 0;
+  for (int32_t base = 0; base < ne; base += 64) {
+    const int32_t i = base + lane;
+    uint64_t v = 0;
+    if (i < ne)
+      for (int b = 0; b < ts; b++) v |= (uint64_t)src[(int64_t)b * ne + i] << (8 * b);
+    if (blk == 0) {
+#pragma unroll
+      for (int dd = 1; dd < 64; dd <<= 1) {
+        const uint64_t y = shfl_up64(v, dd);
+        if (lane >= dd) v ^= y;
+      }
+      v ^= carry;
+      carry = (uint64_t)__shfl((long long)v, 63);
+    } else if (i < ne) {
+      for (int b = 0; b < ts; b++) v ^= (uint64_t)ref[(int64_t)i * ts + b] << (8 * b);
+    }
+    if (i < ne)
+      for (int b = 0; b < ts; b++) dst[(int64_t)i * ts + b] = (uint8_t)(v >> (8 * b));
+  }
+}
+
+template <int RLOG>
 __device__ __forceinline__ void finish_block(const DChunk* __restrict__ ch, const DStream* __restrict__ streams, int32_t s,
                                              uint8_t* const* __restrict__ dsts, uint8_t* __restrict__ stage,
                                              int32_t* __restrict__ bcnt, B2H_LDS uint8_t* ring) {
@@ -2982,20 +3198,53 @@ __device__ __forceinline__ void finish_block(const DChunk* __restrict__ ch, cons
   asm volatile("" ::: "memory");
   const DStream st = streams[s];
   const DChunk& d = ch[st.chunk];
-  if (!d.fuse_unshuffle) return;
+  const bool fuse_ds = __builtin_amdgcn_readfirstlane(d.fuse_ds) != 0;
+  if (!__builtin_amdgcn_readfirstlane(d.fuse_unshuffle) && !fuse_ds) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int32_t blk = st.dst_off / d.blocksize;
   const bool lo = (blk == d.nblocks - 1) && d.leftover;
   const int32_t ns = (!d.dont_split && !lo) ? d.typesize : 1;
+  int32_t* cnt = bcnt + d.block_base;
   int32_t old = 0;
-  if (lane_id() == 0)
-    old = __hip_atomic_fetch_add(bcnt + d.block_base + blk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane_id() == 0) old = __hip_atomic_fetch_add(cnt + blk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   old = __builtin_amdgcn_readfirstlane(old);
   if (old != ns - 1) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int64_t off = (int64_t)blk * d.blocksize;
-  unshuffle4_wave_lds(stage + d.stage_off + off, dsts[st.chunk] + off, lo ? d.leftover : d.blocksize, ring);
+  if (!fuse_ds) {
+    const int64_t off = (int64_t)blk * d.blocksize;
+    unshuffle4_wave_lds(stage + d.stage_off + off, dsts[st.chunk] + off, lo ? d.leftover : d.blocksize, ring);
+    return;
+  }
+  // (DELTA, SHUFFLE): block 0 first; a block whose streams finish before block 0 is final parks,
+  // and whichever of it and block 0's wave sees the other's mark takes it (exactly once: CLAIM)
+  constexpr int32_t kDone = 1 << 30, kPark = 1 << 29, kClaim = 1 << 28;
+  auto ld = [&](int32_t* p) {
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT));
+  };
+  auto orw = [&](int32_t* p, int32_t v) {
+    int32_t o = 0;
+    if (lane_id() == 0) o = __hip_atomic_fetch_or(p, v, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readfirstlane(o);
+  };
+  if (blk != 0) {
+    if (!(ld(cnt) & kDone)) {
+      orw(cnt + blk, kPark);
+      if (!(ld(cnt) & kDone) || (orw(cnt + blk, kClaim) & kClaim)) return;   // block 0's wave takes it
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    ds_finish_block<RLOG>(d, st.chunk, blk, dsts, stage, ring);
+    return;
+  }
+  ds_finish_block<RLOG>(d, st.chunk, 0, dsts, stage, ring);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  orw(cnt, kDone);
+  for (int32_t k = 1; k < d.nblocks; k++) {
+    if (!(ld(cnt + k) & kPark) || (orw(cnt + k, kClaim) & kClaim)) continue;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    ds_finish_block<RLOG>(d, st.chunk, k, dsts, stage, ring);
+  }
 }
 
 template <int RLOG>
@@ -3016,7 +3265,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RLOG == 12 ?
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     int32_t kind = 0;
     if (decode_stream<RLOG>(srcs, dsts, ch, streams[s], stage, maskout, mask_stride, ring, &kind))
-      finish_block(ch, streams, s, dsts, stage, bcnt, ring);
+      finish_block<RLOG>(ch, streams, s, dsts, stage, bcnt, ring);
     if (dbg && lane_id() == 0) {
       dbg[2 * s] = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
       dbg[2 * s + 1] = kind;
@@ -3045,7 +3294,7 @@ __device__ __forceinline__ void dfilter_block(DChunk* __restrict__ ch, const DBl
   if (pass == 1 && bk.block != 0) return;
   if (pass == 2 && bk.block == 0) return;
   const DChunk d = ch[bk.chunk];
-  if (d.status < 0 || d.fuse_unshuffle) return;
+  if (d.status < 0 || d.fuse_unshuffle || d.fuse_ds) return;
   const uint8_t f = d.filters[slot];
   if (bwd_noop(f)) return;
   if (maskout && maskout[(int64_t)bk.chunk * mask_stride + bk.block]) return;
@@ -3178,7 +3427,13 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
     cap_stage = std::max<int64_t>(dst_bound, 0);
   }
   static const int no_fuse = getenv("B2H_FUSE_UNSHUFFLE") && atoi(getenv("B2H_FUSE_UNSHUFFLE")) == 0 ? 8 : 0;
-  k_dplan_chunks<<<(n + 255) / 256, 256, 0, st>>>(d_src, d_srcsize, d_dstsize, ch, n, mode | no_fuse);
+  // mode bit 16: no in-launch DELTA + SHUFFLE -- with block masks (a masked block 0 never
+  // completes) and unless B2H_DEC_FUSE_DS=1: measured slower than the separate k_dfilter pass on
+  // C4 (decompress 20.2 vs 12.0 ms: one wave per 512 KiB block is latency-bound where k_dfilter's
+  // 256-thread workgroups keep the bytes in flight)
+  const char* fds = getenv("B2H_DEC_FUSE_DS");
+  const int ds_off = (d_maskout || !(fds && atoi(fds) == 1)) ? 16 : 0;
+  k_dplan_chunks<<<(n + 255) / 256, 256, 0, st>>>(d_src, d_srcsize, d_dstsize, ch, n, mode | no_fuse | ds_off);
   k_dscan<<<1, 1024, 0, st>>>(ch, n, tot, cap_blocks, cap_streams, cap_stage);
   HIPCHK(hipGetLastError());
   DTotals h{};

@@ -64,6 +64,7 @@ struct DChunk {
   uint8_t codec, delta_self;   // delta_self: every block un-deltas against itself (dest_offset 0)
   int8_t ferr;                 // backward-pipeline error of every decoded block (0, -1, -18)
   uint8_t fuse_unshuffle;      // the lone backward filter is SHUFFLE: undone inside the decode launch
+  uint8_t fuse_ds;             // (DELTA, SHUFFLE) at typesize 2/4/8: undone inside the decode launch
   int32_t dict_off, dict_size; // LZ4 dictionary section (BLOSC2_USEDICT): offset in the chunk, bytes
 };
 

@@ -176,35 +176,35 @@ int64_t put_chunk(blosc2_schunk* s, Op op, int64_t nchunk, uint8_t* chunk, bool 
   return s->nchunks;
 }
 
-// schunk.c:108-153
-int update_schunk_properties(blosc2_schunk* s) {
-  blosc2_cparams* cp = s->storage->cparams;
-  blosc2_dparams* dp = s->storage->dparams;
-  memcpy(s->filters, cp->filters, BLOSC2_MAX_FILTERS);
-  memcpy(s->filters_meta, cp->filters_meta, BLOSC2_MAX_FILTERS);
-  s->compcode = cp->compcode;
-  s->compcode_meta = cp->compcode_meta;
-  s->clevel = cp->clevel;
-  s->splitmode = (uint8_t)cp->splitmode;
-  s->use_dict = (uint8_t)cp->use_dict;
-  s->typesize = cp->typesize;
-  s->blocksize = cp->blocksize;
+// The super-chunk's copies of its storage's parameters and its two contexts (the fields
+// blosc/schunk.c:108-153 derives): the per-chunk knobs come from cparams, chunksize and flags2 are
+// unknown until the first chunk, and each context is told which super-chunk it serves.
+int adopt_params(blosc2_schunk* s) {
+  const blosc2_cparams& cp = *s->storage->cparams;
+  s->compcode = cp.compcode;
+  s->compcode_meta = cp.compcode_meta;
+  s->clevel = cp.clevel;
+  s->splitmode = (uint8_t)cp.splitmode;
+  s->use_dict = (uint8_t)cp.use_dict;
+  s->typesize = cp.typesize;
+  s->blocksize = cp.blocksize;
+  memcpy(s->filters, cp.filters, BLOSC2_MAX_FILTERS);
+  memcpy(s->filters_meta, cp.filters_meta, BLOSC2_MAX_FILTERS);
+  s->tuner_params = cp.tuner_params;
+  s->tuner_id = cp.tuner_id;
   s->chunksize = -1;
   s->flags2 = 0;
-  s->tuner_params = cp->tuner_params;
-  s->tuner_id = cp->tuner_id;
+  blosc2_context* made[2] = {nullptr, nullptr};
+  s->storage->cparams->schunk = s;
+  s->storage->dparams->schunk = s;
+  made[0] = blosc2_create_cctx(*s->storage->cparams);
+  made[1] = blosc2_create_dctx(*s->storage->dparams);
   if (s->cctx) blosc2_free_ctx(s->cctx);
-  cp->schunk = s;
-  s->cctx = blosc2_create_cctx(*cp);
-  if (!s->cctx) {
-    TRACE_ERROR("Could not create compression ctx");
-    return BLOSC2_ERROR_NULL_POINTER;
-  }
   if (s->dctx) blosc2_free_ctx(s->dctx);
-  dp->schunk = s;
-  s->dctx = blosc2_create_dctx(*dp);
-  if (!s->dctx) {
-    TRACE_ERROR("Could not create decompression ctx");
+  s->cctx = made[0];
+  s->dctx = made[1];
+  if (!made[0] || !made[1]) {
+    TRACE_ERROR("super-chunk: %s context not created", made[0] ? "decompression" : "compression");
     return BLOSC2_ERROR_NULL_POINTER;
   }
   return 0;
@@ -262,8 +262,7 @@ blosc2_schunk* blosc2_schunk_new(blosc2_storage* storage) {
   s->storage = ns;
   s->version = 0;   // pre-first version
   s->view = false;
-  if (update_schunk_properties(s) < 0) {
-    TRACE_ERROR("Error when updating schunk properties");
+  if (adopt_params(s) < 0) {
     blosc2_schunk_free(s);
     return nullptr;
   }

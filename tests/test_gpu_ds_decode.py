@@ -1,0 +1,72 @@
+"""GPU tier: (DELTA, SHUFFLE) chunk decode, both by the separate k_dfilter pass (the default) and
+undone inside the decode launch (B2H_DEC_FUSE_DS=1: k_decode finish_block, DChunk::fuse_ds; the
+C4 pipeline, measured slower than the separate pass -- DESIGN.md §3): block 0's completing wave un-shuffles and XOR-scans it, every
+other block is un-shuffled and XORed with the final block 0 once that is published (a block that
+finishes first parks and is taken exactly once).  Checked against the oracle's chunks decoded on
+the CPU (blosc/delta.c:18-161 + blosc/shuffle-generic.h:34-83 restated in oracle/blosc2_oracle.c):
+typesizes 2 / 4 / 8, several blocksizes, leftover blocks that do and do not fuse (a leftover that
+is not whole quads keeps the chunk on the k_dfilter path), destinations at 16-byte-aligned and at
+odd strides (the element loop), and many chunks per batch so blocks race block 0.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "c-blosc2_amd"))
+sys.path.insert(0, HERE)
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(ts, nbytes, seed):
+    """Smooth integer series with noise (LZ, raw and run streams all occur after DELTA+SHUFFLE)."""
+    rng = np.random.default_rng(seed)
+    n = nbytes // ts
+    dt = {2: np.uint16, 4: np.uint32, 8: np.uint64}[ts]
+    base = np.cumsum(rng.integers(0, 3, n)).astype(dt)
+    noise = rng.integers(0, 4, n).astype(dt) * (rng.random(n) < 0.2)
+    return (base + noise).view(np.uint8)[:nbytes]
+
+
+@pytest.mark.parametrize("ts,blocksize,nbytes", [
+    (8, 65536, 6 * 65536 + 32 * 100),     # leftover of whole quads: fused
+    (4, 16384, 9 * 16384),                # no leftover
+    (2, 32768, 3 * 32768 + 8 * 77),       # leftover of whole quads (8-byte quads at ts 2)
+    (8, 65536, 2 * 65536 + 8 * 5),        # leftover NOT whole quads: the k_dfilter path
+])
+@pytest.mark.parametrize("align", [0, 3])
+@pytest.mark.parametrize("fused", ["1", "0"], ids=["in-launch", "k_dfilter"])
+def test_gpu_fused_delta_shuffle_decode(ts, blocksize, nbytes, align, fused, monkeypatch):
+    import torch
+    monkeypatch.setenv("B2H_DEC_FUSE_DS", fused)
+    import blosc2_amd as B
+    from oracle_lib import oracle_compress, oracle_decompress
+    kw = dict(clevel=5, typesize=ts, filters=(0, 0, 0, 0, 3, 1), blocksize=blocksize)
+    nch = 48
+    raws = [_data(ts, nbytes, 100 * ts + i) for i in range(nch)]
+    chunks = [oracle_compress(r, **kw) for r in raws]
+    for c, r in zip(chunks, raws):
+        assert isinstance(c, np.ndarray) and np.array_equal(oracle_decompress(c, nbytes), r)
+    sstride = max(c.nbytes for c in chunks) + 256
+    host = np.zeros(nch * sstride, np.uint8)
+    cbytes = np.zeros(nch, np.int32)
+    for i, c in enumerate(chunks):
+        host[i * sstride:i * sstride + c.nbytes] = c
+        cbytes[i] = c.nbytes
+    dsrc = torch.from_numpy(host).cuda()
+    dcb = torch.from_numpy(cbytes).cuda()
+    dstride = (nbytes + 255) // 256 * 256 + align   # align 3: every chunk but the first at an odd address
+    dout = torch.zeros(nch * dstride + 64, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(nch, dtype=torch.int32, device="cuda")
+    B.decompress_batch(dsrc.data_ptr(), sstride, dcb.data_ptr(), nch, dout.data_ptr(), dstride, nbytes, st.data_ptr())
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == nbytes).all(), st.cpu().numpy()
+    back = dout.cpu().numpy()
+    for i, r in enumerate(raws):
+        assert np.array_equal(back[i * dstride:i * dstride + nbytes], r), i
+    # the single-chunk host path (blosc2_decompress_ctx) decodes the same bytes
+    got = B.decompress(chunks[0], nbytes)
+    assert np.array_equal(np.asarray(got).view(np.uint8).reshape(-1)[:nbytes], raws[0])

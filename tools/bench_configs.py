@@ -347,6 +347,36 @@ def c1(steps, nchunks=67, clevel=5):
            "cratio": round(size / float(cbh[0]), 2),
            "gpu_compress_MBps": round(nchunks * size / (t_c * 1e-3) / 1e6, 1),
            "gpu_decompress_MBps": round(nchunks * size / (t_d * 1e-3) / 1e6, 1)}
+    # the drop-in per-call path, as b2bench calls it (bench/b2bench.c:199, 227): blosc1_compress /
+    # blosc1_decompress on HOST buffers, one 4 MB chunk per call (each call: H2D, one launch chain,
+    # D2H, synchronise) -- SURVEY §7 hard part 5, the single-chunk latency
+    L = B.lib()
+    L.blosc1_set_compressor(b"blosclz")
+    hsrc = src.copy()
+    hdst = np.zeros((nchunks, cap), np.uint8)
+    hback = np.zeros(size, np.uint8)
+    n0 = L.blosc1_compress(clevel, 1, 4, size, p(hsrc), p(hdst[0]), cap)   # warm-up (context, buffers)
+    L.blosc1_decompress(p(hdst[0]), p(hback), size)
+    pc, pd = [], []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        for i in range(nchunks):
+            L.blosc1_compress(clevel, 1, 4, size, p(hsrc), p(hdst[i]), cap)
+        t1 = time.perf_counter()
+        for i in range(nchunks):
+            L.blosc1_decompress(p(hdst[i]), p(hback), size)
+        t2 = time.perf_counter()
+        pc.append(t1 - t0)
+        pd.append(t2 - t1)
+    res["gpu_per_call_host_buffers"] = {
+        "compress_MBps": round(nchunks * size / float(np.median(pc)) / 1e6, 1),
+        "decompress_MBps": round(nchunks * size / float(np.median(pd)) / 1e6, 1),
+        "compress_ms_per_call": round(float(np.median(pc)) / nchunks * 1e3, 3),
+        "decompress_ms_per_call": round(float(np.median(pd)) / nchunks * 1e3, 3),
+        "chunk_bytes_equal_batch": bool(n0 == int(cbh[0]) and np.array_equal(hdst[0][:n0], chunk0)),
+        "round_trip_exact": bool(np.array_equal(hback, src.view(np.uint8))),
+        "note": "product blosc1_compress / blosc1_decompress per 4 MB host chunk (PCIe both ways inside "
+                "every call), median of 3 passes over the 67 chunks"}
     R = ref()
     if R is not None:
         R.blosc1_set_compressor(b"blosclz")
