@@ -38,7 +38,7 @@ struct CompressPlan {
   int32_t compcode;        // BLOSC_BLOSCLZ (0) or BLOSC_LZ4 (1)
   bool use_dict;           // LZ4 with a dictionary requested and in force (clevel > 0, not memcpyed)
   int32_t dict_size;       // its size (0: the reference falls back to no dictionary)
-  int32_t lz_mode = -1;    // BloscLZ encoder: 0 exact, 1 fast, -1 the process default (set_blosclz_mode)
+  int32_t lz_mode = -1;    // BloscLZ encoder: 0 exact, 1 fast, 2 fast + deep candidates, -1 the process default
 };
 
 // Fill the plan from cparams-level values the way blosc2_compress_ctx does (initialize_context_

@@ -83,7 +83,7 @@ struct Scratch {
 };
 
 struct Workspace {
-  Scratch t1, t2, work, sbuf, res, place, mode, qctr, gtab, porder, fsync;    // compress
+  Scratch t1, t2, work, sbuf, res, place, mode, qctr, gtab, porder, fsync, fchain;    // compress
   bool porder_init = false;
   Scratch dchunks, dstreams, dblocks, dtotals, stage, stage2, ptrs, dqctr, ddbg, dorder, dbcnt;  // decompress
   std::mutex mu;
@@ -103,7 +103,7 @@ struct Workspace {
   }
   void free_all() {
     if (used && done) (void)hipEventSynchronize(done);
-    for (Scratch* s : {&t1, &t2, &work, &sbuf, &res, &place, &mode, &qctr, &gtab, &porder, &fsync, &dchunks, &dstreams,
+    for (Scratch* s : {&t1, &t2, &work, &sbuf, &res, &place, &mode, &qctr, &gtab, &porder, &fsync, &fchain, &dchunks, &dstreams,
                        &dblocks, &dtotals, &stage, &stage2, &ptrs, &dqctr, &ddbg, &dorder, &dbcnt})
       s->release();
     if (done) (void)hipEventDestroy(done);
@@ -285,9 +285,11 @@ struct CGeom {
   int32_t nbytes, bs, nblocks, leftover, spb, nsc, neblock, ts, destsize, clevel, overhead, compcode;
   int32_t dict_size;   // LZ4 dictionary section [int32 size | bytes] after the bstarts (0: none)
   int32_t front;   // encoder pull schedule (pull_to_stream), 0 = stream order
-  int32_t lzmode;  // BloscLZ encoder of this batch: 0 exact, 1 fast (the plan's, else the process default)
+  int32_t lzmode;  // BloscLZ encoder of this batch: 0 exact, 1 fast, 2 fast with deep candidates (the plan's, else the process default)
   int64_t src_stride, wstride, dst_stride;
+  uint8_t* chain;  // mode 2: the fast encoder's prev[] arrays, one per workgroup of chain_len() positions
 };
+__host__ __device__ inline int64_t chain_len(const CGeom& g) { return g.neblock > g.leftover ? g.neblock : g.leftover; }
 
 __device__ __forceinline__ void stream_locate(const CGeom& g, int32_t l, int32_t* off, int32_t* len, int32_t* blk) {
   const int32_t full = g.nblocks - (g.leftover ? 1 : 0);
@@ -564,7 +566,7 @@ __global__ __launch_bounds__(64 * (NLDS + NGLB)) void k_encode(EncArgs args, POS
 __host__ __device__ constexpr size_t fast_lds(size_t pos_bytes, int tablog) {
   return (pos_bytes << tablog) + kOutRing + ((sizeof(FastShared) + 15) & ~size_t(15));
 }
-template <typename POS>
+template <typename POS, bool DEEP>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4, 8)))   // <= 128 VGPRs: 16 waves per CU
 void k_encode_fast(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
                    StreamResult* __restrict__ res, int32_t nstreams_total, int32_t* __restrict__ next, int tablog,
@@ -595,8 +597,9 @@ void k_encode_fast(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restric
     gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
-    StreamResult r = encode_stream_fast<POS>(in, len, g.clevel, out, tab, tablog, oring, sh, g.overhead == kHdrExt,
-                                             matcher);
+    StreamResult r = encode_stream_fast<POS, false, DEEP>(in, len, g.clevel, out, tab, tablog, oring, sh,
+                                                          g.overhead == kHdrExt, matcher,
+                                                          (B2H_GLB POS*)g.chain + (int64_t)blockIdx.x * chain_len(g));
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
     if (!matcher && lane_id() == 0) res[s] = r;
@@ -610,13 +613,13 @@ static int g_lz_mode = -1;
 static int lz_mode() {
   if (g_lz_mode < 0) {
     const char* e = getenv("B2H_LZ_MODE");
-    g_lz_mode = (e && !strcmp(e, "fast")) ? 1 : 0;
+    g_lz_mode = (e && !strcmp(e, "fast")) ? 1 : (e && !strcmp(e, "deep")) ? 2 : 0;
   }
   return g_lz_mode;
 }
 int set_blosclz_mode(int mode) {
   const int old = lz_mode();
-  if (mode == 0 || mode == 1) g_lz_mode = mode;
+  if (mode >= 0 && mode <= 2) g_lz_mode = mode;
   return old;
 }
 static int fast_tablog() {
@@ -628,13 +631,24 @@ static int fast_tablog() {
   return v;
 }
 
+// Mode 2: one prev[] array of chain_len(g) positions per workgroup of the grid.
 template <typename POS>
-static int launch_encode_fast_t(Workspace* ws, const CGeom& g, const uint8_t* filt, StreamResult* res, int64_t ntot,
+static int chain_prepare(Workspace* ws, CGeom& g, uint32_t grid) {
+  g.chain = nullptr;
+  if (g.lzmode != 2) return 0;
+  if (ws->fchain.ensure((size_t)grid * (size_t)chain_len(g) * sizeof(POS) + 256)) return E_MEMORY;
+  g.chain = ws->fchain.as<uint8_t>();
+  return 0;
+}
+
+template <typename POS, bool DEEP>
+static int launch_encode_fast_t(Workspace* ws, const CGeom& g0, const uint8_t* filt, StreamResult* res, int64_t ntot,
                                 int32_t* next, const int32_t* porder, hipStream_t st) {
+  CGeom g = g0;
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
   const int tablog = std::min(fast_tablog(), hashlog);
   const size_t lds = fast_lds(sizeof(POS), tablog);
-  const void* fn = reinterpret_cast<const void*>(&k_encode_fast<POS>);
+  const void* fn = reinterpret_cast<const void*>(&k_encode_fast<POS, DEEP>);
   static bool attr_set = false;
   if (!attr_set) {   // > 64 KiB of dynamic LDS (u32, tablog 14): opt in once
     HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -642,7 +656,8 @@ static int launch_encode_fast_t(Workspace* ws, const CGeom& g, const uint8_t* fi
   }
   const int slots = resident_slots(fn, lds, 128);
   const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(ntot, slots));
-  k_encode_fast<POS><<<grid, 128, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog, porder);
+  if (chain_prepare<POS>(ws, g, grid)) return E_MEMORY;
+  k_encode_fast<POS, DEEP><<<grid, 128, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog, porder);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -650,9 +665,12 @@ static int launch_encode_fast_t(Workspace* ws, const CGeom& g, const uint8_t* fi
 // u16 positions (half the LDS: twice the waves per CU) while every stream fits 64 KiB
 static int launch_encode_fast(Workspace* ws, const CGeom& g, const uint8_t* filt, StreamResult* res, int64_t ntot,
                               int32_t* next, const int32_t* porder, hipStream_t st) {
-  if (std::max(g.neblock, g.leftover) <= 65536)
-    return launch_encode_fast_t<uint16_t>(ws, g, filt, res, ntot, next, porder, st);
-  return launch_encode_fast_t<uint32_t>(ws, g, filt, res, ntot, next, porder, st);
+  const bool small = std::max(g.neblock, g.leftover) <= 65536;
+  if (g.lzmode == 2)
+    return small ? launch_encode_fast_t<uint16_t, true>(ws, g, filt, res, ntot, next, porder, st)
+                 : launch_encode_fast_t<uint32_t, true>(ws, g, filt, res, ntot, next, porder, st);
+  return small ? launch_encode_fast_t<uint16_t, false>(ws, g, filt, res, ntot, next, porder, st)
+               : launch_encode_fast_t<uint32_t, false>(ws, g, filt, res, ntot, next, porder, st);
 }
 
 // ------------------------------------------------------------------------ LZ4 encoder ----
@@ -1448,7 +1466,7 @@ __host__ __device__ constexpr size_t fused_lds(size_t pos_bytes, int tablog) {
 
 #undef FUSE_TRACE_PTR
 #define FUSE_TRACE_PTR lds_uniform(&A->f.trace)
-template <typename POS>
+template <typename POS, bool DEEP>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4, 8)))   // as k_encode_fast
 void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint8_t* __restrict__ sbuf_arg,
                          StreamResult* __restrict__ res_arg, int32_t nstreams_total_arg, int32_t* __restrict__ next_arg,
@@ -1616,7 +1634,12 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
     FUSE_TRACE(6, s);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
-    StreamResult r = encode_stream_fast<POS, true>(in, len, clevel, out, tab, tablog, oring, sh, runs, matcher);
+    B2H_GLB POS* chain = nullptr;
+    if constexpr (DEEP) {
+      const CGeom g = lds_uniform(&A->g);
+      chain = (B2H_GLB POS*)g.chain + (int64_t)blockIdx.x * chain_len(g);
+    }
+    StreamResult r = encode_stream_fast<POS, true, DEEP>(in, len, clevel, out, tab, tablog, oring, sh, runs, matcher, chain);
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
     if (!matcher && lane_id() == 0) {
@@ -1746,13 +1769,14 @@ static int fuse_prepare(Workspace* ws, const CGeom& g, int64_t ntot, EncFuse& f,
 }
 
 // Sync words + per-stream results of the fused launch (f.raw / f.filt set by the caller).
-template <typename POS>
-static int launch_encode_fast_fused_t(Workspace* ws, const CGeom& g, const uint8_t* filt, StreamResult* res,
+template <typename POS, bool DEEP>
+static int launch_encode_fast_fused_t(Workspace* ws, const CGeom& g0, const uint8_t* filt, StreamResult* res,
                                       int64_t ntot, int32_t* next, const int32_t* porder, EncFuse f, hipStream_t st) {
+  CGeom g = g0;
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
   const int tablog = std::min(fast_tablog(), hashlog);
   const size_t lds = fused_lds(sizeof(POS), tablog);
-  const void* fn = reinterpret_cast<const void*>(&k_encode_fast_fused<POS>);
+  const void* fn = reinterpret_cast<const void*>(&k_encode_fast_fused<POS, DEEP>);
   static bool attr_set = false;
   if (!attr_set) {
     HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -1761,12 +1785,13 @@ static int launch_encode_fast_fused_t(Workspace* ws, const CGeom& g, const uint8
   const int slots = resident_slots(fn, lds, 128);
   const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(ntot, fuse_grid_cap(slots)));
   if (fuse_prepare(ws, g, ntot, f, st)) return E_MEMORY;
+  if (chain_prepare<POS>(ws, g, grid)) return E_MEMORY;
   static int32_t* trace = nullptr;
   static const bool tr = getenv("B2H_FUSE_TRACE") != nullptr;
   if (tr && !trace) HIPCHK(hipHostMalloc(&trace, 4 << 20, hipHostMallocCoherent));
   f.trace = tr ? trace : nullptr;
   if (tr) memset(trace, 0xff, 4 * (size_t)grid);
-  k_encode_fast_fused<POS><<<grid, 128, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog,
+  k_encode_fast_fused<POS, DEEP><<<grid, 128, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog,
                                                    porder, f);
   HIPCHK(hipGetLastError());
   if (tr) {   // debug watchdog: report where the workgroups are if the launch has not ended after 5 s
@@ -1810,9 +1835,12 @@ static bool fused_encode_ok(const CGeom& g) {
 static int launch_encode_fast_fused(Workspace* ws, const CGeom& g, const uint8_t* filt, StreamResult* res,
                                     int64_t ntot, int32_t* next, const int32_t* porder, const EncFuse& f,
                                     hipStream_t st) {
-  if (std::max(g.neblock, g.leftover) <= 65536)
-    return launch_encode_fast_fused_t<uint16_t>(ws, g, filt, res, ntot, next, porder, f, st);
-  return launch_encode_fast_fused_t<uint32_t>(ws, g, filt, res, ntot, next, porder, f, st);
+  const bool small = std::max(g.neblock, g.leftover) <= 65536;
+  if (g.lzmode == 2)
+    return small ? launch_encode_fast_fused_t<uint16_t, true>(ws, g, filt, res, ntot, next, porder, f, st)
+                 : launch_encode_fast_fused_t<uint32_t, true>(ws, g, filt, res, ntot, next, porder, f, st);
+  return small ? launch_encode_fast_fused_t<uint16_t, false>(ws, g, filt, res, ntot, next, porder, f, st)
+               : launch_encode_fast_fused_t<uint32_t, false>(ws, g, filt, res, ntot, next, porder, f, st);
 }
 
 
@@ -2206,7 +2234,7 @@ static CGeom make_geom(const CompressPlan& P, int64_t src_stride, int64_t dst_st
   g.overhead = P.overhead;
   g.compcode = P.compcode;
   g.dict_size = P.use_dict ? P.dict_size : 0;
-  g.lzmode = (P.lz_mode == 0 || P.lz_mode == 1) ? P.lz_mode : lz_mode();
+  g.lzmode = (P.lz_mode >= 0 && P.lz_mode <= 2) ? P.lz_mode : lz_mode();
   g.src_stride = src_stride;
   g.dst_stride = dst_stride;
   g.wstride = ((int64_t)n + 255) / 256 * 256 + 256;
@@ -2421,10 +2449,10 @@ static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const ui
       f.cbytes = d_cbytes;
       f.htpl = htpl;
       f.nchunks = nchunks;
-      if (g.lzmode == 1) rc = launch_encode_fast_fused(ws, g, filt, res, ntot, next, porder, f, st);
+      if (g.lzmode != 0) rc = launch_encode_fast_fused(ws, g, filt, res, ntot, next, porder, f, st);
       else rc = small ? launch_encode_exact_fused<uint16_t>(ws, g, hashlog, filt, res, ntot, next, porder, f, st)
                       : launch_encode_exact_fused<uint32_t>(ws, g, hashlog, filt, res, ntot, next, porder, f, st);
-    } else if (g.lzmode == 1) rc = launch_encode_fast(ws, g, filt, res, ntot, next, porder, st);
+    } else if (g.lzmode != 0) rc = launch_encode_fast(ws, g, filt, res, ntot, next, porder, st);
     else rc = small ? launch_encode<uint16_t>(ws, g, hashlog, filt, res, ntot, next, porder, st)
                     : launch_encode<uint32_t>(ws, g, hashlog, filt, res, ntot, next, porder, st);
     if (rc) return rc;

@@ -21,6 +21,12 @@
 //
 // Every match is verified byte for byte against its candidate, so any output decodes with
 // blosclz_decompress; the ratio on T is within 0.1 % of the reference's.
+//
+// DEEP (BloscLZ mode 2): the candidate is the best of the bucket chain c1, prev[c1], ... (up to
+// kDeepDepth links, by leading equal bytes up to kDeepSel, the newest on a tie -- tools/fm_model.c
+// insert_tile).  The matcher records prev[p] = c1 in a per-workgroup global array (links into the
+// tile being inserted come from the lanes' own exchange results) and walks the chains of a tile's
+// 128 positions together, one load round trip per link.
 #pragma once
 #include "b2h_lz.h"
 
@@ -56,6 +62,8 @@ __device__ __forceinline__ uint32_t fast_exchange(uint32_t v, int32_t p, bool va
   }
   return old;
 }
+
+constexpr int kDeepDepth = 8, kDeepSel = 24;
 
 // Candidate usable: 0 < distance < MAX_FARDISTANCE (blosc/blosclz.c:516-519).  Lanes without one
 // load their own bytes (compares equal, flagged off).
@@ -135,9 +143,10 @@ __device__ __forceinline__ void fast_clear_half(B2H_LDS uint8_t* tab, int tablog
 // state live everywhere and spilled ~170 SGPRs into VGPR lanes).
 //
 // MATCHER: tile exchanges, candidate loads and 60-byte compares -> the hand-over records.
-template <bool PROBE, typename POS>
+template <bool PROBE, typename POS, bool DEEP>
 __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int32_t length, int probe_hashlog, int tablog,
-                                                               B2H_LDS uint8_t* tab, B2H_LDS FastShared* sh) {
+                                                               B2H_LDS uint8_t* tab, B2H_LDS FastShared* sh,
+                                                               B2H_GLB POS* __restrict__ chain) {
   const int lane = lane_id();
   int32_t limit, bound, loop_end;
   fast_limits<PROBE>(length, probe_hashlog, &limit, &bound, &loop_end);
@@ -156,6 +165,65 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
       s[h] = (uint32_t)(reinterpret_cast<uintptr_t>(q8) & 3);
       w[h][0] = q[0];
       w[h][1] = q[1];
+    }
+  };
+  // DEEP: record prev[p] = c1 and replace each position's candidate by the best of its chain
+  // (tools/fm_model.c insert_tile; sel = equal leading bytes, at most kDeepSel, never at or past
+  // `limit`; a link is followed while positive and within MAX_FARDISTANCE)
+  auto deep_select = [&](int32_t t, const int32_t (&p)[2], const bool (&valid)[2], const uint32_t (&a0)[2][2],
+                         const uint32_t (&ash)[2], uint32_t (&cand)[2], bool (&cok)[2]) {
+    const int32_t P = t * kFastTile;
+    uint32_t c1[2], aw[2][7];
+    int32_t cc[2], best[2], bl[2], cap[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      c1[h] = cand[h];
+      if (valid[h]) chain[p[h]] = (POS)c1[h];
+      const B2H_GLB uint32_t* q = align4(in + (valid[h] ? p[h] : 0));
+      aw[h][0] = a0[h][0];
+      aw[h][1] = a0[h][1];
+#pragma unroll
+      for (int i = 2; i < 7; i++) aw[h][i] = q[i];
+      cap[h] = min(kDeepSel, limit - p[h]);
+      best[h] = (int32_t)c1[h];
+      bl[h] = -1;
+      cc[h] = (cok[h] && (int32_t)c1[h] > 0) ? (int32_t)c1[h] : 0;
+    }
+    for (int k = 0; k < kDeepDepth; k++) {
+      if (__ballot(cc[0] > 0 || cc[1] > 0) == 0) break;   // wave-uniform
+      int32_t nx[2];
+      uint32_t cw7[2][7], csh[2];
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        // the link: a position of this tile holds it in its lane's c1; an earlier one in `chain`
+        const int32_t q = cc[h] - P;
+        const int32_t l0 = __shfl((int)c1[0], q & 63), l1 = __shfl((int)c1[1], q & 63);
+        const bool intile = q >= 0;
+        nx[h] = (cc[h] > 0 && !intile && k + 1 < kDeepDepth) ? (int32_t)chain[cc[h]] : (q >= kHalf ? l1 : l0);
+        gin_t cq = in + (cc[h] > 0 ? cc[h] : 0);
+        const B2H_GLB uint32_t* cw = align4(cq);
+        csh[h] = (uint32_t)(reinterpret_cast<uintptr_t>(cq) & 3);
+#pragma unroll
+        for (int i = 0; i < 7; i++) cw7[h][i] = cw[i];
+      }
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        int32_t n = kDeepSel;
+#pragma unroll
+        for (int i = 5; i >= 0; i--) {
+          const uint32_t x = funnel(aw[h][i], aw[h][i + 1], ash[h]) ^ funnel(cw7[h][i], cw7[h][i + 1], csh[h]);
+          if (x) n = 4 * i + (int32_t)(__builtin_ctz(x) >> 3);
+        }
+        n = min(n, cap[h]);
+        if (cc[h] > 0 && n > bl[h]) { bl[h] = n; best[h] = cc[h]; }
+        const bool more = cc[h] > 0 && bl[h] < cap[h] && k + 1 < kDeepDepth && nx[h] > 0 && p[h] - nx[h] < kLzFar;
+        cc[h] = more ? nx[h] : 0;
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      cand[h] = (uint32_t)best[h];
+      cok[h] = fast_cand_ok(p[h], cand[h], valid[h]);
     }
   };
   // insert tile t (half 0, then half 1: position order), test every position's candidate, hand
@@ -182,6 +250,7 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
       cand[h] = fast_exchange<POS>(v[h], p[h], valid[h], tablog, tab);
       cok[h] = fast_cand_ok(p[h], cand[h], valid[h]);
     }
+    if constexpr (DEEP) deep_select(t, p, valid, a0, ash, cand, cok);
     // the candidate's first word decides most halves: when no lane's 4 bytes match, every first
     // mismatch lies in word 0 and the other 14 words are neither loaded nor compared
     const B2H_GLB uint32_t* cw[2];
@@ -653,12 +722,13 @@ __device__ __forceinline__ LzPassOut lz_pass_fast_parser(gin_t __restrict__ in, 
 }
 
 // One pass, both roles (the matcher's result is not used).
-template <bool PROBE, typename POS, bool WT>
+template <bool PROBE, typename POS, bool WT, bool DEEP>
 __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int probe_hashlog, int tablog, gout_t out,
                                                    int32_t maxout, B2H_LDS uint8_t* tab, B2H_LDS uint8_t* oring,
-                                                   B2H_LDS FastShared* sh, int clevel, bool matcher) {
+                                                   B2H_LDS FastShared* sh, int clevel, bool matcher,
+                                                   B2H_GLB POS* chain) {
   if (matcher) {
-    lz_pass_fast_matcher<PROBE, POS>(in, length, probe_hashlog, tablog, tab, sh);
+    lz_pass_fast_matcher<PROBE, POS, DEEP>(in, length, probe_hashlog, tablog, tab, sh, chain);
     LzPassOut r;
     r.o = 1;
     r.pos = 0;
@@ -674,10 +744,13 @@ __device__ __forceinline__ LzPassOut lz_pass_fast(gin_t in, int32_t length, int 
 
 // Two-wave fast-mode stream encode: both waves run this; the parser's StreamResult is the one
 // to keep.  The run test is split between the waves; decisions travel through sh->decide.
-template <typename POS, bool WT = false>
+// DEEP: the chained candidates of BloscLZ mode 2; `chain` = this workgroup's prev[] array (one
+// POS per position of the longest stream; unused otherwise).
+template <typename POS, bool WT = false, bool DEEP = false>
 __device__ __forceinline__ StreamResult encode_stream_fast(gin_t __restrict__ in, int32_t n, int clevel, gout_t __restrict__ out,
                                                             B2H_LDS uint8_t* tab, int tablog, B2H_LDS uint8_t* oring,
-                                                            B2H_LDS FastShared* sh, bool allow_runs, bool matcher) {
+                                                            B2H_LDS FastShared* sh, bool allow_runs, bool matcher,
+                                                            B2H_GLB POS* chain = nullptr) {
   StreamResult res;
   res.windows = 0;
   res.cycles = 0;
@@ -707,8 +780,8 @@ __device__ __forceinline__ StreamResult encode_stream_fast(gin_t __restrict__ in
   if (clevel < 2) maxlen /= 8;
   else if (clevel < 4) maxlen /= 4;
   else if (clevel < 7) maxlen /= 2;
-  const LzPassOut pr = lz_pass_fast<true, POS, WT>(in + (n - maxlen), maxlen, hashlog, tl, out, 0, tab, oring, sh, clevel,
-                                                matcher);
+  const LzPassOut pr = lz_pass_fast<true, POS, WT, DEEP>(in + (n - maxlen), maxlen, hashlog, tl, out, 0, tab, oring, sh,
+                                                      clevel, matcher, chain);
   res.windows = pr.windows;
   const double ratio = (double)pr.pos / (double)pr.o;
   const double thr = clevel == 1 ? 2.0 : clevel == 2 ? 1.5 : clevel <= 6 ? 1.2 : clevel == 7 ? 1.15 : clevel == 8 ? 1.1 : 1.0;
@@ -717,7 +790,7 @@ __device__ __forceinline__ StreamResult encode_stream_fast(gin_t __restrict__ in
   const bool go = __builtin_amdgcn_readfirstlane(sh->decide[0]) != 0;
   __syncthreads();
   if (!go) return res;
-  const LzPassOut em = lz_pass_fast<false, POS, WT>(in, n, hashlog, tl, out, n, tab, oring, sh, clevel, matcher);
+  const LzPassOut em = lz_pass_fast<false, POS, WT, DEEP>(in, n, hashlog, tl, out, n, tab, oring, sh, clevel, matcher, chain);
   res.windows += em.windows;
   if (em.fail) return res;
   res.kind = kStreamLz;

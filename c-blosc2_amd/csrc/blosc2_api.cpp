@@ -177,7 +177,7 @@ int codec_params_lz_mode(const void* codec_params) {
   if (!codec_params) return -1;
   const b2h_codec_params* p = static_cast<const b2h_codec_params*>(codec_params);
   if (p->magic != B2H_CODEC_PARAMS_MAGIC) return -1;
-  return (p->blosclz_mode == 0 || p->blosclz_mode == 1) ? p->blosclz_mode : -1;
+  return (p->blosclz_mode >= 0 && p->blosclz_mode <= 2) ? p->blosclz_mode : -1;
 }
 }  // namespace b2h
 

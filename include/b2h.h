@@ -153,7 +153,7 @@ BLOSC_EXPORT int b2h_schunk_set_slice_device(blosc2_schunk *schunk, int64_t star
 #define B2H_CODEC_PARAMS_MAGIC 0x68623262u /* "b2bh" */
 typedef struct {
   uint32_t magic;       /* B2H_CODEC_PARAMS_MAGIC */
-  int32_t blosclz_mode; /* 0 exact (byte-identical to the reference), 1 fast */
+  int32_t blosclz_mode; /* 0 exact (byte-identical to the reference), 1 fast, 2 fast + deep candidates */
 } b2h_codec_params;
 
 /* BloscLZ encoder mode, the process-wide default of contexts that do not choose one through
@@ -163,6 +163,10 @@ typedef struct {
  *     hash-table candidates come from positions inserted in 128-position tiles independently of the
  *     parse (c-blosc2_amd/csrc/b2h_lzfast.h, model tools/fm_model.c); every stream decodes with the
  *     reference's blosclz_decompress and the chunk format is unchanged.  Also B2H_LZ_MODE=fast.
+ *   2 fast with deep candidates: as 1, but a position's candidate is the best of its hash bucket's
+ *     last 8 positions (by up to 24 leading equal bytes; tools/fm_model.c fm_set_depth), which
+ *     brings the ratio to the reference's or above on its benchmark data at the
+ *     cost of a longer matcher step.  Also B2H_LZ_MODE=deep.
  * Any other value only queries. */
 BLOSC_EXPORT int b2h_set_blosclz_mode(int mode);
 

@@ -21,13 +21,25 @@
  * The GPU kernel (b2h_lzfast.h lz_pass_fast) runs the tile inserts as one LDS atomic exchange per
  * lane; LDS applies the lanes of one instruction in lane order, so it reproduces this model byte
  * for byte (tests/test_fast_mode.py checks both that and the reference decoder round trip).
+ *
+ * Deep candidates (fm_set_depth(d), d > 1; the engine's BloscLZ mode 2): the most recent position
+ * of a bucket is often a short repeat inside a long-period pattern, where the reference's sparse
+ * table happens to keep an older, longer one (b2bench's data: ratio 12.2 vs 20.6).  So every
+ * inserted position also records its bucket predecessor, prev[p] = cand[p], and the candidate
+ * offered at p is the best of the chain cand[p], prev[cand[p]], ... (at most d positions, while
+ * positive and within MAX_FARDISTANCE): the one with the most equal leading bytes, counted up to
+ * KSEL and never past the pass's limit, the most recent one on a tie.  Still a function of the
+ * input alone, so the kernel's matcher computes it a tile ahead like the plain candidate.
  */
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
 /* TILE = the kernel's parse step: 128 positions, two 64-lane halves exchanged in order */
-enum { LZ_MAX_COPY = 32, LZ_NEAR = 8191, LZ_FAR = 65535 + 8191 - 1, LZ_SHIFT = 4, LZ_MINLEN = 4, TILE = 128 };
+enum { LZ_MAX_COPY = 32, LZ_NEAR = 8191, LZ_FAR = 65535 + 8191 - 1, LZ_SHIFT = 4, LZ_MINLEN = 4, TILE = 128, KSEL = 24 };
+
+static int fm_depth = 1;
+void fm_set_depth(int d) { fm_depth = d < 1 ? 1 : d; }
 
 static inline uint32_t ld32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
 static inline uint32_t lz_hash(uint32_t seq, int hashlog) { return (seq * 2654435761U) >> (32 - hashlog); }
@@ -41,13 +53,35 @@ static inline int32_t lz_match_end(const uint8_t *in, int32_t p, int32_t r, int3
   return bound;
 }
 
-static void insert_tile(const uint8_t *in, int32_t t, int32_t loop_end, int tablog, uint32_t *tab, int32_t *cand) {
+/* equal leading bytes of in[p..] and in[c..], at most KSEL and never at or past `limit` */
+static int32_t sel_len(const uint8_t *in, int32_t p, int32_t c, int32_t limit) {
+  const int32_t cap = limit - p < KSEL ? limit - p : KSEL;
+  int32_t n = 0;
+  while (n < cap && in[p + n] == in[c + n]) n++;
+  return n;
+}
+
+static void insert_tile(const uint8_t *in, int32_t t, int32_t loop_end, int32_t limit, int tablog, uint32_t *tab,
+                        int32_t *prev, int32_t *cand) {
   for (int32_t i = 0; i < TILE; i++) {
     const int32_t p = t * TILE + i;
     if (p >= loop_end) break;
     const uint32_t h = lz_hash(ld32(in + p), tablog);
-    cand[p] = (int32_t)tab[h];
+    const int32_t c1 = (int32_t)tab[h];
     tab[h] = (uint32_t)p;
+    prev[p] = c1;
+    cand[p] = c1;
+    /* a usable first candidate (0 < p - c1 < MAX_FARDISTANCE, the parse's own test) opens the chain;
+     * older links are only farther */
+    if (fm_depth < 2 || c1 <= 0 || p - c1 >= LZ_FAR) continue;
+    int32_t best = c1, bl = sel_len(in, p, c1, limit), c = c1;
+    for (int k = 1; k < fm_depth; k++) {
+      c = prev[c];
+      if (c <= 0 || p - c >= LZ_FAR) break;
+      const int32_t l = sel_len(in, p, c, limit);
+      if (l > bl) { bl = l; best = c; }
+    }
+    cand[p] = best;
   }
 }
 
@@ -61,6 +95,7 @@ static int fm_parse(const uint8_t *in, int32_t length, int tablog, int probe, in
   const int32_t bound = limit - 1, loop_end = limit - 12;
   uint32_t *tab = (uint32_t *)calloc((size_t)1 << tablog, sizeof(uint32_t));
   int32_t *cand = (int32_t *)calloc((size_t)(limit > 0 ? limit : 1) + TILE, sizeof(int32_t));
+  int32_t *prev = (int32_t *)calloc((size_t)(limit > 0 ? limit : 1) + TILE, sizeof(int32_t));
   int32_t o = 5, lit = 4, pos = probe ? 0 : 4;
   if (!probe) {
     out[0] = LZ_MAX_COPY - 1;
@@ -70,8 +105,8 @@ static int fm_parse(const uint8_t *in, int32_t length, int tablog, int probe, in
   int fail = 0;
   while (pos < loop_end && !fail) {
     const int32_t T = pos / TILE;
-    if (T > hi) { insert_tile(in, T, loop_end, tablog, tab, cand); hi = T; }
-    if (T + 1 > hi && (T + 1) * TILE < loop_end) { insert_tile(in, T + 1, loop_end, tablog, tab, cand); hi = T + 1; }
+    if (T > hi) { insert_tile(in, T, loop_end, limit, tablog, tab, prev, cand); hi = T; }
+    if (T + 1 > hi && (T + 1) * TILE < loop_end) { insert_tile(in, T + 1, loop_end, limit, tablog, tab, prev, cand); hi = T + 1; }
     while (pos < loop_end && pos < (T + 1) * TILE) {
       const int32_t anchor = pos;
       const int32_t ref = cand[anchor];
@@ -143,6 +178,7 @@ static int fm_parse(const uint8_t *in, int32_t length, int tablog, int probe, in
   }
   free(tab);
   free(cand);
+  free(prev);
   if (fail) return 0;
   if (probe) {
     *ratio = (double)pos / (double)o;
