@@ -118,6 +118,8 @@ def bind_schunk(lib):
         "blosc2_getitem_bytes_ctx": ([vp, vp, i32, i32, i32, vp, i32], C.c_int),
         "b2h_schunk_append_device": ([sp, vp, vp, i32, i64], i64),
         "b2h_schunk_decompress_device": ([sp, i64, i32, vp, i64, i32, vp], C.c_int),
+        "b2h_schunk_append_buffers": ([sp, vp, vp, i32, i64, i32], i64),
+        "b2h_schunk_decompress_buffers": ([sp, i64, i32, vp, i64, i32, vp, i32], C.c_int),
         "b2h_schunk_get_slice_device": ([sp, i64, i64, vp], C.c_int),
         "blosc2_schunk_from_buffer": ([vp, i64, C.c_bool], sp),
         "blosc2_schunk_open": ([C.c_char_p], sp),

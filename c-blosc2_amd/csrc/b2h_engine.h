@@ -146,6 +146,13 @@ int ctx_append_device(::blosc2_context_s* ctx, const uint8_t* d_src, const int32
                       int64_t src_stride, uint8_t** chunks_out);
 int ctx_decompress_device(::blosc2_context_s* ctx, const uint8_t* const* chunks, int32_t n, uint8_t* d_dst,
                           int64_t dst_stride, int32_t dst_cap, int32_t* status);
+// The multi-device fan-out (b2h_schunk_append_buffers): a context with ctx's parameters, sticky
+// blocksize and encoder mode, but device state of its own (created on the calling thread's device);
+// and the sticky-blocksize walk of n consecutive compressions, before[i] = the state chunk i starts
+// from (before[n] = the state after the last), ctx itself unchanged.
+::blosc2_context_s* ctx_clone(const ::blosc2_context_s* ctx);
+int ctx_blocksize_walk(const ::blosc2_context_s* ctx, const int32_t* nbytes, int32_t n, int32_t* before);
+void ctx_set_blocksize(::blosc2_context_s* ctx, int32_t blocksize);
 
 // Device bookkeeping
 int device_count();

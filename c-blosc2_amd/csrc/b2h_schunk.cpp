@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "../../include/b2h.h"
@@ -586,6 +587,140 @@ int b2h_schunk_get_slice_device(blosc2_schunk* schunk, int64_t start, int64_t st
     schunk->current_nchunk = f1;
   }
   return 0;
+}
+
+// ------------------------------------------------------------ multi-device fan-out ----
+// The reference's C callers loop over chunks (blosc2_schunk_append_buffer /
+// blosc2_schunk_decompress_chunk, blosc/schunk.c:1459-1530) and its thread pool spreads each chunk's
+// blocks over cores.  Here a C caller hands over many chunks at once and they are spread over the
+// node's GPUs: `workers` host threads, worker k on device k % device_count, each with its own
+// contexts (stream, workspace) and a contiguous range of the chunks.  No collective: chunks are
+// independent.  Worker k's compression context starts from the sticky blocksize the serial calls
+// would have reached at its first chunk (ctx_blocksize_walk), so every chunk equals the serial
+// call's bytes and the super-chunk's context ends in the serial state.
+namespace {
+int fanout_workers(int32_t ndevices, int32_t n) {
+  const int nd = b2h::device_count();
+  if (nd <= 0) return 0;
+  const int w = ndevices > 0 ? ndevices : nd;
+  return std::max(1, std::min(w, (int)std::max<int32_t>(n, 1)));
+}
+}  // namespace
+
+int64_t b2h_schunk_append_buffers(blosc2_schunk* schunk, const void* src, const int32_t* nbytes, int32_t n,
+                                  int64_t src_stride, int32_t ndevices) {
+  if (!schunk || (n > 0 && (!src || !nbytes))) return BLOSC2_ERROR_NULL_POINTER;
+  if (n < 0 || src_stride < 0) return BLOSC2_ERROR_INVALID_PARAM;
+  if (n == 0) return schunk->nchunks;
+  for (int32_t i = 0; i < n; i++)
+    if (nbytes[i] < 0 || nbytes[i] > BLOSC2_MAX_BUFFERSIZE || (int64_t)nbytes[i] > src_stride)
+      return BLOSC2_ERROR_INVALID_PARAM;
+  const int W = fanout_workers(ndevices, n);
+  if (W == 0) {
+    TRACE_ERROR("no HIP device available: the MI355X engine has no CPU fallback");
+    return BLOSC2_ERROR_FAILURE;
+  }
+  const uint8_t* h = static_cast<const uint8_t*>(src);
+  std::vector<int32_t> before((size_t)n + 1);
+  int rc = b2h::ctx_blocksize_walk(schunk->cctx, nbytes, n, before.data());
+  if (rc < 0) return rc;
+  std::vector<uint8_t*> chunks((size_t)n, nullptr);
+  std::vector<int> wrc((size_t)W, 0);
+  auto work = [&](int k) {
+    const int32_t i0 = (int32_t)((int64_t)n * k / W), i1 = (int32_t)((int64_t)n * (k + 1) / W);
+    if (i1 <= i0) return;
+    if (hipSetDevice(k % b2h::device_count()) != hipSuccess) { wrc[k] = BLOSC2_ERROR_FAILURE; return; }
+    blosc2_context* ctx = b2h::ctx_clone(schunk->cctx);
+    if (!ctx) { wrc[k] = BLOSC2_ERROR_MEMORY_ALLOC; return; }
+    b2h::ctx_set_blocksize(ctx, before[i0]);
+    uint8_t* d = nullptr;
+    const size_t bytes = (size_t)(i1 - i0) * (size_t)src_stride;
+    if (hipMalloc(&d, std::max<size_t>(bytes, 1)) != hipSuccess) {
+      wrc[k] = BLOSC2_ERROR_MEMORY_ALLOC;
+    } else if (hipMemcpy(d, h + (int64_t)i0 * src_stride, bytes, hipMemcpyHostToDevice) != hipSuccess) {
+      wrc[k] = BLOSC2_ERROR_FAILURE;
+    } else {
+      wrc[k] = b2h::ctx_append_device(ctx, d, nbytes + i0, i1 - i0, src_stride, chunks.data() + i0);
+    }
+    if (d) (void)hipFree(d);
+    blosc2_free_ctx(ctx);
+  };
+  std::vector<std::thread> th;
+  for (int k = 1; k < W; k++) th.emplace_back(work, k);
+  work(0);
+  for (auto& t : th) t.join();
+  rc = 0;
+  for (int k = 0; k < W && rc == 0; k++) rc = wrc[k];
+  if (rc == BLOSC2_ERROR_FILTER_PIPELINE) {   // user filters / codecs: the serial calls, through host memory
+    for (uint8_t* c : chunks) free(c);
+    int64_t r = schunk->nchunks;
+    for (int32_t i = 0; i < n && r >= 0; i++) r = blosc2_schunk_append_buffer(schunk, h + (int64_t)i * src_stride, nbytes[i]);
+    return r;
+  }
+  if (rc < 0) {
+    for (uint8_t* c : chunks) free(c);
+    return rc;
+  }
+  b2h::ctx_set_blocksize(schunk->cctx, before[n]);
+  int64_t r = schunk->nchunks;
+  for (int32_t i = 0; i < n; i++) {
+    r = blosc2_schunk_append_chunk(schunk, chunks[i], false);
+    if (r < 0) {
+      for (int32_t j = i; j < n; j++) free(chunks[j]);
+      return r;
+    }
+  }
+  return r;
+}
+
+int b2h_schunk_decompress_buffers(blosc2_schunk* schunk, int64_t nchunk, int32_t n, void* dst, int64_t dst_stride,
+                                  int32_t dst_capacity, int32_t* status, int32_t ndevices) {
+  if (!schunk || (n > 0 && !dst)) return BLOSC2_ERROR_NULL_POINTER;
+  if (n < 0 || nchunk < 0 || nchunk + n > schunk->nchunks || dst_capacity < 0 || dst_stride < dst_capacity) {
+    TRACE_ERROR("chunks [%lld, %lld) are outside the super-chunk (%lld chunks) or the strides do not fit",
+                (long long)nchunk, (long long)(nchunk + n), (long long)schunk->nchunks);
+    return BLOSC2_ERROR_INVALID_PARAM;
+  }
+  if (n == 0) return 0;
+  const int W = fanout_workers(ndevices, n);
+  if (W == 0) {
+    TRACE_ERROR("no HIP device available: the MI355X engine has no CPU fallback");
+    return BLOSC2_ERROR_FAILURE;
+  }
+  uint8_t* out = static_cast<uint8_t*>(dst);
+  blosc2_dparams dp;
+  int rc = blosc2_ctx_get_dparams(schunk->dctx, &dp);
+  if (rc < 0) return rc;
+  std::vector<int32_t> st((size_t)n, BLOSC2_ERROR_FAILURE);
+  std::vector<int> wrc((size_t)W, 0);
+  auto work = [&](int k) {
+    const int32_t i0 = (int32_t)((int64_t)n * k / W), i1 = (int32_t)((int64_t)n * (k + 1) / W);
+    if (i1 <= i0) return;
+    if (hipSetDevice(k % b2h::device_count()) != hipSuccess) { wrc[k] = BLOSC2_ERROR_FAILURE; return; }
+    blosc2_context* ctx = blosc2_create_dctx(dp);
+    if (!ctx) { wrc[k] = BLOSC2_ERROR_MEMORY_ALLOC; return; }
+    uint8_t* d = nullptr;
+    const size_t bytes = (size_t)(i1 - i0) * (size_t)dst_stride;
+    if (hipMalloc(&d, std::max<size_t>(bytes, 1)) != hipSuccess) {
+      wrc[k] = BLOSC2_ERROR_MEMORY_ALLOC;
+    } else {
+      wrc[k] = b2h::ctx_decompress_device(ctx, schunk->data + nchunk + i0, i1 - i0, d, dst_stride, dst_capacity,
+                                          st.data() + i0);
+      if (wrc[k] >= 0 && hipMemcpy(out + (int64_t)i0 * dst_stride, d, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+        wrc[k] = BLOSC2_ERROR_FAILURE;
+    }
+    if (d) (void)hipFree(d);
+    blosc2_free_ctx(ctx);
+  };
+  std::vector<std::thread> th;
+  for (int k = 1; k < W; k++) th.emplace_back(work, k);
+  work(0);
+  for (auto& t : th) t.join();
+  rc = 0;
+  for (int k = 0; k < W && rc == 0; k++) rc = wrc[k];
+  if (status) memcpy(status, st.data(), sizeof(int32_t) * (size_t)n);
+  schunk->current_nchunk = nchunk + n - 1;
+  return rc;
 }
 
 // ------------------------------------------------------------------------ slice writes ----

@@ -935,6 +935,56 @@ static int compress_device_locked(blosc2_context* ctx, const uint8_t* d_src, con
   return 0;
 }
 
+blosc2_context* ctx_clone(const blosc2_context* ctx) {
+  if (!ctx) return nullptr;
+  blosc2_context* c = new (std::nothrow) blosc2_context();
+  if (!c) return nullptr;
+  c->do_compress = ctx->do_compress;
+  c->compcode = ctx->compcode;
+  c->compcode_meta = ctx->compcode_meta;
+  c->clevel = ctx->clevel;
+  c->use_dict = ctx->use_dict;
+  c->typesize = ctx->typesize;
+  c->nthreads = ctx->nthreads;
+  c->blocksize = ctx->blocksize;
+  c->splitmode = ctx->splitmode;
+  c->schunk = ctx->schunk;
+  memcpy(c->filters, ctx->filters, sizeof c->filters);
+  memcpy(c->filters_meta, ctx->filters_meta, sizeof c->filters_meta);
+  c->prefilter = ctx->prefilter;
+  c->preparams = ctx->preparams;
+  c->tuner_params = ctx->tuner_params;
+  c->tuner_id = ctx->tuner_id;
+  c->instr_codec = ctx->instr_codec;
+  c->codec_params = ctx->codec_params;
+  c->lz_mode = ctx->lz_mode;
+  memcpy(c->filter_params, ctx->filter_params, sizeof c->filter_params);
+  c->dparams = ctx->dparams;
+  return c;
+}
+
+int ctx_blocksize_walk(const blosc2_context* ctx, const int32_t* nbytes, int32_t n, int32_t* before) {
+  if (!ctx || !before || (n > 0 && !nbytes)) return BLOSC2_ERROR_NULL_POINTER;
+  int32_t state = ctx->blocksize;
+  for (int32_t i = 0; i < n; i++) {
+    before[i] = state;
+    b2h::CompressPlan plan;
+    int32_t computed = 0;
+    const int rc = b2h::make_compress_plan(&plan, nbytes[i], nbytes[i] + BLOSC2_MAX_OVERHEAD, ctx->clevel, ctx->typesize,
+                                           state, ctx->splitmode, ctx->filters, ctx->filters_meta, &computed, true,
+                                           ctx->compcode, ctx->compcode_meta, 1, ctx->use_dict);
+    if (rc < 0) return rc;
+    state = computed;
+  }
+  before[n] = state;
+  return 0;
+}
+
+void ctx_set_blocksize(blosc2_context* ctx, int32_t blocksize) {
+  std::lock_guard<std::mutex> g(ctx->mu);
+  ctx->blocksize = blocksize;
+}
+
 int ctx_compress_device(blosc2_context* ctx, const uint8_t* d_src, const int32_t* nbytes, int32_t n,
                         int64_t src_stride, uint8_t* d_dst, int64_t dst_stride, int32_t* d_cbytes) {
   if (!ctx) return BLOSC2_ERROR_NULL_POINTER;

@@ -144,6 +144,22 @@ BLOSC_EXPORT int b2h_schunk_decompress_device(blosc2_schunk *schunk, int64_t nch
 BLOSC_EXPORT int b2h_schunk_get_slice_device(blosc2_schunk *schunk, int64_t start, int64_t stop, void *d_dst);
 BLOSC_EXPORT int b2h_schunk_set_slice_device(blosc2_schunk *schunk, int64_t start, int64_t stop, const void *d_src);
 
+/* Multi-GPU fan-out from C.  n blosc2_schunk_append_buffer calls (reference blosc/schunk.c:1459-1477)
+ * from HOST buffers (chunk i = src + i * src_stride, nbytes[i] bytes), spread over the node's GPUs:
+ * `ndevices` workers (<= 0: one per visible device; more workers than devices share them round
+ * robin), worker k compressing a contiguous range of the chunks on device k % count with its own
+ * stream and workspace.  The chunks are appended in order and equal the serial calls' bytes (each
+ * worker starts from the sticky blocksize the serial walk reaches at its first chunk).  Returns the
+ * new number of chunks, or a negative error with nothing appended. */
+BLOSC_EXPORT int64_t b2h_schunk_append_buffers(blosc2_schunk *schunk, const void *src, const int32_t *nbytes,
+                                               int32_t n, int64_t src_stride, int32_t ndevices);
+/* Chunks [nchunk, nchunk + n) into HOST dst + i * dst_stride (capacity dst_capacity each), spread the
+ * same way; status[i] (optional) = what blosc2_schunk_decompress_chunk (schunk.c:1481-1530) returns
+ * for chunk nchunk + i.  Returns 0 or the first worker's error. */
+BLOSC_EXPORT int b2h_schunk_decompress_buffers(blosc2_schunk *schunk, int64_t nchunk, int32_t n, void *dst,
+                                               int64_t dst_stride, int32_t dst_capacity, int32_t *status,
+                                               int32_t ndevices);
+
 /* Per-context BloscLZ encoder mode.  Built-in BloscLZ does not read blosc2_cparams.codec_params
  * (reference include/blosc2.h:1207; only user codecs receive it), so a context selects its encoder
  * by pointing codec_params at one of these when it is created (blosc2_create_cctx copies the mode;
