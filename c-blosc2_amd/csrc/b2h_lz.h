@@ -1293,16 +1293,20 @@ __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, 
       }
       DPROF_T(t4);
       // ---- 4b. matches ----
-      // Matches whose whole source precedes the batch (src + len <= op, in the ring, <= 64 bytes)
-      // read nothing this batch writes: their ring reads go out four at a time, ahead of the
-      // writes (62 % of T's fast-mode matches); the others follow in order, after them.
-      const bool indep = inb && !lit && olen <= 64 && dist >= ex + olen && op + ex - dist >= F;
+      // Matches whose whole source precedes the batch (src + len <= op, <= 64 bytes) read nothing
+      // this batch writes: their reads go out eight at a time, ahead of the writes -- from the
+      // ring (62 % of T's fast-mode matches), or from `out` when the source has already left the
+      // ring (src + len <= F: far matches, 41 % of T's exact-mode matches, which one at a time
+      // through copy_general cost a global round trip each); the others follow in order, after.
+      const int32_t srcv = op + ex - dist;
+      const bool indep = inb && !lit && olen <= 64 && dist >= ex + olen && (srcv >= F || srcv + olen <= F);
       uint64_t im = __ballot(indep);
+      if (__ballot(indep && srcv < F)) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // as copy_general
       while (im) {
-        int32_t oj[4], lj[4], sj[4];
-        uint8_t vb[4];
+        int32_t oj[8], lj[8], sj[8];
+        uint8_t vb[8];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < 8; u++) {
           lj[u] = 0;
           oj[u] = 0;
           sj[u] = 0;
@@ -1315,9 +1319,10 @@ __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, 
           }
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) vb[u] = lane < lj[u] ? ring[(sj[u] + lane) & RM] : (uint8_t)0;
+        for (int u = 0; u < 8; u++)
+          vb[u] = lane < lj[u] ? (sj[u] >= F ? ring[(sj[u] + lane) & RM] : out[sj[u] + lane]) : (uint8_t)0;
 #pragma unroll
-        for (int u = 0; u < 4; u++)
+        for (int u = 0; u < 8; u++)
           if (lane < lj[u]) ring[(oj[u] + lane) & RM] = vb[u];
       }
       uint64_t mm = batch & ~__ballot(lit) & ~__ballot(indep);
