@@ -1277,7 +1277,8 @@ __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, 
     if (batch) {
       if (nop - F > R) F = flush_to<RLOG>(ring, out, nop, F);
       // ---- 4a. literal bytes: byte lane x belongs to the last batch token at or before it ----
-      const int32_t owner = wave_scan_max(inb ? lane : -1);
+      const bool inbt = (batch >> lane) & 1ull;   // `batch` after the violation cut (`inb` is before it)
+      const int32_t owner = wave_scan_max(inbt ? lane : -1);
       const uint32_t opk = (uint32_t)(ex << 6) | (uint32_t)(lit ? olen : 0);   // ex < 2^13, run <= 32
       const uint32_t ow_pk = (uint32_t)__shfl((int)opk, owner & 63);
       const int32_t orun = (int32_t)(ow_pk & 63u), oex = (int32_t)(ow_pk >> 6);
@@ -1299,7 +1300,7 @@ __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, 
       // ring (src + len <= F: far matches, 41 % of T's exact-mode matches, which one at a time
       // through copy_general cost a global round trip each); the others follow in order, after.
       const int32_t srcv = op + ex - dist;
-      const bool indep = inb && !lit && olen <= 64 && dist >= ex + olen && (srcv >= F || srcv + olen <= F);
+      const bool indep = inbt && !lit && olen <= 64 && dist >= ex + olen && (srcv >= F || srcv + olen <= F);
       uint64_t im = __ballot(indep);
       if (__ballot(indep && srcv < F)) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // as copy_general
       while (im) {
