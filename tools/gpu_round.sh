@@ -22,10 +22,14 @@ for mode in fast exact; do
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rp_${TAG}_$mode -o run -- python3 -u $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --lz-mode $mode > $O/rp_${TAG}_$mode.log 2>&1 || { echo "rocprof failed"; tail -30 $O/rp_${TAG}_$mode.log; exit 1; }
   tail -1 $O/rp_${TAG}_$mode.log | cut -c1-300
 done
-for ctr in FETCH_SIZE WRITE_SIZE; do
-  echo "pmc $ctr..."
-  timeout -s KILL 200 rocprofv3 --pmc $ctr --kernel-include-regex "k_encode|k_decode|k_ffilter|k_dfilter|k_scatter" --output-format csv \
-      -d $O/pmc_${TAG}_$ctr -o run -- python3 -u $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --lz-mode fast > $O/pmc_${TAG}_$ctr.log 2>&1 || { echo "pmc $ctr failed"; tail -20 $O/pmc_${TAG}_$ctr.log; exit 1; }
+# HBM traffic per launch, fast mode (tag TAG) and exact mode (tag TAGx)
+for mode in fast exact; do
+  T=$TAG; [ $mode = exact ] && T=${TAG}x
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    echo "pmc $mode $ctr..."
+    timeout -s KILL 200 rocprofv3 --pmc $ctr --kernel-include-regex "k_encode|k_decode|k_ffilter|k_dfilter|k_scatter" --output-format csv \
+        -d $O/pmc_${T}_$ctr -o run -- python3 -u $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --lz-mode $mode > $O/pmc_${T}_$ctr.log 2>&1 || { echo "pmc $ctr failed"; tail -20 $O/pmc_${T}_$ctr.log; exit 1; }
+  done
+  python3 $R/tools/pmc_traffic.py $O $T $O/pmc_traffic_$T.json $mode > /dev/null && echo "traffic summary: gpurun_out/pmc_traffic_$T.json"
 done
-python3 $R/tools/pmc_traffic.py $O $TAG $O/pmc_traffic_$TAG.json fast > /dev/null && echo "traffic summary: gpurun_out/pmc_traffic_$TAG.json"
 echo DONE
