@@ -533,7 +533,8 @@ __host__ __device__ constexpr size_t enc_wg_lds(int hashlog, int nlds, int nglb)
 }
 
 template <typename POS, int NLDS, int NGLB>
-__global__ __launch_bounds__(64 * (NLDS + NGLB)) void k_encode(EncArgs args, POS* __restrict__ gtab) {
+__global__ __launch_bounds__(64 * (NLDS + NGLB)) __attribute__((amdgpu_waves_per_eu(3, 8)))   // <= 168 VGPRs (kExWords)
+void k_encode(EncArgs args, POS* __restrict__ gtab) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int hashlog = args.g.clevel == 1 ? 12 : (args.g.clevel == 2 ? 13 : 14);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1984,7 +1985,8 @@ __device__ void encode_loop_fused(const CGeom& g, TAB htab, B2H_LDS uint32_t* db
 }
 
 template <typename POS, int NLDS, int NGLB>
-__global__ __launch_bounds__(64 * (NLDS + NGLB)) void k_encode_fused(CGeom g, const uint8_t* __restrict__ filt,
+__global__ __launch_bounds__(64 * (NLDS + NGLB)) __attribute__((amdgpu_waves_per_eu(3, 8)))
+void k_encode_fused(CGeom g, const uint8_t* __restrict__ filt,
                                                                      uint8_t* __restrict__ sbuf,
                                                                      StreamResult* __restrict__ res,
                                                                      int32_t nstreams_total, int32_t* __restrict__ next,

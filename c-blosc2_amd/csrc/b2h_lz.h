@@ -7,7 +7,7 @@
 //     loop's candidate for every lane below W, the first lane whose hash bucket already occurs at
 //     an earlier lane of the window (found exactly with one LDS atomic-or per lane on a
 //     one-bit-per-bucket table).
-//   * every lane tests its candidate (a 28-byte compare) and decides literal / match exactly as
+//   * every lane tests its candidate (a 60-byte compare) and decides literal / match exactly as
 //     the serial loop would; `__ballot` yields the accepted-match mask.
 //   * a short scalar chain walk picks the matches the serial loop takes (first accepted lane,
 //     then the first accepted lane at or after that match's end + 2, ...) while they stay below
@@ -139,16 +139,22 @@ __device__ __forceinline__ void ld16(gin_t p, uint32_t (&w)[4]) {
   w[3] = funnel(d, e, sh);
 }
 
-// 28 unaligned bytes as seven words (8 dword loads).
-__device__ __forceinline__ void ld28(gin_t p, uint32_t (&w)[7]) {
+// 4N unaligned bytes as N words (N + 1 dword loads).
+template <int N>
+__device__ __forceinline__ void ldw(gin_t p, uint32_t (&w)[N]) {
   const B2H_GLB uint32_t* q = align4(p);
   const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
-  uint32_t d[8];
+  uint32_t d[N + 1];
 #pragma unroll
-  for (int i = 0; i < 8; i++) d[i] = q[i];
+  for (int i = 0; i < N + 1; i++) d[i] = q[i];
 #pragma unroll
-  for (int i = 0; i < 7; i++) w[i] = funnel(d[i], d[i + 1], sh);
+  for (int i = 0; i < N; i++) w[i] = funnel(d[i], d[i + 1], sh);
 }
+// Exact mode's up-front compare: kExWords words per lane and candidate.  60 bytes (15 words): a
+// match the compare does not end needs a cooperative extension through memory (one round trip);
+// with 28 bytes that was half of T's matches.  The wave can afford the registers: the encoder's
+// workgroup shape is LDS-bound at 3 waves per SIMD (k_encode's waves_per_eu).
+constexpr int kExWords = 15, kExBytes = 4 * kExWords;
 
 
 __device__ __forceinline__ int32_t rdlane(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -348,8 +354,8 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t __restrict__ in, int32_t leng
     const int32_t P = pos;
     const int32_t p = P + lane;
     const bool valid = p < loop_end;
-    uint32_t a[7] = {0, 0, 0, 0, 0, 0, 0};   // in[p .. p+27]
-    if (valid) ld28(in + p, a);
+    uint32_t a[kExWords] = {};   // in[p .. p + kExBytes - 1]
+    if (valid) ldw<kExWords>(in + p, a);
     const uint32_t v = a[0];
     EPROF_T(t1);
     const uint32_t h = lz_hash(v, hashlog);
@@ -378,23 +384,23 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t __restrict__ in, int32_t leng
     // candidate test (lanes < W): literal or match, exactly as the serial loop decides
     const uint32_t cand = same1 ? (uint32_t)(p - 1) : c0;
     const uint32_t dist = (uint32_t)(p - (int32_t)cand);
-    // 28 bytes are compared up front; only longer matches need the cooperative extension
+    // kExBytes are compared up front; only longer matches need the cooperative extension
     bool accept = false;
-    int32_t lenx = 0;   // match length, or -1: the first 28 bytes all match (extend later)
+    int32_t lenx = 0;   // match length, or -1: the first kExBytes bytes all match (extend later)
     if (lane < W && dist != 0 && dist < kLzFar) {
-      uint32_t rr[7];
-      ld28(in + cand, rr);
+      uint32_t rr[kExWords];
+      ldw<kExWords>(in + cand, rr);
       if (rr[0] == v) {
-        int32_t mm = 28;   // index of the first mismatching byte
+        int32_t mm = kExBytes;   // index of the first mismatching byte
 #pragma unroll
-        for (int i = 6; i >= 1; i--) {
+        for (int i = kExWords - 1; i >= 1; i--) {
           const uint32_t x = a[i] ^ rr[i];
           if (x) mm = 4 * i + (__builtin_ctz(x) >> 3);
         }
-        const int32_t e = min(mm < 28 ? p + mm + 1 : 0x7fffffff, bound);
+        const int32_t e = min(mm < kExBytes ? p + mm + 1 : 0x7fffffff, bound);
         const int32_t len = e - 4 - p;
         accept = len >= 4 && (PROBE || !(len <= 5 && (dist - 1) >= kLzNear));
-        lenx = (mm < 28 || p + 29 >= bound) ? len : -1;
+        lenx = (mm < kExBytes || p + kExBytes + 1 >= bound) ? len : -1;
       }
     }
     const uint64_t am = __ballot(accept);
@@ -441,7 +447,7 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t __restrict__ in, int32_t leng
         int32_t lm = rdlane(lenx, m);
         if (lm < 0) {
           EPROF_T(te0);
-          lm = wave_match_end(in, P + m + 28, (uint32_t)rdlane((int32_t)dist, m), bound) - 4 - (P + m);
+          lm = wave_match_end(in, P + m + kExBytes, (uint32_t)rdlane((int32_t)dist, m), bound) - 4 - (P + m);
           lenx = lane == m ? lm : lenx;
           EPROF_T(te1);
           EPROF_ADD(5, te0, te1);
