@@ -1369,6 +1369,7 @@ struct EncFuse {
   int32_t nchunks, lead;
   int32_t* trace;          // debug (B2H_FUSE_TRACE): per workgroup, the phase it is in (host memory)
   int32_t mode_bits;       // fuse_bits()
+  int32_t ds;              // raw's filter job: 0 the typesize-4 SHUFFLE, 2/4/8 (DELTA, SHUFFLE) at that typesize
 };
 constexpr int32_t kFuseHdr = 16;   // [0] shuffle claims [1] scatter claims [2] ready slots [3] published items [4] timeouts
 constexpr int32_t kFuseSpi = 8;    // streams per scatter item
@@ -1444,6 +1445,67 @@ __device__ void shuffle4_block_wt(const uint8_t* __restrict__ s, uint8_t* __rest
       }
     }
   }
+}
+
+// (DELTA, SHUFFLE) of one block by the workgroup (or one wave: tid / nth), the planes' dwords
+// stored write-through: the fused launch's filter job for k_ffilter_ds's pipeline (the same
+// arithmetic as delta_shuffle_fast: block 0 XORs each element with the previous one, the other
+// blocks with the same element of the chunk's raw block 0, blosc/delta.c:18-92; then the byte
+// shuffle, shuffle-generic.h:34-55).  Whole quads, 16-byte aligned (checked by the host).
+template <int TS>
+__device__ void ds_block_wt(const uint8_t* __restrict__ src, const uint8_t* __restrict__ dref, uint8_t* __restrict__ dst,
+                            int32_t n, bool first_block, int32_t tid, int32_t nth) {
+  const int32_t quads = n / 4;
+  const __amdgpu_buffer_rsrc_t r = wt_rsrc((gout_t)dst);
+  constexpr int EW = TS / 4 > 0 ? TS / 4 : 1;   // u32 words per element (TS 2: half a word)
+  for (int32_t q = tid; q < quads; q += nth) {
+    uint32_t w[TS], x[TS];
+    load_words<TS>(src, q, w);
+    if (first_block) {
+      if constexpr (TS == 2) {
+        const uint32_t pe = q ? (uint32_t)reinterpret_cast<const uint16_t*>(src)[4 * (int64_t)q - 1] : 0u;
+        x[0] = (w[0] << 16) | pe;
+        x[1] = (w[1] << 16) | (w[0] >> 16);
+      } else {
+        uint32_t prev[EW];
+#pragma unroll
+        for (int k = 0; k < EW; k++) prev[k] = q ? reinterpret_cast<const uint32_t*>(src)[(int64_t)q * TS - EW + k] : 0u;
+#pragma unroll
+        for (int k = 0; k < TS; k++) x[k] = k < EW ? prev[k] : w[k - EW];
+      }
+    } else {
+      load_words<TS>(dref, q, x);
+    }
+#pragma unroll
+    for (int k = 0; k < TS; k++) w[k] ^= x[k];
+#pragma unroll
+    for (int plane = 0; plane < TS; plane++) {
+      uint32_t o = 0;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int byte = e * TS + plane;
+        o |= ((w[byte / 4] >> (8 * (byte % 4))) & 0xffu) << (8 * e);
+      }
+      __builtin_amdgcn_raw_buffer_store_b32(o, r, plane * n + 4 * q, 0, 16);
+    }
+  }
+}
+
+// The fused launch's filter job for global block k = chunk cc, block b.  The (DELTA, SHUFFLE) job
+// is an out-of-line call: inlined, it cost T's shuffle-only launch 0.1 ms (register allocation).
+__device__ __noinline__ void fuse_ds_block(const uint8_t* chunk, uint8_t* d, int32_t ts, int32_t b, int32_t bsize,
+                                           int32_t bs, int32_t tid, int32_t nth) {
+  const uint8_t* s = chunk + (int64_t)b * bs;
+  if (ts == 8) ds_block_wt<8>(s, chunk, d, bsize / 8, b == 0, tid, nth);
+  else if (ts == 4) ds_block_wt<4>(s, chunk, d, bsize / 4, b == 0, tid, nth);
+  else ds_block_wt<2>(s, chunk, d, bsize / 2, b == 0, tid, nth);
+}
+__device__ __forceinline__ void fuse_filter_block(const EncFuse& f, const CGeom& g, int32_t cc, int32_t b, int32_t bsize,
+                                                  int32_t tid, int32_t nth) {
+  const uint8_t* chunk = f.raw + (int64_t)cc * f.raw_stride;
+  uint8_t* d = f.filt + (int64_t)cc * g.wstride + (int64_t)b * g.bs;
+  if (f.ds == 0) shuffle4_block_wt(chunk + (int64_t)b * g.bs, d, bsize, tid, nth);
+  else fuse_ds_block(chunk, d, f.ds, b, bsize, g.bs, tid, nth);
 }
 
 // The fused kernel's arguments, staged in LDS at launch and read back (as wave-uniform values) in
@@ -1605,8 +1667,7 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
           const EncFuse fk = lds_uniform(&A->f);
           const int32_t cc = k / gk.nblocks, b = k - cc * gk.nblocks;
           const int32_t bsize = (b == gk.nblocks - 1 && gk.leftover) ? gk.leftover : gk.bs;
-          shuffle4_block_wt(fk.raw + (int64_t)cc * fk.raw_stride + (int64_t)b * gk.bs,
-                            fk.filt + (int64_t)cc * gk.wstride + (int64_t)b * gk.bs, bsize);
+          fuse_filter_block(fk, gk, cc, b, bsize, threadIdx.x, blockDim.x);
           drain_stores();
           __syncthreads();
           int32_t nk = -1;
@@ -1891,8 +1952,7 @@ __device__ void encode_loop_fused(const CGeom& g, TAB htab, B2H_LDS uint32_t* db
       while (k >= 0 && k < nblk) {
         const int32_t cc = k / g.nblocks, b = k - cc * g.nblocks;
         const int32_t bsize = (b == g.nblocks - 1 && g.leftover) ? g.leftover : g.bs;
-        shuffle4_block_wt(f.raw + (int64_t)cc * f.raw_stride + (int64_t)b * g.bs,
-                          f.filt + (int64_t)cc * g.wstride + (int64_t)b * g.bs, bsize, lane, 64);
+        fuse_filter_block(f, g, cc, b, bsize, lane, 64);
         drain_stores();
         if (lane == 0) st_agent(blk_ready + k, 1);
         k = claim_block(target);
@@ -2253,7 +2313,8 @@ static CGeom make_geom(const CompressPlan& P, int64_t src_stride, int64_t dst_st
 
 static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const uint8_t* filt, const uint8_t* raw,
                         int64_t raw_stride, uint8_t* d_dst, int64_t dst_stride, int32_t* d_cbytes, int32_t nchunks,
-                        const uint8_t* htpl, int64_t ntot, hipStream_t st, const uint8_t* fuse_raw = nullptr);
+                        const uint8_t* htpl, int64_t ntot, hipStream_t st, const uint8_t* fuse_raw = nullptr,
+                        int fuse_ds_ts = 0);
 
 int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stride, int32_t nchunks, uint8_t* d_dst,
                    int64_t dst_stride, int32_t* d_cbytes, hipStream_t st, Workspace* wsx) {
@@ -2382,7 +2443,11 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
                             g.bs % 64 == 0 && g.leftover % 64 == 0 && !clobber && g.dict_size == 0 &&
                             (reinterpret_cast<uintptr_t>(raw) & 15) == 0 && raw_stride % 16 == 0 &&
                             (fuse_bits() & 2) && fused_encode_ok(g);
-  if (fuse_shuffle) {
+  // and (DELTA, SHUFFLE) at typesize 2/4/8 too (k_ffilter_ds's job, whole 64-byte groups)
+  const bool fuse_dsjob = !fuse_shuffle && fuse_ds && g.bs % 64 == 0 && g.leftover % 64 == 0 && !clobber &&
+                          g.dict_size == 0 && (reinterpret_cast<uintptr_t>(raw) & 15) == 0 && raw_stride % 16 == 0 &&
+                          (fuse_bits() & 2) && fused_encode_ok(g);
+  if (fuse_shuffle || fuse_dsjob) {
     filt = ring[0];
     filt_stride = g.wstride;
   } else if ((rc = run_filters())) {
@@ -2407,14 +2472,14 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
   ev_filter.stop(st);
   HIPCHK(hipGetLastError());
   return encode_stage(ws, P, g, filt, raw, raw_stride, d_dst, dst_stride, d_cbytes, nchunks, htpl, ntot, st,
-                      fuse_shuffle ? raw : nullptr);
+                      (fuse_shuffle || fuse_dsjob) ? raw : nullptr, fuse_dsjob ? g.ts : 0);
 }
 
 // The codec stage of a batch whose filtered images sit at filt + c * g.wstride: encode every stream,
 // then the serial-layout finalisation, the payload scatter and the memcpy fallbacks (from raw).
 static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const uint8_t* filt, const uint8_t* raw,
                         int64_t raw_stride, uint8_t* d_dst, int64_t dst_stride, int32_t* d_cbytes, int32_t nchunks,
-                        const uint8_t* htpl, int64_t ntot, hipStream_t st, const uint8_t* fuse_raw) {
+                        const uint8_t* htpl, int64_t ntot, hipStream_t st, const uint8_t* fuse_raw, int fuse_ds_ts) {
   const int32_t n = P.nbytes;
   int rc = 0;
   // encode
@@ -2443,6 +2508,7 @@ static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const ui
     if (fused) {
       EncFuse f{};
       f.raw = fuse_raw;
+      f.ds = fuse_ds_ts;
       f.raw_stride = raw_stride;
       f.filt = const_cast<uint8_t*>(filt);
       f.place = ws->place.as<Place>();
