@@ -296,13 +296,27 @@ int blosc2_schunk_free(blosc2_schunk* schunk) {
 }
 
 // ---------------------------------------------------------------------- chunk index ops ----
+// A handle attached to a contiguous frame (blosc2_schunk_open / _from_buffer(copy = false),
+// b2h_frame.cpp) holds the frame's chunks in host memory; the reference's writes go back to the
+// frame (frame_append_chunk etc.), which this engine does not write.  Such handles are read-only:
+// every write entry point refuses them instead of changing only the in-memory copy.
+static int refuse_if_attached(const blosc2_schunk* s, const char* fn) {
+  if (s->storage && (s->storage->contiguous || s->storage->urlpath)) {
+    TRACE_ERROR("%s: super-chunks attached to a frame are read-only in the MI355X engine", fn);
+    return BLOSC2_ERROR_INVALID_PARAM;
+  }
+  return 0;
+}
+
 int64_t blosc2_schunk_append_chunk(blosc2_schunk* schunk, uint8_t* chunk, bool copy) {
   if (!schunk) return BLOSC2_ERROR_NULL_POINTER;
+  if (int rc0 = refuse_if_attached(schunk, "blosc2_schunk_append_chunk")) return rc0;
   return put_chunk(schunk, kAppend, schunk->nchunks, chunk, copy);
 }
 
 int64_t blosc2_schunk_insert_chunk(blosc2_schunk* schunk, int64_t nchunk, uint8_t* chunk, bool copy) {
   if (!schunk) return BLOSC2_ERROR_NULL_POINTER;
+  if (int rc0 = refuse_if_attached(schunk, "blosc2_schunk_insert_chunk")) return rc0;
   const int rc = validate_nchunk(schunk, nchunk, true, "blosc2_schunk_insert_chunk");
   if (rc < 0) return rc;
   return put_chunk(schunk, kInsert, nchunk, chunk, copy);
@@ -311,6 +325,7 @@ int64_t blosc2_schunk_insert_chunk(blosc2_schunk* schunk, int64_t nchunk, uint8_
 // schunk.c:1235-1360
 int64_t blosc2_schunk_update_chunk(blosc2_schunk* schunk, int64_t nchunk, uint8_t* chunk, bool copy) {
   if (!schunk || !chunk) return BLOSC2_ERROR_NULL_POINTER;
+  if (int rc0 = refuse_if_attached(schunk, "blosc2_schunk_update_chunk")) return rc0;
   int rc = validate_nchunk(schunk, nchunk, false, "blosc2_schunk_update_chunk");
   if (rc < 0) return rc;
   ChunkInfo ci;
@@ -334,6 +349,7 @@ int64_t blosc2_schunk_update_chunk(blosc2_schunk* schunk, int64_t nchunk, uint8_
 // schunk.c:1375-1442
 int64_t blosc2_schunk_delete_chunk(blosc2_schunk* schunk, int64_t nchunk) {
   if (!schunk) return BLOSC2_ERROR_NULL_POINTER;
+  if (int rc0 = refuse_if_attached(schunk, "blosc2_schunk_delete_chunk")) return rc0;
   const int rc = validate_nchunk(schunk, nchunk, false, "blosc2_schunk_delete_chunk");
   if (rc < 0) return rc;
   int32_t nb_old, cb_old;
@@ -353,6 +369,7 @@ int64_t blosc2_schunk_delete_chunk(blosc2_schunk* schunk, int64_t nchunk) {
 // schunk.c:1459-1477
 int64_t blosc2_schunk_append_buffer(blosc2_schunk* schunk, const void* src, int32_t nbytes) {
   if (!schunk) return BLOSC2_ERROR_NULL_POINTER;
+  if (int rc0 = refuse_if_attached(schunk, "blosc2_schunk_append_buffer")) return rc0;
   if (nbytes < 0 || nbytes > BLOSC2_MAX_BUFFERSIZE) return BLOSC2_ERROR_INVALID_PARAM;
   uint8_t* chunk = static_cast<uint8_t*>(malloc((size_t)nbytes + BLOSC2_MAX_OVERHEAD));
   if (!chunk) return BLOSC2_ERROR_MEMORY_ALLOC;
@@ -501,6 +518,7 @@ int blosc2_schunk_get_dparams(blosc2_schunk* schunk, blosc2_dparams** dparams) {
 int64_t b2h_schunk_append_device(blosc2_schunk* schunk, const void* d_src, const int32_t* nbytes, int32_t n,
                                  int64_t src_stride) {
   if (!schunk || (n > 0 && (!d_src || !nbytes))) return BLOSC2_ERROR_NULL_POINTER;
+  if (int rc0 = refuse_if_attached(schunk, "b2h_schunk_append_device")) return rc0;
   if (n < 0) return BLOSC2_ERROR_INVALID_PARAM;
   if (n == 0) return schunk->nchunks;
   const uint8_t* src = static_cast<const uint8_t*>(d_src);
@@ -605,11 +623,62 @@ int fanout_workers(int32_t ndevices, int32_t n) {
   const int w = ndevices > 0 ? ndevices : nd;
   return std::max(1, std::min(w, (int)std::max<int32_t>(n, 1)));
 }
+
+// Bytes of one staging group: the device batches move through host memory in groups of this
+// size, so a range larger than HBM streams through instead of failing its allocation.
+constexpr int64_t kGroupBytes = int64_t(128) << 20;
+
+// Host copies between the caller's (pageable) buffers and a pinned staging buffer, split over a
+// few threads: one thread's memcpy (~10 GB/s) would otherwise bound the whole fan-out.
+void par_copy(uint8_t* dst, int64_t dst_stride, const uint8_t* src, int64_t src_stride, int32_t rows, int64_t row_bytes) {
+  const int64_t total = (int64_t)rows * row_bytes;
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(4, total >> 24));
+  auto part = [&](int t) {
+    for (int32_t r = (int32_t)((int64_t)rows * t / T); r < (int32_t)((int64_t)rows * (t + 1) / T); r++)
+      memcpy(dst + (int64_t)r * dst_stride, src + (int64_t)r * src_stride, (size_t)row_bytes);
+  };
+  if (T == 1) return part(0);
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; t++) th.emplace_back(part, t);
+  part(0);
+  for (auto& x : th) x.join();
+}
+
+// One fan-out worker's staging: three pinned host buffers (a ring: one being filled by the host
+// copy, one in flight over PCIe, one spare) and two device buffers (one being copied into while
+// the engine works on the other), a copy stream and an event per device buffer.
+struct Stage {
+  void* pin[3] = {nullptr, nullptr, nullptr};
+  uint8_t* dev[2] = {nullptr, nullptr};
+  hipStream_t cs = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  bool init(size_t bytes) {
+    for (auto& x : pin)
+      if (hipHostMalloc(&x, std::max<size_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) return false;
+    for (auto& x : dev)
+      if (hipMalloc(&x, std::max<size_t>(bytes, 1)) != hipSuccess) return false;
+    if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return false;
+    for (auto& e : ev)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+    return true;
+  }
+  ~Stage() {
+    if (cs) (void)hipStreamSynchronize(cs);
+    for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+    if (cs) (void)hipStreamDestroy(cs);
+    for (auto& x : dev) if (x) (void)hipFree(x);
+    for (auto& x : pin) if (x) (void)hipHostFree(x);
+  }
+  uint8_t* p(int i) const { return static_cast<uint8_t*>(pin[i % 3]); }
+};
 }  // namespace
 
+// Worker threads are spawned for every device, the caller's thread included none: its current
+// device is never changed (a torch rank bound to device d keeps d).
 int64_t b2h_schunk_append_buffers(blosc2_schunk* schunk, const void* src, const int32_t* nbytes, int32_t n,
                                   int64_t src_stride, int32_t ndevices) {
   if (!schunk || (n > 0 && (!src || !nbytes))) return BLOSC2_ERROR_NULL_POINTER;
+  if (int rc0 = refuse_if_attached(schunk, "b2h_schunk_append_buffers")) return rc0;
   if (n < 0 || src_stride < 0) return BLOSC2_ERROR_INVALID_PARAM;
   if (n == 0) return schunk->nchunks;
   for (int32_t i = 0; i < n; i++)
@@ -626,6 +695,7 @@ int64_t b2h_schunk_append_buffers(blosc2_schunk* schunk, const void* src, const 
   if (rc < 0) return rc;
   std::vector<uint8_t*> chunks((size_t)n, nullptr);
   std::vector<int> wrc((size_t)W, 0);
+  const int32_t maxnb = *std::max_element(nbytes, nbytes + n);
   auto work = [&](int k) {
     const int32_t i0 = (int32_t)((int64_t)n * k / W), i1 = (int32_t)((int64_t)n * (k + 1) / W);
     if (i1 <= i0) return;
@@ -633,25 +703,43 @@ int64_t b2h_schunk_append_buffers(blosc2_schunk* schunk, const void* src, const 
     blosc2_context* ctx = b2h::ctx_clone(schunk->cctx);
     if (!ctx) { wrc[k] = BLOSC2_ERROR_MEMORY_ALLOC; return; }
     b2h::ctx_set_blocksize(ctx, before[i0]);
-    uint8_t* d = nullptr;
-    const size_t bytes = (size_t)(i1 - i0) * (size_t)src_stride;
-    if (hipMalloc(&d, std::max<size_t>(bytes, 1)) != hipSuccess) {
-      wrc[k] = BLOSC2_ERROR_MEMORY_ALLOC;
-    } else if (hipMemcpy(d, h + (int64_t)i0 * src_stride, bytes, hipMemcpyHostToDevice) != hipSuccess) {
-      wrc[k] = BLOSC2_ERROR_FAILURE;
-    } else {
-      wrc[k] = b2h::ctx_append_device(ctx, d, nbytes + i0, i1 - i0, src_stride, chunks.data() + i0);
+    // groups of G chunks: host copy of group g + 2, H2D of group g + 1 and the engine on group g
+    // run at once (the copy on helper threads, the H2D on the copy stream)
+    const int32_t G = (int32_t)std::max<int64_t>(1, std::min<int64_t>(i1 - i0, kGroupBytes / std::max<int64_t>(src_stride, 1)));
+    const int32_t ng = (i1 - i0 + G - 1) / G;
+    const int64_t row = std::min<int64_t>(src_stride, maxnb);
+    Stage S;
+    auto lo = [&](int32_t g) { return i0 + g * G; };
+    auto cnt = [&](int32_t g) { return std::min(G, i1 - lo(g)); };
+    auto stage = [&](int32_t g) { par_copy(S.p(g), src_stride, h + (int64_t)lo(g) * src_stride, src_stride, cnt(g), row); };
+    auto h2d = [&](int32_t g) {
+      return hipMemcpyAsync(S.dev[g % 2], S.p(g), (size_t)cnt(g) * (size_t)src_stride, hipMemcpyHostToDevice, S.cs) ==
+                 hipSuccess &&
+             hipEventRecord(S.ev[g % 2], S.cs) == hipSuccess;
+    };
+    int r = S.init((size_t)G * (size_t)src_stride) ? 0 : BLOSC2_ERROR_MEMORY_ALLOC;
+    if (r == 0) {
+      stage(0);
+      if (ng > 1) stage(1);
+      if (!h2d(0)) r = BLOSC2_ERROR_FAILURE;
     }
-    if (d) (void)hipFree(d);
+    for (int32_t g = 0; g < ng && r == 0; g++) {
+      std::thread ahead;
+      if (g + 2 < ng) ahead = std::thread(stage, g + 2);   // its buffer's H2D (group g - 1) completed
+      if (hipEventSynchronize(S.ev[g % 2]) != hipSuccess) r = BLOSC2_ERROR_FAILURE;
+      if (r == 0 && g + 1 < ng && !h2d(g + 1)) r = BLOSC2_ERROR_FAILURE;
+      if (r == 0) r = b2h::ctx_append_device(ctx, S.dev[g % 2], nbytes + lo(g), cnt(g), src_stride, chunks.data() + lo(g));
+      if (ahead.joinable()) ahead.join();
+    }
+    wrc[k] = r;
     blosc2_free_ctx(ctx);
   };
   std::vector<std::thread> th;
-  for (int k = 1; k < W; k++) th.emplace_back(work, k);
-  work(0);
+  for (int k = 0; k < W; k++) th.emplace_back(work, k);
   for (auto& t : th) t.join();
   rc = 0;
   for (int k = 0; k < W && rc == 0; k++) rc = wrc[k];
-  if (rc == BLOSC2_ERROR_FILTER_PIPELINE) {   // user filters / codecs: the serial calls, through host memory
+  if (rc == BLOSC2_ERROR_FILTER_PIPELINE) {   // user callbacks, prefilters: the serial calls, through host memory
     for (uint8_t* c : chunks) free(c);
     int64_t r = schunk->nchunks;
     for (int32_t i = 0; i < n && r >= 0; i++) r = blosc2_schunk_append_buffer(schunk, h + (int64_t)i * src_stride, nbytes[i]);
@@ -661,15 +749,18 @@ int64_t b2h_schunk_append_buffers(blosc2_schunk* schunk, const void* src, const 
     for (uint8_t* c : chunks) free(c);
     return rc;
   }
-  b2h::ctx_set_blocksize(schunk->cctx, before[n]);
   int64_t r = schunk->nchunks;
   for (int32_t i = 0; i < n; i++) {
     r = blosc2_schunk_append_chunk(schunk, chunks[i], false);
     if (r < 0) {
+      // chunks [0, i) stay appended (include/b2h.h); the context is left where the serial calls
+      // would have left it after chunk i - 1
       for (int32_t j = i; j < n; j++) free(chunks[j]);
+      b2h::ctx_set_blocksize(schunk->cctx, before[i]);
       return r;
     }
   }
+  b2h::ctx_set_blocksize(schunk->cctx, before[n]);
   return r;
 }
 
@@ -699,22 +790,46 @@ int b2h_schunk_decompress_buffers(blosc2_schunk* schunk, int64_t nchunk, int32_t
     if (hipSetDevice(k % b2h::device_count()) != hipSuccess) { wrc[k] = BLOSC2_ERROR_FAILURE; return; }
     blosc2_context* ctx = blosc2_create_dctx(dp);
     if (!ctx) { wrc[k] = BLOSC2_ERROR_MEMORY_ALLOC; return; }
-    uint8_t* d = nullptr;
-    const size_t bytes = (size_t)(i1 - i0) * (size_t)dst_stride;
-    if (hipMalloc(&d, std::max<size_t>(bytes, 1)) != hipSuccess) {
-      wrc[k] = BLOSC2_ERROR_MEMORY_ALLOC;
-    } else {
-      wrc[k] = b2h::ctx_decompress_device(ctx, schunk->data + nchunk + i0, i1 - i0, d, dst_stride, dst_capacity,
-                                          st.data() + i0);
-      if (wrc[k] >= 0 && hipMemcpy(out + (int64_t)i0 * dst_stride, d, bytes, hipMemcpyDeviceToHost) != hipSuccess)
-        wrc[k] = BLOSC2_ERROR_FAILURE;
+    // groups of G chunks: the engine decodes group g while group g - 1 comes back over PCIe into
+    // a pinned buffer and group g - 2 is copied from pinned memory into the caller's buffer
+    const int32_t G = (int32_t)std::max<int64_t>(1, std::min<int64_t>(i1 - i0, kGroupBytes / std::max<int64_t>(dst_stride, 1)));
+    const int32_t ng = (i1 - i0 + G - 1) / G;
+    Stage S;
+    auto lo = [&](int32_t g) { return i0 + g * G; };
+    auto cnt = [&](int32_t g) { return std::min(G, i1 - lo(g)); };
+    auto unstage = [&](int32_t g) {
+      par_copy(out + (int64_t)lo(g) * dst_stride, dst_stride, S.p(g), dst_stride, cnt(g), dst_capacity);
+    };
+    int r = S.init((size_t)G * (size_t)dst_stride) ? 0 : BLOSC2_ERROR_MEMORY_ALLOC;
+    std::thread behind;
+    for (int32_t g = 0; g < ng && r == 0; g++) {
+      // the device buffer's previous D2H (group g - 2) must be done before the engine rewrites it
+      if (g >= 2 && hipEventSynchronize(S.ev[g % 2]) != hipSuccess) { r = BLOSC2_ERROR_FAILURE; break; }
+      const int rr = b2h::ctx_decompress_device(ctx, schunk->data + nchunk + lo(g), cnt(g), S.dev[g % 2], dst_stride,
+                                                dst_capacity, st.data() + lo(g));
+      if (rr < 0) { r = rr; break; }
+      if (behind.joinable()) behind.join();   // group g - 3's pinned buffer is free again
+      if (hipMemcpyAsync(S.p(g), S.dev[g % 2], (size_t)cnt(g) * (size_t)dst_stride, hipMemcpyDeviceToHost, S.cs) != hipSuccess ||
+          hipEventRecord(S.ev[g % 2], S.cs) != hipSuccess) {
+        r = BLOSC2_ERROR_FAILURE;
+        break;
+      }
+      if (g >= 1) {   // group g - 1 has landed in pinned memory once its event fires
+        const int32_t gp = g - 1;
+        if (hipEventSynchronize(S.ev[gp % 2]) != hipSuccess) { r = BLOSC2_ERROR_FAILURE; break; }
+        behind = std::thread(unstage, gp);
+      }
     }
-    if (d) (void)hipFree(d);
+    if (behind.joinable()) behind.join();
+    if (r == 0 && ng >= 1) {
+      if (hipEventSynchronize(S.ev[(ng - 1) % 2]) != hipSuccess) r = BLOSC2_ERROR_FAILURE;
+      else unstage(ng - 1);
+    }
+    wrc[k] = r;
     blosc2_free_ctx(ctx);
   };
   std::vector<std::thread> th;
-  for (int k = 1; k < W; k++) th.emplace_back(work, k);
-  work(0);
+  for (int k = 0; k < W; k++) th.emplace_back(work, k);
   for (auto& t : th) t.join();
   rc = 0;
   for (int k = 0; k < W && rc == 0; k++) rc = wrc[k];
@@ -804,6 +919,7 @@ int set_one(blosc2_schunk* s, const SliceStep& st, const uint8_t* src, std::vect
 
 int blosc2_schunk_set_slice_buffer(blosc2_schunk* schunk, int64_t start, int64_t stop, void* buffer) {
   if (!schunk || !buffer) return BLOSC2_ERROR_NULL_POINTER;
+  if (int rc0 = refuse_if_attached(schunk, "blosc2_schunk_set_slice_buffer")) return rc0;
   int rc = check_slice(schunk, start, stop);
   if (rc < 0) return rc;
   const uint8_t* src = static_cast<const uint8_t*>(buffer);
@@ -820,6 +936,7 @@ int blosc2_schunk_set_slice_buffer(blosc2_schunk* schunk, int64_t start, int64_t
 // then updated in order; the (at most two) edge chunks go through the host walk above.
 int b2h_schunk_set_slice_device(blosc2_schunk* schunk, int64_t start, int64_t stop, const void* d_src) {
   if (!schunk || !d_src) return BLOSC2_ERROR_NULL_POINTER;
+  if (int rc0 = refuse_if_attached(schunk, "b2h_schunk_set_slice_device")) return rc0;
   int rc = check_slice(schunk, start, stop);
   if (rc < 0) return rc;
   const uint8_t* src = static_cast<const uint8_t*>(d_src);

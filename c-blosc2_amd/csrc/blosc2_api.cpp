@@ -154,7 +154,10 @@ struct blosc2_context_s {
   uint8_t filters[6] = {0, 0, 0, 0, 0, BLOSC_SHUFFLE};
   uint8_t filters_meta[6] = {0};
   blosc2_prefilter_fn prefilter = nullptr;
-  blosc2_prefilter_params* preparams = nullptr;
+  blosc2_prefilter_params* preparams = nullptr;   // -> pre_copy when a prefilter is set
+  blosc2_prefilter_params pre_copy{};             // the context's own copy (blosc/blosc2.c:6215-6219)
+  blosc2_postfilter_params post_copy{};           // dparams.postparams points here (6279-6283)
+  std::vector<uint8_t> ttmp;                      // the callbacks' `ttmp` (a thread context's 4 x ebsize tmp)
   void* tuner_params = nullptr;
   int tuner_id = 0;
   bool instr_codec = false;
@@ -216,7 +219,7 @@ int compname_to_code(const char* name) {
 
 // Pipelines the device path executes: built-in filters and BloscLZ.
 // User-registered filters and codecs run through the host-callback pipelines below.
-int check_supported(const blosc2_context* c) {
+int check_supported(const blosc2_context* c, bool host_pipeline = false) {
   if (c->compcode != BLOSC_BLOSCLZ && c->compcode != BLOSC_LZ4 && c->compcode <= BLOSC2_DEFINED_CODECS_STOP) {
     TRACE_ERROR("codec %d is not implemented by the MI355X engine (BloscLZ, LZ4 and user codecs)", c->compcode);
     return BLOSC2_ERROR_CODEC_SUPPORT;
@@ -235,8 +238,12 @@ int check_supported(const blosc2_context* c) {
       return BLOSC2_ERROR_FILTER_PIPELINE;
     }
   }
-  if (c->prefilter || c->instr_codec || c->tuner_params || c->tuner_id != 0) {
-    TRACE_ERROR("prefilters / instrumented codecs / tuners are not supported by the device pipeline");
+  if (c->prefilter && !host_pipeline) {
+    TRACE_ERROR("prefilters run per chunk through blosc2_compress_ctx, not the device batch");
+    return BLOSC2_ERROR_FILTER_PIPELINE;
+  }
+  if (c->instr_codec || c->tuner_params || c->tuner_id != 0) {
+    TRACE_ERROR("instrumented codecs / tuners are not supported by the device pipeline");
     return BLOSC2_ERROR_FILTER_PIPELINE;
   }
   return 0;
@@ -255,7 +262,7 @@ int decompress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, voi
 int compress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void* dest, int32_t destsize,
                   int32_t blocksize_in, bool sticky, bool extended) {
   if (srcsize < 0) return BLOSC2_ERROR_INVALID_PARAM;
-  if (needs_host_callbacks(ctx->filters, ctx->compcode))
+  if (ctx->prefilter || needs_host_callbacks(ctx->filters, ctx->compcode))
     return compress_hybrid(ctx, src, srcsize, dest, destsize, blocksize_in, sticky, extended);
   b2h::CompressPlan plan;
   int32_t computed = 0;
@@ -379,6 +386,41 @@ bool chunk_needs_host(const uint8_t* s, const ChunkHdr& H) {
   return true;
 }
 
+uint8_t* ctx_ttmp(blosc2_context* ctx, int32_t blocksize, int32_t typesize, size_t* nbytes);
+
+// pipeline_backward's postfilter step for block `nblock` (blosc/blosc2.c:1586-1606; for memcpyed
+// and special chunks 1910-1931): `in` is the block as the backward filters leave it, the
+// callback writes `out`.  A special-value chunk passes its value's width as the typesize
+// (blosc_d 1743-1746).
+int call_postfilter(blosc2_context* ctx, const ChunkHdr& H, const uint8_t* in, uint8_t* out, int32_t nblock) {
+  blosc2_postfilter_params pp;
+  memcpy(&pp, ctx->dparams.postparams, sizeof pp);
+  const int32_t off = nblock * H.blocksize;
+  pp.input = in;
+  pp.output = out;
+  pp.size = std::min(H.blocksize, H.nbytes - off);
+  pp.typesize = H.special == BLOSC2_SPECIAL_VALUE ? H.cbytes - H.overhead : H.typesize;
+  pp.offset = off;
+  pp.nchunk = ctx->schunk ? static_cast<blosc2_schunk*>(ctx->schunk)->current_nchunk : -1;
+  pp.nblock = nblock;
+  pp.tid = 0;
+  pp.ttmp = ctx_ttmp(ctx, H.blocksize, H.typesize, &pp.ttmp_nbytes);
+  pp.ctx = ctx;
+  if (ctx->dparams.postfilter(&pp) != 0) {
+    TRACE_ERROR("Execution of postfilter function failed");
+    return BLOSC2_ERROR_POSTFILTER;
+  }
+  return 0;
+}
+
+// The chunk's block images without the postfilter (the caller holds ctx->mu).
+struct NoPostfilter {
+  blosc2_context* c;
+  blosc2_postfilter_fn f;
+  explicit NoPostfilter(blosc2_context* ctx) : c(ctx), f(ctx->dparams.postfilter) { ctx->dparams.postfilter = nullptr; }
+  ~NoPostfilter() { c->dparams.postfilter = f; }
+};
+
 // Decompress one host chunk through the engine.  With a block mask only unmasked blocks are
 // copied back so masked regions of `dest` keep the caller's bytes (blosc/blosc2.c:1734-1737).
 // `mode`: b2h::kDecDeltaSelf for the per-block entry points (getitem, decompress_block).
@@ -394,6 +436,23 @@ int decompress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void*
     TRACE_ERROR("The number of items in block_maskout (%zu) must match the number of blocks in chunk (%d).",
                 mask->size(), nblocks);
     return BLOSC2_ERROR_DATA;
+  }
+  if (ctx->dparams.postfilter) {
+    // The engine decodes the chunk (every backward filter) into a host image; the callback then
+    // runs per unmasked block, in block order, writing `dest` (blosc_d with a postfilter never
+    // writes dest itself: 1880-1883, 1960-1965, 1489, 1581).
+    std::vector<uint8_t> img((size_t)std::max(nbytes, 1));
+    {
+      NoPostfilter np(ctx);
+      rc = decompress_host(ctx, src, srcsize, img.data(), nbytes, mask, mode);
+    }
+    if (rc < 0) return rc;
+    for (int32_t b = 0; b < nblocks; b++) {
+      if (mask && (*mask)[(size_t)b]) continue;
+      const int64_t off = (int64_t)b * bs;
+      if ((rc = call_postfilter(ctx, H, img.data() + off, static_cast<uint8_t*>(dest) + off, b)) < 0) return rc;
+    }
+    return nbytes;
   }
   if (chunk_needs_host(static_cast<const uint8_t*>(src), H))
     return decompress_hybrid(ctx, src, srcsize, dest, destsize, mask, mode);
@@ -574,6 +633,70 @@ int to_device(hipStream_t st, void* d, const void* h, size_t n) {
   return 0;
 }
 
+// The callbacks' `ttmp`: a thread context's temporaries, 4 x (blocksize + 4 * typesize) bytes
+// (blosc/blosc2.c:2233-2261, 4663-4673).
+uint8_t* ctx_ttmp(blosc2_context* ctx, int32_t blocksize, int32_t typesize, size_t* nbytes) {
+  const size_t need = (size_t)4 * ((size_t)blocksize + 4 * (size_t)typesize);
+  if (ctx->ttmp.size() < need) ctx->ttmp.assign(need, 0);
+  *nbytes = need;
+  return ctx->ttmp.data();
+}
+
+// pipeline_forward's prefilter step for the block at `offset` (blosc/blosc2.c:1066-1103): a copy
+// of the context's params completed for the block, the output zeroed first unless disposable.
+// Returns 0, 1 (the callback failed on a disposable output: the block's pipeline ends at the
+// prefilter output, 1096-1099) or BLOSC2_ERROR_FILTER_PIPELINE.  `out` holds >= the output size.
+int call_prefilter(blosc2_context* ctx, const b2h::CompressPlan& P, const uint8_t* in, uint8_t* out, int32_t bsize,
+                   int32_t offset) {
+  blosc2_prefilter_params pp;
+  memcpy(&pp, ctx->preparams, sizeof pp);
+  const bool disposable = ctx->preparams->output_is_disposable;
+  const int32_t ts = P.typesize;
+  const int32_t ots = pp.output_typesize > 0 ? pp.output_typesize : ts;
+  const int32_t osize = bsize / ts * ots;
+  pp.output_typesize = ots;
+  if (!disposable) memset(out, 0, (size_t)osize);
+  pp.input = in;
+  pp.output = out;
+  pp.output_size = osize;
+  pp.output_offset = offset;
+  pp.nblock = offset / P.blocksize;
+  pp.nchunk = ctx->schunk ? static_cast<blosc2_schunk*>(ctx->schunk)->current_nchunk : -1;
+  pp.tid = 0;
+  pp.ttmp = ctx_ttmp(ctx, P.blocksize, ts, &pp.ttmp_nbytes);
+  pp.ctx = ctx;
+  pp.output_is_disposable = disposable;
+  if (ctx->prefilter(&pp) != 0) {
+    if (disposable) return 1;
+    TRACE_ERROR("Execution of prefilter function failed");
+    return BLOSC2_ERROR_FILTER_PIPELINE;
+  }
+  return 0;
+}
+
+// Bytes a prefilter may write for one block (its output size, or the block).
+size_t prefilter_span(const blosc2_context* ctx, const b2h::CompressPlan& P) {
+  const int32_t ots = ctx->preparams->output_typesize > 0 ? ctx->preparams->output_typesize : P.typesize;
+  return (size_t)std::max<int64_t>(P.blocksize, (int64_t)(P.blocksize / P.typesize) * ots) + 64;
+}
+
+// A memcpyed chunk compressed with a prefilter holds the prefilter's outputs, block by block
+// (serial_blosc 2188-2200 -> blosc_c 1241-1248: the prefilter writes straight into the chunk).
+// `raw` is the input as the pipeline leaves it; the chunk's payload in `dest` is rewritten.
+int prefilter_memcpyed(blosc2_context* ctx, const b2h::CompressPlan& P, const uint8_t* raw, int32_t n, uint8_t* dest,
+                       int32_t destsize, int32_t ovh) {
+  std::vector<uint8_t> blk(prefilter_span(ctx, P));
+  for (int64_t off = 0; off < n; off += P.blocksize) {
+    const int32_t bsize = (int32_t)std::min<int64_t>(P.blocksize, n - off);
+    uint8_t* o = dest + ovh + off;
+    memcpy(blk.data(), o, (size_t)std::min<int64_t>(bsize, destsize - ovh - off));   // bytes left unwritten stay
+    const int r = call_prefilter(ctx, P, raw + off, blk.data(), bsize, (int32_t)off);
+    if (r < 0) return r;
+    memcpy(o, blk.data(), (size_t)std::min<int64_t>(bsize, destsize - ovh - off));
+  }
+  return 0;
+}
+
 int compress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void* dest, int32_t destsize,
                     int32_t blocksize_in, bool sticky, bool extended) {
   blosc2_codec codec{};
@@ -590,10 +713,10 @@ int compress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void*
   if (rc < 0) return rc;
   P.lz_mode = ctx->lz_mode;
   if (sticky) ctx->blocksize = computed;
-  if ((rc = check_supported(ctx)) < 0) return rc;
+  if ((rc = check_supported(ctx, true)) < 0) return rc;
   if (P.use_dict) {
     // the dictionary's training pass is a device-pipeline feature (compress_batch); host-callback
-    // pipelines (user filters) do not run it
+    // pipelines (user filters, prefilters) do not run it
     TRACE_ERROR("`use_dict` with user-registered filters is not supported by the MI355X engine");
     return BLOSC2_ERROR_CODEC_PARAM;
   }
@@ -608,25 +731,61 @@ int compress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void*
   int32_t* d_cb = reinterpret_cast<int32_t*>(d.small.p);
   blosc2_cparams cp;
   blosc2_ctx_get_cparams(ctx, &cp);
-  if (P.memcpyed) {   // chunk-level memcpy: no filter or codec runs
+  if (P.memcpyed) {   // chunk-level memcpy: no filter or codec runs (a prefilter does)
     rc = b2h::compress_batch(P, hb.a.u8(), 0, 1, hb.out.u8(), 0, d_cb, d.stream, d.ws);
     if (rc < 0) return rc;
     int32_t cb = 0;
     if ((rc = sync_to_host(d.stream, &cb, d_cb, 4))) return rc;
     const int32_t ncopy = cb > 0 ? cb : std::min(destsize, ovh);
     if (hipMemcpy(dest, hb.out.p, (size_t)ncopy, hipMemcpyDeviceToHost) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+    if (cb > 0 && ctx->prefilter &&
+        (rc = prefilter_memcpyed(ctx, P, static_cast<const uint8_t*>(src), n, static_cast<uint8_t*>(dest), destsize, ovh)))
+      return rc;
     return cb;
   }
   const int32_t bs = P.blocksize, nblocks = n / bs + (n % bs ? 1 : 0);
+  if (ctx->prefilter && ctx->preparams->output_is_disposable && extended) {
+    // A disposable output: blosc_c writes every stream as a run of zeros whatever the pipeline
+    // produced (blosc/blosc2.c:1286-1291), so the chunk ends as SPECIAL_ZERO (3054-3063); the
+    // prefilter still runs once per block, in block order
+    std::vector<uint8_t> blk(prefilter_span(ctx, P));
+    for (int32_t b = 0; b < nblocks; b++)
+      (void)call_prefilter(ctx, P, static_cast<const uint8_t*>(src) + (int64_t)b * bs, blk.data(),
+                           std::min<int32_t>(bs, n - b * bs), b * bs);
+    if (destsize < ovh) return 0;
+    uint8_t hdr[BLOSC_EXTENDED_HEADER_LENGTH];
+    memcpy(hdr, P.header, sizeof hdr);
+    hdr[31] |= (uint8_t)(BLOSC2_SPECIAL_ZERO << 4);
+    const int32_t cb = ovh;
+    memcpy(hdr + 12, &cb, 4);
+    memcpy(dest, hdr, sizeof hdr);
+    return cb;
+  }
   bool has_delta = false;
   for (int i = 0; i < 6; i++) has_delta |= P.filters[i] == BLOSC_DELTA;
   // ---- forward pipeline (block 0 first with DELTA: the serial walk's order) ----
   std::vector<uint8_t> hs, hd;
+  std::vector<std::pair<int32_t, std::vector<uint8_t>>> disposed;   // blocks whose pipeline ended at the prefilter
   uint8_t* fsrc = hb.a.u8();
   for (int pass = (has_delta && nblocks > 1) ? 1 : 0; pass <= ((has_delta && nblocks > 1) ? 2 : 0); pass++) {
     uint8_t *s = hb.a.u8(), *t = hb.b.u8(), *u = hb.c.u8();
     const int32_t b0 = pass == 2 ? 1 : 0, b1 = pass == 1 ? 1 : nblocks;
     const int64_t lo = (int64_t)b0 * bs, hi = std::min<int64_t>((int64_t)b1 * bs, n);
+    if (ctx->prefilter) {   // pipeline_forward's prefilter, before slot 0 (blosc/blosc2.c:1069-1110)
+      hs.resize((size_t)n);
+      hd.resize((size_t)n);
+      std::vector<uint8_t> blk(prefilter_span(ctx, P));
+      if ((rc = sync_to_host(d.stream, hs.data() + lo, s + lo, (size_t)(hi - lo)))) return rc;
+      for (int32_t b = b0; b < b1; b++) {
+        const int32_t bsize = std::min<int32_t>(bs, n - b * bs);
+        const int r = call_prefilter(ctx, P, hs.data() + (int64_t)b * bs, blk.data(), bsize, b * bs);
+        if (r < 0) return r;
+        memcpy(hd.data() + (int64_t)b * bs, blk.data(), (size_t)bsize);
+        if (r == 1) disposed.emplace_back(b, std::vector<uint8_t>(blk.data(), blk.data() + bsize));
+      }
+      if ((rc = to_device(d.stream, t + lo, hd.data() + lo, (size_t)(hi - lo)))) return rc;
+      cycle(s, t, u);
+    }
     for (int i = 0; i < 6; i++) {
       const uint8_t f = P.filters[i];
       if (f == BLOSC_NOFILTER) continue;
@@ -656,6 +815,8 @@ int compress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void*
     }
     fsrc = s;
   }
+  for (auto& db : disposed)   // 1096-1099: no filter ran after a disposable prefilter failure
+    if ((rc = to_device(d.stream, fsrc + (int64_t)db.first * bs, db.second.data(), db.second.size()))) return rc;
   // ---- codec ----
   int32_t cb = 0;
   if (!ucodec) {
@@ -664,6 +825,13 @@ int compress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void*
     if ((rc = sync_to_host(d.stream, &cb, d_cb, 4))) return rc;
     const int32_t ncopy = cb > 0 ? cb : std::min(destsize, ovh);
     if (hipMemcpy(dest, hb.out.p, (size_t)ncopy, hipMemcpyDeviceToHost) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+    // the memcpy fallback re-runs the pipeline as a memcpyed chunk: the prefilter again, over
+    // the input as the first pass left it (blosc_compress_context 3017-3051)
+    if (cb > 0 && ctx->prefilter && (static_cast<uint8_t*>(dest)[2] & BLOSC_MEMCPYED)) {
+      std::vector<uint8_t> raw((size_t)n);
+      if ((rc = sync_to_host(d.stream, raw.data(), hb.a.p, (size_t)n))) return rc;
+      if ((rc = prefilter_memcpyed(ctx, P, raw.data(), n, static_cast<uint8_t*>(dest), destsize, ovh))) return rc;
+    }
     return cb;
   }
   // user encoder per stream, serial layout (blosc_c / serial_blosc / blosc_compress_context)
@@ -725,6 +893,7 @@ int compress_hybrid(blosc2_context* ctx, const void* src, int32_t srcsize, void*
     o[2] |= BLOSC_MEMCPYED;
     memcpy(o + ovh, raw.data(), (size_t)n);
     cb = n + ovh;
+    if (ctx->prefilter && (rc = prefilter_memcpyed(ctx, P, raw.data(), n, o, destsize, ovh))) return rc;
   } else {
     cb = 0;
   }
@@ -952,7 +1121,9 @@ blosc2_context* ctx_clone(const blosc2_context* ctx) {
   memcpy(c->filters, ctx->filters, sizeof c->filters);
   memcpy(c->filters_meta, ctx->filters_meta, sizeof c->filters_meta);
   c->prefilter = ctx->prefilter;
-  c->preparams = ctx->preparams;
+  c->pre_copy = ctx->pre_copy;
+  c->preparams = ctx->prefilter ? &c->pre_copy : nullptr;
+  c->post_copy = ctx->post_copy;
   c->tuner_params = ctx->tuner_params;
   c->tuner_id = ctx->tuner_id;
   c->instr_codec = ctx->instr_codec;
@@ -960,6 +1131,7 @@ blosc2_context* ctx_clone(const blosc2_context* ctx) {
   c->lz_mode = ctx->lz_mode;
   memcpy(c->filter_params, ctx->filter_params, sizeof c->filter_params);
   c->dparams = ctx->dparams;
+  if (c->dparams.postfilter) c->dparams.postparams = &c->post_copy;
   return c;
 }
 
@@ -1103,8 +1275,8 @@ int ctx_decompress_device(blosc2_context* ctx, const uint8_t* const* chunks, int
       continue;
     }
     ChunkHdr H;
-    if (read_header(c, cb[i], &H) == 0 && chunk_needs_host(c, H)) {
-      host_idx.push_back(i);
+    if (ctx->dparams.postfilter || (read_header(c, cb[i], &H) == 0 && chunk_needs_host(c, H))) {
+      host_idx.push_back(i);   // user callbacks (filters, codecs, a postfilter) run on the host
       continue;
     }
     dev_idx.push_back(i);
@@ -1265,8 +1437,11 @@ blosc2_context* blosc2_create_cctx(blosc2_cparams cparams) {
     else if (!strcmp(v, "FORWARD_COMPAT")) c->splitmode = BLOSC_FORWARD_COMPAT_SPLIT;
   }
   c->schunk = cparams.schunk;
-  c->prefilter = cparams.prefilter;
-  c->preparams = cparams.preparams;
+  if (cparams.prefilter) {   // blosc/blosc2.c:6215-6219: the context keeps a copy of the params
+    c->prefilter = cparams.prefilter;
+    if (cparams.preparams) memcpy(&c->pre_copy, cparams.preparams, sizeof c->pre_copy);
+    c->preparams = &c->pre_copy;
+  }
   c->tuner_params = cparams.tuner_params;
   c->tuner_id = cparams.tuner_id;
   c->codec_params = cparams.codec_params;
@@ -1279,6 +1454,12 @@ blosc2_context* blosc2_create_dctx(blosc2_dparams dparams) {
   blosc2_context* c = new blosc2_context_s();
   c->do_compress = 0;
   c->dparams = dparams;
+  if (dparams.postfilter) {   // blosc/blosc2.c:6279-6283: the context keeps a copy of the params
+    if (dparams.postparams) memcpy(&c->post_copy, dparams.postparams, sizeof c->post_copy);
+    c->dparams.postparams = &c->post_copy;
+  } else {
+    c->dparams.postparams = nullptr;
+  }
   c->nthreads = dparams.nthreads;
   long x;
   if (env_long("BLOSC_NTHREADS", &x) && x > 0) c->nthreads = (int16_t)x;
@@ -1380,6 +1561,9 @@ static void carve_items(const uint8_t* s, const ChunkHdr& H, int64_t off, int32_
   }
 }
 
+static int blosc2_decompress_block_unlocked(blosc2_context* context, const void* src, int32_t srcsize, int32_t nblock,
+                                            void* dest, int32_t destsize, const ChunkHdr& H);
+
 // blosc2_decompress_block_ctx (blosc/blosc2.c:4580-4687; declared in blosc-private.h:29 and used
 // by the sparse reader, schunk.c:1858): block `nblock` of a chunk into dest, returning its size.
 // Checks in the reference's order; then the chunk is decoded on the device with every other block
@@ -1416,8 +1600,28 @@ int blosc2_decompress_block_ctx(blosc2_context* context, const void* src, int32_
     return BLOSC2_ERROR_WRITE_BUFFER;
   }
   if (H.lazy && !H.special) return BLOSC2_ERROR_INVALID_PARAM;   // lazy chunks need their frame
-  const uint8_t* s = static_cast<const uint8_t*>(src);
   std::lock_guard<std::mutex> g(context->mu);
+  if (context->dparams.postfilter) {
+    // blosc_d(dest, dest_offset 0) with the postfilter: the block's image, then the callback
+    // writes dest (blosc/blosc2.c:4678-4682, 1586-1606, 1910-1931)
+    std::vector<uint8_t> blk((size_t)bsize);
+    {
+      NoPostfilter np(context);
+      rc = blosc2_decompress_block_unlocked(context, src, srcsize, nblock, blk.data(), bsize, H);
+    }
+    if (rc < 0) return rc;
+    if ((rc = call_postfilter(context, H, blk.data(), static_cast<uint8_t*>(dest), nblock)) < 0) return rc;
+    return bsize;
+  }
+  return blosc2_decompress_block_unlocked(context, src, srcsize, nblock, dest, destsize, H);
+}
+
+static int blosc2_decompress_block_unlocked(blosc2_context* context, const void* src, int32_t srcsize, int32_t nblock,
+                                            void* dest, int32_t destsize, const ChunkHdr& H) {
+  const uint8_t* s = static_cast<const uint8_t*>(src);
+  const bool leftover = nblock == H.nblocks - 1 && H.leftover > 0;
+  const int32_t bsize = leftover ? H.leftover : H.blocksize;
+  int rc;
   if (H.memcpyed || H.special) {
     if (!H.special) {
       if (H.nbytes + H.overhead != H.cbytes) return BLOSC2_ERROR_WRITE_BUFFER;
@@ -1472,6 +1676,32 @@ int blosc2_getitem_ctx(blosc2_context* context, const void* src, int32_t srcsize
   const uint8_t* s = static_cast<const uint8_t*>(src);
   const bool lazy = H.lazy && !H.special;
   std::lock_guard<std::mutex> g(context->mu);
+  if (context->dparams.postfilter && !lazy) {
+    // With a postfilter there is no memcpyed / special short-circuit (blosc/blosc2.c:4336): every
+    // touched block is decoded as blosc_d(dest_offset 0) leaves it, the callback writes the whole
+    // block, and the slice is copied out (4399-4461)
+    std::vector<uint8_t> mask((size_t)H.nblocks, 1);
+    for (int32_t b = 0; b < H.nblocks; b++) {
+      const int64_t lo = (int64_t)b * H.blocksize, hi = lo + H.blocksize;
+      if (hi > sb && lo < stop * ts) mask[b] = 0;
+    }
+    std::vector<uint8_t> full((size_t)std::max(H.nbytes, 1)), blk((size_t)H.blocksize);
+    {
+      NoPostfilter np(context);
+      rc = decompress_host(context, src, srcsize, full.data(), H.nbytes, &mask, b2h::kDecDeltaSelf | b2h::kDecNoDict);
+    }
+    if (rc < 0) return rc;
+    int64_t nt = 0;
+    for (int32_t b = 0; b < H.nblocks; b++) {
+      if (mask[b]) continue;
+      const int64_t lo = (int64_t)b * H.blocksize;
+      const int64_t startb = std::max<int64_t>(sb - lo, 0), stopb = std::min<int64_t>(stop * ts - lo, H.blocksize);
+      if ((rc = call_postfilter(context, H, full.data() + lo, blk.data(), b)) < 0) return rc;
+      memcpy(static_cast<uint8_t*>(dest) + nt, blk.data() + startb, (size_t)(stopb - startb));
+      nt += stopb - startb;
+    }
+    return (int)nib;
+  }
   if ((H.memcpyed || H.special) && !lazy) {
     if (H.special > BLOSC2_SPECIAL_LASTID) return BLOSC2_ERROR_SCHUNK_SPECIAL;
     const int32_t its = H.special == BLOSC2_SPECIAL_VALUE ? H.cbytes - H.overhead : H.typesize;

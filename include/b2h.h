@@ -149,13 +149,18 @@ BLOSC_EXPORT int b2h_schunk_set_slice_device(blosc2_schunk *schunk, int64_t star
  * `ndevices` workers (<= 0: one per visible device; more workers than devices share them round
  * robin), worker k compressing a contiguous range of the chunks on device k % count with its own
  * stream and workspace.  The chunks are appended in order and equal the serial calls' bytes (each
- * worker starts from the sticky blocksize the serial walk reaches at its first chunk).  Returns the
- * new number of chunks, or a negative error with nothing appended. */
+ * worker starts from the sticky blocksize the serial walk reaches at its first chunk).  Each worker
+ * streams its range through pinned memory in groups of <= 128 MiB (host copy, H2D and compression of
+ * three groups overlapped); every worker runs on a thread of its own, so the caller's current device
+ * is unchanged.  Returns the new number of chunks, or a negative error: nothing is appended when a
+ * worker fails; if the final appends fail at chunk i, chunks before i stay appended and the context
+ * holds the blocksize the serial calls leave after chunk i - 1. */
 BLOSC_EXPORT int64_t b2h_schunk_append_buffers(blosc2_schunk *schunk, const void *src, const int32_t *nbytes,
                                                int32_t n, int64_t src_stride, int32_t ndevices);
 /* Chunks [nchunk, nchunk + n) into HOST dst + i * dst_stride (capacity dst_capacity each), spread the
  * same way; status[i] (optional) = what blosc2_schunk_decompress_chunk (schunk.c:1481-1530) returns
- * for chunk nchunk + i.  Returns 0 or the first worker's error. */
+ * for chunk nchunk + i.  Decoded groups come back through pinned memory while the next group
+ * decodes.  Returns 0 or the first worker's error. */
 BLOSC_EXPORT int b2h_schunk_decompress_buffers(blosc2_schunk *schunk, int64_t nchunk, int32_t n, void *dst,
                                                int64_t dst_stride, int32_t dst_capacity, int32_t *status,
                                                int32_t ndevices);

@@ -7,9 +7,11 @@
  * What runs where: every built-in filter (SHUFFLE, BITSHUFFLE, DELTA, TRUNC_PREC), the registered
  * filters bytedelta (35) and int_trunc (36), and the BloscLZ and LZ4 codecs execute as HIP kernels
  * on the GPU; host code only parses/writes headers, stages buffers and keeps context state.
- * Chunks needing another codec (LZ4HC, ZLIB, ZSTD, user codecs) or user filters / pre- /
- * postfilters return BLOSC2_ERROR_CODEC_SUPPORT / BLOSC2_ERROR_FILTER_PIPELINE (see DESIGN.md,
- * "Out of scope").
+ * User-registered filters and codecs, and cparams.prefilter / dparams.postfilter, run as host
+ * callbacks per block (per stream for codecs) between the device stages, with the reference's
+ * params and return codes (blosc/blosc2.c:1069-1110, 1586-1606, 1910-1931).  Chunks needing
+ * LZ4HC, ZLIB or ZSTD return BLOSC2_ERROR_CODEC_SUPPORT; the device batch entry points of b2h.h
+ * refuse prefilters and user callbacks with BLOSC2_ERROR_FILTER_PIPELINE.
  */
 #ifndef BLOSC2_AMD_BLOSC2_H
 #define BLOSC2_AMD_BLOSC2_H

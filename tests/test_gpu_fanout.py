@@ -78,6 +78,32 @@ def test_gpu_append_buffers_equals_serial_appends(lz_mode, workers):
     ser.free()
 
 
+@pytest.mark.parametrize("workers", [1, 2])
+def test_gpu_fanout_streams_groups(workers):
+    """Ranges larger than one staging group (128 MiB) stream through the pinned ring: 80 chunks of
+    4 MiB (3 groups for one worker), chunk for chunk the serial appends' bytes, and back."""
+    import blosc2_amd as B
+    L = B.lib()
+    chunk, n = 4 << 20, 80
+    raw, sizes = _chunks(n, chunk, 90 + workers)
+    fan = B.SChunk(B.cparams(clevel=5, typesize=4, lz_mode=1), B.dparams())
+    ser = B.SChunk(B.cparams(clevel=5, typesize=4, lz_mode=1), B.dparams())
+    assert L.b2h_schunk_append_buffers(fan.p, _p(raw), _p(sizes), n, chunk, workers) == n
+    for i in range(n):
+        assert ser.append_buffer(raw[i * chunk:i * chunk + int(sizes[i])]) == i + 1
+    for i in range(n):
+        assert np.array_equal(fan.chunk(i), ser.chunk(i)), i
+    assert fan.counters() == ser.counters()
+    out = np.zeros(n * chunk, np.uint8)
+    st = np.zeros(n, np.int32)
+    assert L.b2h_schunk_decompress_buffers(fan.p, 0, n, _p(out), chunk, chunk, _p(st), workers) == 0
+    assert list(st) == list(sizes)
+    for i in range(n):
+        assert np.array_equal(out[i * chunk:i * chunk + int(sizes[i])], raw[i * chunk:i * chunk + int(sizes[i])]), i
+    fan.free()
+    ser.free()
+
+
 def test_gpu_fanout_argument_errors():
     import blosc2_amd as B
     L = B.lib()

@@ -132,6 +132,35 @@ def test_open_file_matches_reference(name, tmp_path):
         b.free()
 
 
+@pytest.mark.parametrize("how", ["open", "from_buffer_attached"])
+def test_frame_attached_handles_are_read_only(how):
+    """Writes to a frame-attached handle would only change the in-memory copy (the reference
+    writes them back to the frame): every write entry point refuses them, the counters
+    and chunks stay, and a copy (from_buffer(copy=True)) stays writable."""
+    L = B.bind_schunk(B.lib())
+    path = os.path.join(GOLD, FRAMES[0] + ".b2frame")
+    buf = np.fromfile(path, np.uint8)
+    a = B.SChunk.wrap(L.blosc2_schunk_open(path.encode()), L) if how == "open" else _from_buffer(L, buf, False)
+    try:
+        before = (a.s.nchunks, a.s.nbytes, a.s.cbytes)
+        c0 = a.chunk(0)
+        n0 = a.s.chunksize
+        raw = np.zeros(n0, np.uint8)
+        assert a.append_buffer(raw) == -12                 # BLOSC2_ERROR_INVALID_PARAM
+        assert a.append_chunk(c0) == -12
+        assert a.insert_chunk(0, c0) == -12
+        assert a.update_chunk(0, c0) == -12
+        assert a.delete_chunk(0) == -12
+        assert (a.s.nchunks, a.s.nbytes, a.s.cbytes) == before
+    finally:
+        a.free()
+    c = _from_buffer(L, buf, True)
+    try:
+        assert c.append_chunk(c.chunk(0)) != -12
+    finally:
+        c.free()
+
+
 def test_open_rejects_what_the_reference_rejects(tmp_path):
     L, R = B.bind_schunk(B.lib()), _ref()
     assert not L.blosc2_schunk_open(str(tmp_path / "absent.b2frame").encode())
