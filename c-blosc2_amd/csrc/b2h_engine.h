@@ -130,6 +130,7 @@ struct KernelTimes { float filter_ms, encode_ms, finalize_ms, decode_ms, unfilte
 void enable_timing(bool on);
 int debug_stream_results(void* host, int32_t n);
 int debug_decode_cycles(void* host, int32_t n);
+int debug_fuse_timed_out();
 KernelTimes last_times();   // the latest batch (waits for its events)
 KernelTimes mean_times();   // mean over every batch since enable_timing(true)
 

@@ -182,6 +182,18 @@ int debug_stream_results(void* host, int32_t n) {
   return n;
 }
 
+// Diagnostics: whether the last fused encode launch on this device's default workspace hit a
+// hand-off timeout (its sync word 4; the rescue launches then redid the batch).
+int debug_fuse_timed_out() {
+  Workspace* ws = ws_for_current_device();
+  std::lock_guard<std::mutex> lock(ws->mu);
+  if (!ws->fsync.p) return 0;
+  if (ws->used && ws->done) HIPCHK(hipEventSynchronize(ws->done));
+  int32_t v = 0;
+  HIPCHK(hipMemcpy(&v, ws->fsync.as<int32_t>() + 4, sizeof v, hipMemcpyDeviceToHost));
+  return v != 0;
+}
+
 // Diagnostics: per-stream decoder cycles of the last decompression batch (B2H_DECODE_DEBUG=1).
 static const bool g_ddebug = getenv("B2H_DECODE_DEBUG") != nullptr;
 int debug_decode_cycles(void* host, int32_t n) {
@@ -288,7 +300,15 @@ struct CGeom {
   int32_t lzmode;  // BloscLZ encoder of this batch: 0 exact, 1 fast, 2 fast with deep candidates (the plan's, else the process default)
   int64_t src_stride, wstride, dst_stride;
   uint8_t* chain;  // mode 2: the fast encoder's prev[] arrays, one per workgroup of chain_len() positions
+  const int32_t* gate;   // rescue launches (see compress_batch): run only if *gate != 0; null: always
 };
+// A launch of the rescue sequence queued behind a fused encode launch does its work only when that
+// launch's hand-off wait timed out (the gate word is its timeout flag); otherwise every workgroup
+// leaves at once.  Uniform: one scalar load per workgroup.
+__device__ __forceinline__ bool gated_off(const CGeom& g) {
+  return g.gate != nullptr &&
+         __builtin_amdgcn_readfirstlane(__hip_atomic_load(g.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0;
+}
 __host__ __device__ inline int64_t chain_len(const CGeom& g) { return g.neblock > g.leftover ? g.neblock : g.leftover; }
 
 __device__ __forceinline__ void stream_locate(const CGeom& g, int32_t l, int32_t* off, int32_t* len, int32_t* blk) {
@@ -319,6 +339,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_ffilter(CGeom g, int pass, ui
                                                            uint8_t* __restrict__ out, int64_t out_stride,
                                                            const uint8_t* __restrict__ dref, int64_t dref_stride,
                                                            int zeroed) {
+  if (gated_off(g)) return;
   const int32_t c = blockIdx.y;
   const int32_t b = pass == 2 ? (int32_t)blockIdx.x + 1 : (int32_t)blockIdx.x;
   if (b >= g.nblocks) return;
@@ -343,6 +364,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_ffilter(CGeom g, int pass, ui
 __global__ __launch_bounds__(kBlockThreads) void k_ffilter_ds(CGeom g, const uint8_t* __restrict__ raw, int64_t raw_stride,
                                                               uint8_t* __restrict__ tmp, uint8_t* __restrict__ out,
                                                               int64_t out_stride) {
+  if (gated_off(g)) return;
   const int32_t c = blockIdx.y, b = blockIdx.x;
   if (b >= g.nblocks) return;
   const int32_t off = b * g.bs;
@@ -413,6 +435,7 @@ __device__ __forceinline__ int32_t pull_to_stream(const CGeom& g, const int32_t*
 __global__ __launch_bounds__(1024) void k_plane_cost(CGeom g, const StreamResult* __restrict__ res, int32_t ntot,
                                                      int32_t* __restrict__ porder) {
   __shared__ unsigned long long sum[16];
+  if (gated_off(g)) return;
   if (g.spb < 2 || g.spb > 16) {
     if (threadIdx.x == 0) porder[0] = 0;
     return;
@@ -535,6 +558,7 @@ __host__ __device__ constexpr size_t enc_wg_lds(int hashlog, int nlds, int nglb)
 template <typename POS, int NLDS, int NGLB>
 __global__ __launch_bounds__(64 * (NLDS + NGLB)) __attribute__((amdgpu_waves_per_eu(3, 8)))   // <= 168 VGPRs (kExWords)
 void k_encode(EncArgs args, POS* __restrict__ gtab) {
+  if (gated_off(args.g)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int hashlog = args.g.clevel == 1 ? 12 : (args.g.clevel == 2 ? 13 : 14);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -572,6 +596,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4, 8)))   /
 void k_encode_fast(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
                    StreamResult* __restrict__ res, int32_t nstreams_total, int32_t* __restrict__ next, int tablog,
                    const int32_t* __restrict__ porder) {
+  if (gated_off(g)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   B2H_LDS uint8_t* tab = (B2H_LDS uint8_t*)smem;
   B2H_LDS uint8_t* oring = (B2H_LDS uint8_t*)(smem + (sizeof(POS) << tablog));
@@ -1256,6 +1281,7 @@ __device__ __forceinline__ int32_t finalize_chunk(const CGeom& g, uint8_t* __res
 __global__ void k_finalize(CGeom g, const StreamResult* __restrict__ res, Place* __restrict__ place,
                            int32_t* __restrict__ mode, uint8_t* __restrict__ dst, int32_t* __restrict__ cbytes,
                            int32_t nchunks, const uint8_t* __restrict__ header_template) {
+  if (gated_off(g)) return;
   const int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= nchunks) return;
   const StreamResult* r = res + (int64_t)c * g.nsc;
@@ -1291,6 +1317,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_scatter(CGeom g, const Place*
                                                            const uint8_t* __restrict__ filt,
                                                            const uint8_t* __restrict__ sbuf, uint8_t* __restrict__ dst,
                                                            int32_t nstreams_total) {
+  if (gated_off(g)) return;
   const int32_t s = blockIdx.x;
   if (s >= nstreams_total) return;
   const int32_t c = s / g.nsc, l = s - c * g.nsc;
@@ -1318,7 +1345,9 @@ __global__ __launch_bounds__(kBlockThreads) void k_scatter(CGeom g, const Place*
 __global__ void k_memcpy_chunks(const uint8_t* __restrict__ src, int64_t src_stride, uint8_t* __restrict__ dst,
                                 int64_t dst_stride, int32_t nbytes, const int32_t* __restrict__ mode,
                                 const uint8_t* __restrict__ header_template, int32_t* __restrict__ cbytes,
-                                int32_t overhead, int32_t destsize) {
+                                int32_t overhead, int32_t destsize, const int32_t* __restrict__ gate) {
+  if (gate && __builtin_amdgcn_readfirstlane(__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0)
+    return;
   const int32_t c = blockIdx.y;
   if (mode && mode[c] != 1) return;
   const uint8_t* s = src + (int64_t)c * src_stride;
@@ -1800,6 +1829,12 @@ static int fuse_bits() {
 }
 // Per host thread: the fused launches off (set around a retry after a hand-off timeout).
 static thread_local bool t_fuse_off = false;
+// The gated separate launches queued behind every fused launch (compress_batch); B2H_FUSE_RESCUE=0
+// drops them (measurement only: a timed-out batch then fails with BLOSC2_ERROR_FAILURE).
+static bool fuse_rescue() {
+  const char* e = getenv("B2H_FUSE_RESCUE");
+  return !e || atoi(e) != 0;
+}
 void set_fuse_disabled(bool off) { t_fuse_off = off; }
 static bool fuse_enabled() { return !t_fuse_off && (fuse_bits() & 1) != 0; }
 // B2H_FUSE_GRID (tests): cap the fused launch's persistent grid -- a few workgroups then do every
@@ -2314,7 +2349,7 @@ static CGeom make_geom(const CompressPlan& P, int64_t src_stride, int64_t dst_st
 static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const uint8_t* filt, const uint8_t* raw,
                         int64_t raw_stride, uint8_t* d_dst, int64_t dst_stride, int32_t* d_cbytes, int32_t nchunks,
                         const uint8_t* htpl, int64_t ntot, hipStream_t st, const uint8_t* fuse_raw = nullptr,
-                        int fuse_ds_ts = 0);
+                        int fuse_ds_ts = 0, bool timed = true);
 
 int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stride, int32_t nchunks, uint8_t* d_dst,
                    int64_t dst_stride, int32_t* d_cbytes, hipStream_t st, Workspace* wsx) {
@@ -2330,7 +2365,7 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
     HIPCHK(hipMemcpyAsync(htpl, P.header, 32, hipMemcpyHostToDevice, st));
     dim3 grid(std::max(1, std::min(64, n / (256 * 16) + 1)), nchunks);
     k_memcpy_chunks<<<grid, 256, 0, st>>>(d_src, src_stride, d_dst, dst_stride, n, nullptr, htpl, d_cbytes,
-                                          P.overhead, P.destsize);
+                                          P.overhead, P.destsize, nullptr);
     HIPCHK(hipGetLastError());
     return 0;
   }
@@ -2379,7 +2414,7 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
       return E_WRITE;
     }
     k_memcpy_chunks<<<dim3(1, nchunks), 256, 0, st>>>(d_src, src_stride, d_dst, dst_stride, n, nullptr, htpl,
-                                                      d_cbytes, P.overhead, P.destsize);
+                                                      d_cbytes, P.overhead, P.destsize, nullptr);
     HIPCHK(hipGetLastError());
     return 0;
   }
@@ -2471,19 +2506,35 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
   }
   ev_filter.stop(st);
   HIPCHK(hipGetLastError());
-  return encode_stage(ws, P, g, filt, raw, raw_stride, d_dst, dst_stride, d_cbytes, nchunks, htpl, ntot, st,
-                      (fuse_shuffle || fuse_dsjob) ? raw : nullptr, fuse_dsjob ? g.ts : 0);
+  const bool fused = g.compcode == 0 && fused_encode_ok(g);
+  rc = encode_stage(ws, P, g, filt, raw, raw_stride, d_dst, dst_stride, d_cbytes, nchunks, htpl, ntot, st,
+                    (fuse_shuffle || fuse_dsjob) ? raw : nullptr, fuse_dsjob ? g.ts : 0);
+  if (rc || !fused || !fuse_rescue()) return rc;
+  // Rescue: a fused launch whose hand-off wait timed out leaves every chunk of the batch
+  // BLOSC2_ERROR_FAILURE (k_fuse_check).  The separate launches are queued behind it, gated on its
+  // timeout word: they redo the batch (filters the fused launch ran, encode, finalize, scatter,
+  // memcpy fallbacks) only when that word is set, and exit at once otherwise -- so the batch API
+  // stays asynchronous and a timeout no longer fails it.
+  g.gate = ws->fsync.as<int32_t>() + 4;
+  if ((fuse_shuffle || fuse_dsjob) && (rc = run_filters())) return rc;
+  const bool was_off = t_fuse_off;
+  t_fuse_off = true;
+  rc = encode_stage(ws, P, g, filt, raw, raw_stride, d_dst, dst_stride, d_cbytes, nchunks, htpl, ntot, st, nullptr, 0,
+                    false);
+  t_fuse_off = was_off;
+  return rc;
 }
 
 // The codec stage of a batch whose filtered images sit at filt + c * g.wstride: encode every stream,
 // then the serial-layout finalisation, the payload scatter and the memcpy fallbacks (from raw).
 static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const uint8_t* filt, const uint8_t* raw,
                         int64_t raw_stride, uint8_t* d_dst, int64_t dst_stride, int32_t* d_cbytes, int32_t nchunks,
-                        const uint8_t* htpl, int64_t ntot, hipStream_t st, const uint8_t* fuse_raw, int fuse_ds_ts) {
+                        const uint8_t* htpl, int64_t ntot, hipStream_t st, const uint8_t* fuse_raw, int fuse_ds_ts,
+                        bool timed) {
   const int32_t n = P.nbytes;
   int rc = 0;
   // encode
-  ev_encode.start(st);
+  if (timed) ev_encode.start(st);
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
   const bool small = std::max(g.neblock, g.leftover) <= 65536;
   StreamResult* res = ws->res.as<StreamResult>();
@@ -2526,10 +2577,10 @@ static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const ui
     if (rc) return rc;
     k_plane_cost<<<1, 1024, 0, st>>>(g, res, (int32_t)ntot, porder);
   }
-  ev_encode.stop(st);
+  if (timed) ev_encode.stop(st);
   HIPCHK(hipGetLastError());
 
-  ev_final.start(st);
+  if (timed) ev_final.start(st);
   Place* place = ws->place.as<Place>();
   int32_t* mode = ws->mode.as<int32_t>();
   if (!fused) {
@@ -2540,9 +2591,9 @@ static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const ui
   {
     dim3 grid(std::max(1, std::min(64, n / (256 * 16) + 1)), nchunks);
     k_memcpy_chunks<<<grid, 256, 0, st>>>(raw, raw_stride, d_dst, dst_stride, n, mode, htpl, d_cbytes,
-                                          P.overhead, P.destsize);
+                                          P.overhead, P.destsize, g.gate);
   }
-  ev_final.stop(st);
+  if (timed) ev_final.stop(st);
   HIPCHK(hipGetLastError());
   return 0;
 }

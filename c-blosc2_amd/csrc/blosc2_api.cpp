@@ -2201,6 +2201,7 @@ void b2h_mean_times(float out[5]) {
 const char* b2h_last_error(void) { return b2h::last_error(); }
 int b2h_debug_stream_results(void* host, int32_t n) { return b2h::debug_stream_results(host, n); }
 int b2h_debug_decode_cycles(void* host, int32_t n) { return b2h::debug_decode_cycles(host, n); }
+int b2h_debug_fuse_timed_out(void) { return b2h::debug_fuse_timed_out(); }
 int b2h_device_count(void) { return b2h::device_count(); }
 
 }  // extern "C"

@@ -205,6 +205,9 @@ BLOSC_EXPORT int b2h_debug_stream_results(void *host, int32_t n);
 /* Diagnostics (B2H_DECODE_DEBUG=1 only): {int64 cycles, int64 kind} per stream of the last
  * decompression batch.  Returns n or < 0. Synchronous. */
 BLOSC_EXPORT int b2h_debug_decode_cycles(void *host, int32_t n);
+/* 1 if the last fused encode launch of the current device's default workspace timed out in a
+ * hand-off wait (its batch was then redone by the gated separate launches), else 0. */
+BLOSC_EXPORT int b2h_debug_fuse_timed_out(void);
 BLOSC_EXPORT int b2h_device_count(void);
 
 #ifdef __cplusplus

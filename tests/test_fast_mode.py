@@ -555,10 +555,10 @@ def test_gpu_fused_launches_on_two_streams_at_once(fast):
 @pytest.mark.gpu
 @pytest.mark.parametrize("lzmode", [1, 0], ids=["fast", "exact"])
 def test_gpu_fused_timeout_falls_back_to_separate_launches(fast, lzmode, monkeypatch):
-    """a fused launch whose hand-off wait times out (simulated: B2H_FUSE_SIMULATE_TIMEOUT
-    starts it with the timeout flag set) fails its whole batch with BLOSC2_ERROR_FAILURE on the
-    asynchronous batch API (documented), while blosc2_compress_ctx, which synchronises anyway,
-    re-runs the chunk with the separate launches and returns the normal chunk."""
+    """ADVICE r2 / VERDICT r4 item 8: a fused launch whose hand-off wait times out (simulated:
+    B2H_FUSE_SIMULATE_TIMEOUT starts it with the timeout flag set) no longer fails its batch: the
+    separate launches queued behind it, gated on its timeout word, redo the batch on the stream
+    (the asynchronous batch API), and blosc2_compress_ctx returns the normal chunk too."""
     import torch
     B = fast
     L = B.lib()
@@ -576,9 +576,63 @@ def test_gpu_fused_timeout_falls_back_to_separate_launches(fast, lzmode, monkeyp
     chunk, n = 4 << 20, 3
     dsrc = torch.from_numpy(gen_f32(29, n * chunk // 4).view(np.uint8)).cuda()
     stride = chunk + 256
-    comp = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
-    cb = torch.zeros(n, dtype=torch.int32, device="cuda")
-    B.compress_batch(B.cparams(clevel=5, typesize=4, lz_mode=lzmode), dsrc.data_ptr(), chunk, n, chunk,
-                     comp.data_ptr(), stride, chunk + 64, cb.data_ptr(), 0)
-    torch.cuda.synchronize()
-    assert (cb.cpu().numpy() == -1).all()   # BLOSC2_ERROR_FAILURE for every chunk of the batch
+    out = {}
+    for sim in ("1", None):
+        if sim:
+            monkeypatch.setenv("B2H_FUSE_SIMULATE_TIMEOUT", sim)
+        else:
+            monkeypatch.delenv("B2H_FUSE_SIMULATE_TIMEOUT")
+        comp = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+        cb = torch.zeros(n, dtype=torch.int32, device="cuda")
+        B.compress_batch(B.cparams(clevel=5, typesize=4, lz_mode=lzmode), dsrc.data_ptr(), chunk, n, chunk,
+                         comp.data_ptr(), stride, chunk + 64, cb.data_ptr(), 0)
+        torch.cuda.synchronize()
+        assert L.b2h_debug_fuse_timed_out() == (1 if sim else 0)
+        cbh = cb.cpu().numpy()
+        assert (cbh > 0).all(), cbh   # the rescue launches redid the batch
+        cm = comp.cpu().numpy().reshape(n, stride)
+        out[sim] = [cm[i, :cbh[i]].copy() for i in range(n)]
+    for a, b in zip(out["1"], out[None]):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grid", [1, 2, 5])
+@pytest.mark.parametrize("kind", ["runs", "raw", "zeros"])
+@pytest.mark.parametrize("lzmode", [1, 2], ids=["fast", "deep"])
+def test_gpu_fused_uniform_stream_batches(fast, lzmode, kind, grid, monkeypatch):
+    """the shape that exposed round 4's non-uniform barrier loops (DESIGN §3,
+    "Barrier loops must be structurized as uniform") -- batches whose streams are ALL runs, all raw
+    (incompressible) or all zero runs, through k_encode_fast_fused with a persistent grid of 1, 2
+    or 5 workgroups (B2H_FUSE_GRID: a few workgroups do every shuffle job, stream, finalisation and
+    scatter item).  The launch must not time out, and its chunks equal the separate launches'."""
+    import torch
+    B = fast
+    L = B.lib()
+    chunk, n = 1 << 20, 6
+    if kind == "runs":
+        host = np.repeat(np.arange(1, n * chunk // 262144 + 1, dtype=np.uint8), 262144)   # every plane a run
+    elif kind == "raw":
+        host = np.random.default_rng(5).integers(0, 256, n * chunk, dtype=np.uint8)
+    else:
+        host = np.zeros(n * chunk, np.uint8)
+    src = torch.from_numpy(host).cuda()
+    stride = chunk + 256
+    cp = B.cparams(clevel=5, typesize=4, lz_mode=lzmode)
+    out = {}
+    for fuse in ("83", "0"):
+        monkeypatch.setenv("B2H_FUSE", fuse)
+        monkeypatch.setenv("B2H_FUSE_GRID", str(grid))
+        comp = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+        cb = torch.zeros(n, dtype=torch.int32, device="cuda")
+        B.compress_batch(cp, src.data_ptr(), chunk, n, chunk, comp.data_ptr(), stride, chunk + 64, cb.data_ptr(), 0)
+        torch.cuda.synchronize()
+        if fuse == "83":
+            assert L.b2h_debug_fuse_timed_out() == 0, "fused launch timed out"
+        cbh = cb.cpu().numpy()
+        assert (cbh > 0).all(), cbh
+        cm = comp.cpu().numpy().reshape(n, stride)
+        out[fuse] = [cm[i, :cbh[i]].copy() for i in range(n)]
+    for i, (a, b) in enumerate(zip(out["83"], out["0"])):
+        assert np.array_equal(a, b), i
+    assert np.array_equal(B.decompress(np.concatenate([out["83"][0]]), chunk), host[:chunk])
