@@ -1318,54 +1318,57 @@ __global__ __launch_bounds__(kBlockThreads) void k_scatter(CGeom g, const Place*
                                                            const uint8_t* __restrict__ sbuf, uint8_t* __restrict__ dst,
                                                            int32_t nstreams_total) {
   if (gated_off(g)) return;
-  const int32_t s = blockIdx.x;
-  if (s >= nstreams_total) return;
-  const int32_t c = s / g.nsc, l = s - c * g.nsc;
-  if (mode[c] != 0) return;
-  int32_t off, len, blk;
-  stream_locate(g, l, &off, &len, &blk);
-  const Place pl = place[s];
-  uint8_t* d = dst + (int64_t)c * g.dst_stride;
-  if (threadIdx.x == 0) {
-    const uint32_t w = (uint32_t)pl.csize;
-    uint8_t* q = d + pl.off - 4;
-    q[0] = (uint8_t)w; q[1] = (uint8_t)(w >> 8); q[2] = (uint8_t)(w >> 16); q[3] = (uint8_t)(w >> 24);
-    if (pl.csize < 0) d[pl.off] = 0x1;   // run-length token
+  for (int32_t s = blockIdx.x; s < nstreams_total; s += gridDim.x) {   // grid: min(streams, kScatterGrid)
+    const int32_t c = s / g.nsc, l = s - c * g.nsc;
+    if (mode[c] != 0) continue;
+    int32_t off, len, blk;
+    stream_locate(g, l, &off, &len, &blk);
+    const Place pl = place[s];
+    uint8_t* d = dst + (int64_t)c * g.dst_stride;
+    if (threadIdx.x == 0) {
+      const uint32_t w = (uint32_t)pl.csize;
+      uint8_t* q = d + pl.off - 4;
+      q[0] = (uint8_t)w; q[1] = (uint8_t)(w >> 8); q[2] = (uint8_t)(w >> 16); q[3] = (uint8_t)(w >> 24);
+      if (pl.csize < 0) d[pl.off] = 0x1;   // run-length token
+    }
+    if (pl.csize <= 0) continue;
+    const uint8_t* src = (pl.csize == len) ? filt + (int64_t)c * g.wstride + off : sbuf + (int64_t)c * g.wstride + off;
+    // each wave moves a contiguous quarter with 16-byte aligned stores (wave_copy)
+    const int32_t nw = kBlockThreads / 64, w = threadIdx.x >> 6;
+    const int32_t q = ((pl.csize + nw - 1) / nw + 15) & ~15;
+    const int32_t a = min(pl.csize, w * q), b = min(pl.csize, a + q);
+    if (b > a) wave_copy((gout_t)(d + pl.off + a), (gin_t)(src + a), b - a);
   }
-  if (pl.csize <= 0) return;
-  const uint8_t* src = (pl.csize == len) ? filt + (int64_t)c * g.wstride + off : sbuf + (int64_t)c * g.wstride + off;
-  // each wave moves a contiguous quarter with 16-byte aligned stores (wave_copy)
-  const int32_t nw = kBlockThreads / 64, w = threadIdx.x >> 6;
-  const int32_t q = ((pl.csize + nw - 1) / nw + 15) & ~15;
-  const int32_t a = min(pl.csize, w * q), b = min(pl.csize, a + q);
-  if (b > a) wave_copy((gout_t)(d + pl.off + a), (gin_t)(src + a), b - a);
 }
+constexpr int32_t kScatterGrid = 16384;
 
 // memcpyed chunks: header + raw bytes.  `only_mode1`: fallback chunks only (mode[] == 1).
 __global__ void k_memcpy_chunks(const uint8_t* __restrict__ src, int64_t src_stride, uint8_t* __restrict__ dst,
                                 int64_t dst_stride, int32_t nbytes, const int32_t* __restrict__ mode,
                                 const uint8_t* __restrict__ header_template, int32_t* __restrict__ cbytes,
-                                int32_t overhead, int32_t destsize, const int32_t* __restrict__ gate) {
+                                int32_t overhead, int32_t destsize, const int32_t* __restrict__ gate, int32_t nchunks) {
   if (gate && __builtin_amdgcn_readfirstlane(__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0)
     return;
-  const int32_t c = blockIdx.y;
-  if (mode && mode[c] != 1) return;
-  const uint8_t* s = src + (int64_t)c * src_stride;
-  uint8_t* d = dst + (int64_t)c * dst_stride;
-  const bool fits = nbytes + overhead <= destsize;
-  if (!mode && blockIdx.x == 0 && (int32_t)threadIdx.x < overhead) {
-    // memcpyed from the start: header written here; cbytes 0 when it cannot fit
-    // (blosc/blosc2.c:3038-3041)
-    uint8_t v = header_template[threadIdx.x];
-    const int32_t cb = fits ? nbytes + overhead : 0;
-    if (threadIdx.x >= 12 && threadIdx.x < 16) v = (uint8_t)(cb >> (8 * (threadIdx.x - 12)));
-    d[threadIdx.x] = v;
-    if (threadIdx.x == 0) cbytes[c] = cb;
+  for (int32_t c = blockIdx.y; c < nchunks; c += gridDim.y) {   // grid.y: min(chunks, kMemcpyGridY)
+    if (mode && mode[c] != 1) continue;
+    const uint8_t* s = src + (int64_t)c * src_stride;
+    uint8_t* d = dst + (int64_t)c * dst_stride;
+    const bool fits = nbytes + overhead <= destsize;
+    if (!mode && blockIdx.x == 0 && (int32_t)threadIdx.x < overhead) {
+      // memcpyed from the start: header written here; cbytes 0 when it cannot fit
+      // (blosc/blosc2.c:3038-3041)
+      uint8_t v = header_template[threadIdx.x];
+      const int32_t cb = fits ? nbytes + overhead : 0;
+      if (threadIdx.x >= 12 && threadIdx.x < 16) v = (uint8_t)(cb >> (8 * (threadIdx.x - 12)));
+      d[threadIdx.x] = v;
+      if (threadIdx.x == 0) cbytes[c] = cb;
+    }
+    if (!fits) continue;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nbytes; i += (int64_t)gridDim.x * blockDim.x)
+      d[overhead + i] = s[i];
   }
-  if (!fits) return;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nbytes; i += (int64_t)gridDim.x * blockDim.x)
-    d[overhead + i] = s[i];
 }
+constexpr int32_t kMemcpyGridY = 256;
 
 // ------------------------------------- fast mode, one launch: shuffle -> encode -> finalize/scatter ----
 // k_encode_fast with the passes on either side of it moved inside the launch, so that their HBM
@@ -1518,6 +1521,89 @@ __device__ void ds_block_wt(const uint8_t* __restrict__ src, const uint8_t* __re
       __builtin_amdgcn_raw_buffer_store_b32(o, r, plane * n + 4 * q, 0, 16);
     }
   }
+}
+
+// The same job over a whole split block, deciding the run verdict on the way (VERDICT r4 item 3,
+// blosc_c's per-stream run test, blosc/blosc2.c:1296-1340): a pass over the block computes every
+// plane, compared with its first byte (byte j of the block's first element after DELTA); the
+// workgroup ORs the mismatches (LDS word `red`), and a second pass writes only the planes that are
+// not runs.  Returns the run planes (bit j: plane j's stream is a run of byte j of element 0) --
+// the encoder never reads them.  A block of runs only (C4's blocks after the first) is read once
+// and writes nothing.  The workgroup calls it together (tid / nth = its threads).
+template <int TS>
+__device__ uint32_t ds_block_runs(const uint8_t* __restrict__ src, const uint8_t* __restrict__ dref, uint8_t* __restrict__ dst,
+                                  int32_t n, bool first_block, int32_t tid, int32_t nth, B2H_LDS uint32_t* red) {
+  const int32_t quads = n / 4;
+  uint32_t rep[TS];
+#pragma unroll
+  for (int p = 0; p < TS; p++) rep[p] = 0x01010101u * (uint32_t)(src[p] ^ (first_block ? 0 : dref[p]));
+  constexpr int EW = TS / 4 > 0 ? TS / 4 : 1;
+  auto planes = [&](int32_t q, uint32_t (&o)[TS]) {
+    uint32_t w[TS], x[TS];
+    load_words<TS>(src, q, w);
+    if (first_block) {
+      if constexpr (TS == 2) {
+        const uint32_t pe = q ? (uint32_t)reinterpret_cast<const uint16_t*>(src)[4 * (int64_t)q - 1] : 0u;
+        x[0] = (w[0] << 16) | pe;
+        x[1] = (w[1] << 16) | (w[0] >> 16);
+      } else {
+        uint32_t prev[EW];
+#pragma unroll
+        for (int k = 0; k < EW; k++) prev[k] = q ? reinterpret_cast<const uint32_t*>(src)[(int64_t)q * TS - EW + k] : 0u;
+#pragma unroll
+        for (int k = 0; k < TS; k++) x[k] = k < EW ? prev[k] : w[k - EW];
+      }
+    } else {
+      load_words<TS>(dref, q, x);
+    }
+#pragma unroll
+    for (int k = 0; k < TS; k++) w[k] ^= x[k];
+#pragma unroll
+    for (int plane = 0; plane < TS; plane++) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int byte = e * TS + plane;
+        v |= ((w[byte / 4] >> (8 * (byte % 4))) & 0xffu) << (8 * e);
+      }
+      o[plane] = v;
+    }
+  };
+  if (tid == 0) *red = 0u;
+  __syncthreads();
+  uint32_t mis = 0;
+  for (int32_t q = tid; q < quads; q += nth) {
+    uint32_t o[TS];
+    planes(q, o);
+#pragma unroll
+    for (int p = 0; p < TS; p++) mis |= (o[p] != rep[p] ? 1u : 0u) << p;
+  }
+  uint32_t wm = 0;
+#pragma unroll
+  for (int p = 0; p < TS; p++) wm |= __ballot((mis >> p) & 1u) ? (1u << p) : 0u;
+  if ((tid & 63) == 0 && wm) __hip_atomic_fetch_or(red, wm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __syncthreads();
+  const uint32_t M = __builtin_amdgcn_readfirstlane(*red);
+  __syncthreads();
+  if (M) {
+    const __amdgpu_buffer_rsrc_t r = wt_rsrc((gout_t)dst);
+    for (int32_t q = tid; q < quads; q += nth) {
+      uint32_t o[TS];
+      planes(q, o);
+#pragma unroll
+      for (int plane = 0; plane < TS; plane++)
+        if ((M >> plane) & 1u) __builtin_amdgcn_raw_buffer_store_b32(o[plane], r, plane * n + 4 * q, 0, 16);
+    }
+  }
+  return ~M & ((1u << TS) - 1u);
+}
+__device__ __noinline__ uint32_t fuse_ds_block_runs(const uint8_t* chunk, uint8_t* d, int32_t ts, int32_t b, int32_t bsize,
+                                                    int32_t bs, B2H_LDS uint32_t* red) {
+  const uint8_t* s = chunk + (int64_t)b * bs;
+  const int32_t tid = threadIdx.x, nth = blockDim.x;
+  if (ts == 8) return ds_block_runs<8>(s, chunk, d, bsize / 8, b == 0, tid, nth, red);
+  if (ts == 4) return ds_block_runs<4>(s, chunk, d, bsize / 4, b == 0, tid, nth, red);
+  return ds_block_runs<2>(s, chunk, d, bsize / 2, b == 0, tid, nth, red);
 }
 
 // The fused launch's filter job for global block k = chunk cc, block b.  The (DELTA, SHUFFLE) job
@@ -1676,6 +1762,7 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
     gin_t in;
     gout_t out;
     int32_t len, clevel, tablog;
+    int32_t run_byte = -1;   // >= 0: the stream is a run of this byte (decided by the filter job)
     bool runs;
     {
       const CGeom g = lds_uniform(&A->g);
@@ -1695,25 +1782,42 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
           const CGeom gk = lds_uniform(&A->g);
           const EncFuse fk = lds_uniform(&A->f);
           const int32_t cc = k / gk.nblocks, b = k - cc * gk.nblocks;
-          const int32_t bsize = (b == gk.nblocks - 1 && gk.leftover) ? gk.leftover : gk.bs;
-          fuse_filter_block(fk, gk, cc, b, bsize, threadIdx.x, blockDim.x);
+          const bool lo = b == gk.nblocks - 1 && gk.leftover;
+          const int32_t bsize = lo ? gk.leftover : gk.bs;
+          // a split (DELTA, SHUFFLE) block of a chunk with run streams (extended header): the run
+          // verdict comes with the filter job, published with the block (ready word 1 | runs << 1)
+          uint32_t runs = 0;
+          if (fk.ds && !lo && gk.spb == fk.ds && gk.overhead == kHdrExt && (fk.mode_bits & 128) == 0) {
+            runs = fuse_ds_block_runs(fk.raw + (int64_t)cc * fk.raw_stride, fk.filt + (int64_t)cc * gk.wstride + (int64_t)b * gk.bs,
+                                      fk.ds, b, bsize, gk.bs, &sh->runred);
+          } else {
+            fuse_filter_block(fk, gk, cc, b, bsize, threadIdx.x, blockDim.x);
+          }
           drain_stores();
           __syncthreads();
           int32_t nk = -1;
           if (threadIdx.x == 0) {
-            st_agent(fk.sync + kFuseHdr + k, 1);
+            st_agent(fk.sync + kFuseHdr + k, (int32_t)(1u | (runs << 1)));
             nk = claim_block(target);
           }
           k = bcast(nk);
         }
         FUSE_TRACE(5, gb);
+        int32_t rv = 0;
         if (threadIdx.x == 0) {
           int32_t* sync = lds_uniform(&A->f.sync);
-          (void)wait_nonzero(sync + kFuseHdr + gb, sync + 4);
+          rv = wait_nonzero(sync + kFuseHdr + gb, sync + 4);
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           drain_stores();
         }
-        __syncthreads();
+        rv = bcast(rv);
+        // the stream's plane was found a run by the filter job: its byte is plane j's of the
+        // block's first element after DELTA, and nothing was stored for it
+        const int32_t j = l - blk * g.spb;
+        if (blk < g.nblocks - (g.leftover ? 1 : 0) && (((uint32_t)rv >> 1) >> j) & 1u) {
+          const uint8_t* raw = f.raw + (int64_t)c * f.raw_stride;
+          run_byte = (int32_t)(uint8_t)(raw[(int64_t)blk * g.bs + j] ^ (blk ? raw[j] : 0));
+        }
       }
       const CGeom g2 = lds_uniform(&A->g);
       in = (gin_t)(lds_uniform(&A->filt) + (int64_t)c * g2.wstride + off);
@@ -1730,7 +1834,16 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
       const CGeom g = lds_uniform(&A->g);
       chain = (B2H_GLB POS*)g.chain + (int64_t)blockIdx.x * chain_len(g);
     }
-    StreamResult r = encode_stream_fast<POS, true, DEEP>(in, len, clevel, out, tab, tablog, oring, sh, runs, matcher, chain);
+    StreamResult r;
+    if (__builtin_amdgcn_readfirstlane(run_byte) >= 0) {   // what the run test would return
+      r.windows = 0;
+      r.cycles = 0;
+      r.peak = 0;
+      r.size = run_byte;
+      r.kind = run_byte ? kStreamByteRun : kStreamZeroRun;
+    } else {
+      r = encode_stream_fast<POS, true, DEEP>(in, len, clevel, out, tab, tablog, oring, sh, runs, matcher, chain);
+    }
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
     if (!matcher && lane_id() == 0) {
@@ -2363,9 +2476,9 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
     if (ws->mode.ensure(64) < 0) return E_MEMORY;
     uint8_t* htpl = ws->mode.as<uint8_t>();
     HIPCHK(hipMemcpyAsync(htpl, P.header, 32, hipMemcpyHostToDevice, st));
-    dim3 grid(std::max(1, std::min(64, n / (256 * 16) + 1)), nchunks);
+    dim3 grid(std::max(1, std::min(64, n / (256 * 16) + 1)), std::min(nchunks, kMemcpyGridY));
     k_memcpy_chunks<<<grid, 256, 0, st>>>(d_src, src_stride, d_dst, dst_stride, n, nullptr, htpl, d_cbytes,
-                                          P.overhead, P.destsize, nullptr);
+                                          P.overhead, P.destsize, nullptr, nchunks);
     HIPCHK(hipGetLastError());
     return 0;
   }
@@ -2413,8 +2526,9 @@ int compress_batch(const CompressPlan& P, const uint8_t* d_src, int64_t src_stri
       snprintf(g_err, sizeof g_err, "dictionary training block overruns the destination");
       return E_WRITE;
     }
-    k_memcpy_chunks<<<dim3(1, nchunks), 256, 0, st>>>(d_src, src_stride, d_dst, dst_stride, n, nullptr, htpl,
-                                                      d_cbytes, P.overhead, P.destsize, nullptr);
+    k_memcpy_chunks<<<dim3(1, std::min(nchunks, kMemcpyGridY)), 256, 0, st>>>(d_src, src_stride, d_dst, dst_stride, n, nullptr,
+                                                                            htpl, d_cbytes, P.overhead, P.destsize, nullptr,
+                                                                            nchunks);
     HIPCHK(hipGetLastError());
     return 0;
   }
@@ -2585,13 +2699,13 @@ static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const ui
   int32_t* mode = ws->mode.as<int32_t>();
   if (!fused) {
     k_finalize<<<(nchunks + 63) / 64, 64, 0, st>>>(g, res, place, mode, d_dst, d_cbytes, nchunks, htpl);
-    k_scatter<<<(uint32_t)ntot, kBlockThreads, 0, st>>>(g, place, mode, res, filt, ws->sbuf.as<uint8_t>(), d_dst,
-                                                        (int32_t)ntot);
+    k_scatter<<<(uint32_t)std::min<int64_t>(ntot, kScatterGrid), kBlockThreads, 0, st>>>(
+        g, place, mode, res, filt, ws->sbuf.as<uint8_t>(), d_dst, (int32_t)ntot);
   }
   {
-    dim3 grid(std::max(1, std::min(64, n / (256 * 16) + 1)), nchunks);
+    dim3 grid(std::max(1, std::min(64, n / (256 * 16) + 1)), std::min(nchunks, kMemcpyGridY));
     k_memcpy_chunks<<<grid, 256, 0, st>>>(raw, raw_stride, d_dst, dst_stride, n, mode, htpl, d_cbytes,
-                                          P.overhead, P.destsize, g.gate);
+                                          P.overhead, P.destsize, g.gate, nchunks);
   }
   if (timed) ev_final.stop(st);
   HIPCHK(hipGetLastError());
@@ -2837,6 +2951,14 @@ __global__ void k_dplan_chunks(const uint8_t* const* __restrict__ srcs, const in
     d.fuse_ds = (d.filters_meta[5] == 0 || d.filters_meta[5] == ts) && (ts == 2 || ts == 4 || ts == 8) &&
                 d.blocksize % (4 * ts) == 0 && d.leftover % (4 * ts) == 0;
   }
+  // (DELTA, SHUFFLE) undone by k_dfilter: a stream that is a run is never
+  // staged -- k_dfilter reads its plane as the run byte straight from the csize word, so at C4's
+  // ratio (~800, almost every stream a run) the decode writes the output once instead of staging
+  // the whole image and reading it back
+  if (K == 2 && d.ferr == 0 && !d.fuse_ds && d.filters[5] == kShuffle && d.filters[4] == kDelta) {
+    const int32_t ts = d.typesize;
+    d.ds_runs = (d.filters_meta[5] == 0 || d.filters_meta[5] == ts) && (ts == 2 || ts == 4 || ts == 8);
+  }
   ch[c] = d;
 }
 
@@ -2847,13 +2969,15 @@ struct DTotals {
   int32_t slot_mask;   // filter slots with a backward filter in any chunk (bit i = slot i)
   int32_t any_special; // some chunk is memcpyed / special (k_dspecial has work)
   int32_t overflow;    // the batch exceeds the table capacities of the sync-free path
+  int32_t any_ds;      // some chunk is ds_runs (k_dfilter_ds has work)
 };
 
 // Single-workgroup exclusive scans (block_base, stream_base, stage_off) + totals.  With
 // capacities (cap_blocks >= 0, the sync-free path) a batch whose tables would not fit fails every
 // chunk with E_MEMORY and leaves nothing for the later kernels to do.
 __global__ __launch_bounds__(1024) void k_dscan(DChunk* __restrict__ ch, int32_t n, DTotals* __restrict__ tot,
-                                                int64_t cap_blocks, int64_t cap_streams, int64_t cap_stage) {
+                                                int64_t cap_blocks, int64_t cap_streams, int64_t cap_stage,
+                                                uint8_t* const* __restrict__ dsts) {
   __shared__ int64_t sb[1024];
   __shared__ int32_t sbk[1024], sst[1024], sdl[1024], smf[1024];
   __shared__ int32_t s_over;
@@ -2868,8 +2992,16 @@ __global__ __launch_bounds__(1024) void k_dscan(DChunk* __restrict__ ch, int32_t
     st += ch[i].nstreams;
     dl |= (ch[i].has_delta && !ch[i].fuse_ds) ? 0x100 : 0;
     dl |= (ch[i].nstreams == 0 && ch[i].nbytes != 0) ? 0x200 : 0;   // k_dspecial's chunks
+    dl |= ch[i].nstreams && (ch[i].nbytes & 15) ? 0x400 : 0;        // a stage offset not 16-aligned follows
+    dl |= ch[i].ds_runs ? 0x800 : 0;
+    // a ds_runs chunk whose every block takes the one-pass form leaves k_dfilter nothing to do
+    // (decided for sure once every stage offset is 16-aligned: bit 0x400 clear batch-wide)
+    const int32_t ts = ch[i].typesize;
+    const bool all_fast = ch[i].ds_runs && ch[i].blocksize % (4 * ts) == 0 && ch[i].leftover % (4 * ts) == 0 &&
+                          (reinterpret_cast<uintptr_t>(dsts[i]) & 15) == 0 && ch[i].blocksize % 16 == 0;
     for (int f = 0; f < 6; f++)
-      if (!bwd_noop(ch[i].filters[f]) && !ch[i].fuse_unshuffle && !ch[i].fuse_ds) dl |= 1 << f;
+      if (!bwd_noop(ch[i].filters[f]) && !ch[i].fuse_unshuffle && !ch[i].fuse_ds)
+        dl |= all_fast ? (1 << (12 + f)) : (1 << f);
     mf = max(mf, (int32_t)ch[i].nfilters_bwd);
   }
   sb[threadIdx.x] = a; sbk[threadIdx.x] = bk; sst[threadIdx.x] = st; sdl[threadIdx.x] = dl; smf[threadIdx.x] = mf;
@@ -2888,8 +3020,10 @@ __global__ __launch_bounds__(1024) void k_dscan(DChunk* __restrict__ ch, int32_t
     tot->stage_bytes = over ? 0 : ra;
     tot->nblocks = over ? 0 : (int32_t)rb;
     tot->nstreams = over ? 0 : (int32_t)rs;
-    tot->any_delta = (rd >> 8) & 1; tot->slot_mask = over ? 0 : rd & 0x3f; tot->max_filters = rm;
+    const int32_t slots = (rd & 0x3f) | (((rd >> 10) & 1) ? (rd >> 12) & 0x3f : 0);
+    tot->any_delta = (rd >> 8) & 1; tot->slot_mask = over ? 0 : slots; tot->max_filters = rm;
     tot->any_special = over ? 0 : (rd >> 9) & 1;
+    tot->any_ds = over ? 0 : (rd >> 11) & 1;
   }
   __syncthreads();
   const bool over = s_over;
@@ -3036,13 +3170,13 @@ __device__ __forceinline__ bool decode_stream(const uint8_t* const* __restrict__
   const int32_t blk = st.dst_off / d.blocksize;
   const int32_t step = 1 + (st.dst_off - blk * d.blocksize) / nb;
   if (st.csize == 0) {
-    wave_fill<true>(out, 0, nb);
+    if (!d.ds_runs) wave_fill<true>(out, 0, nb);   // ds_runs: k_dfilter synthesises the plane
   } else if (st.csize < 0) {
     const uint8_t token = in[0];
     if (!(token & 1) || st.csize < -255) {
       if (lane == 0) rec_err(ch, c, blk, step, E_RUNLEN);
     } else {
-      wave_fill<true>(out, (uint8_t)(-st.csize), nb);
+      if (!d.ds_runs) wave_fill<true>(out, (uint8_t)(-st.csize), nb);
       *kind_out = 1;
     }
   } else if (st.csize == nb) {
@@ -3433,7 +3567,46 @@ __device__ __forceinline__ bool fused_delta_shuffle(const DChunk& d, int32_t bsi
 
 // Backward filter for filter slot `slot` on one block; pass 0: all blocks, 1: block 0 only,
 // 2: blocks >= 1.  Every early return is uniform over the workgroup.
+// A (DELTA, SHUFFLE) block undone in one pass (unshuffle + un-delta, stage -> dst): whole quads,
+// 16-byte aligned image and destination.  k_dfilter_ds and k_dfilter take the same decision.
+__device__ __forceinline__ bool ds_fast_block(const DChunk& d, int32_t bsize, const uint8_t* img, const uint8_t* out,
+                                              const uint8_t* dst0) {
+  return fused_delta_shuffle(d, bsize) && aligned16(img) && aligned16(out) && aligned16(dst0);
+}
+
+// The run planes of block `bk` of a ds_runs chunk: bit j of the mask = plane j's stream is a run,
+// byte j of *rb its byte (a block of one stream -- unsplit or the leftover -- that is a run has
+// every plane of its byte).  Wave-uniform.
+__device__ __forceinline__ uint32_t block_run_planes(const DChunk& d, const DStream* __restrict__ streams,
+                                                     const DBlock& bk, uint64_t* rb) {
+  const int32_t ts = d.typesize;
+  const int32_t full = d.nblocks - (d.leftover ? 1 : 0);
+  const bool split = !d.dont_split && bk.block < full;
+  const int32_t spb = d.dont_split ? 1 : ts;
+  const int32_t s0 = d.stream_base + (bk.block < full ? bk.block * spb : full * spb);
+  uint32_t rm = 0;
+  uint64_t b = 0;
+  if (split) {
+    for (int j = 0; j < ts; j++) {
+      const int32_t cs = __builtin_amdgcn_readfirstlane(streams[s0 + j].csize);
+      if (cs <= 0) {
+        rm |= 1u << j;
+        b |= (uint64_t)(uint8_t)(-cs) << (8 * j);
+      }
+    }
+  } else {
+    const int32_t cs = __builtin_amdgcn_readfirstlane(streams[s0].csize);
+    if (cs <= 0) {
+      rm = (1u << ts) - 1;
+      b = 0x0101010101010101ull * (uint8_t)(-cs);
+    }
+  }
+  *rb = b;
+  return rm;
+}
+
 __device__ __forceinline__ void dfilter_block(DChunk* __restrict__ ch, const DBlock* __restrict__ blocks,
+                                              const DStream* __restrict__ streams,
                                               uint8_t* const* __restrict__ dsts, uint8_t* __restrict__ stage,
                                               uint8_t* __restrict__ stage2, int slot, int pass, int32_t idx,
                                               const uint8_t* __restrict__ maskout, int32_t mask_stride) {
@@ -3449,21 +3622,20 @@ __device__ __forceinline__ void dfilter_block(DChunk* __restrict__ ch, const DBl
   const int32_t bsize = lo ? d.leftover : d.blocksize;
   const int64_t off = (int64_t)bk.block * d.blocksize;
   uint8_t* bufs[3] = {stage + d.stage_off + off, stage2 + d.stage_off + off, dsts[bk.chunk] + off};
-  // (DELTA, SHUFFLE) pipelines: the slot-5 launch unshuffles and un-deltas in one pass (stage ->
-  // dst), the slot-4 launch then has nothing left to do; both launches take the same decision.
-  if (fused_delta_shuffle(d, bsize) && aligned16(bufs[0]) && aligned16(bufs[2]) && aligned16(dsts[bk.chunk])) {
-    if (slot != 5) return;
-    const int32_t ne = bsize / d.typesize;
-    if (bk.block == 0 || d.delta_self) {
-      if (d.typesize == 4) unshuffle_scan_fast<4>(bufs[0], bufs[2], ne);
-      else if (d.typesize == 8) unshuffle_scan_fast<8>(bufs[0], bufs[2], ne);
-      else unshuffle_scan_fast<2>(bufs[0], bufs[2], ne);
-    } else {
-      if (d.typesize == 4) unshuffle_xor_fast<4>(bufs[0], dsts[bk.chunk], bufs[2], ne);
-      else if (d.typesize == 8) unshuffle_xor_fast<8>(bufs[0], dsts[bk.chunk], bufs[2], ne);
-      else unshuffle_xor_fast<2>(bufs[0], dsts[bk.chunk], bufs[2], ne);
+  // (DELTA, SHUFFLE) blocks in the one-pass form are k_dfilter_ds's (both slots)
+  if (d.ds_runs && ds_fast_block(d, bsize, bufs[0], bufs[2], dsts[bk.chunk])) return;
+  uint64_t rb = 0;
+  const uint32_t rm = d.ds_runs ? block_run_planes(d, streams, bk, &rb) : 0u;
+  if (rm && slot == 5) {   // any other form of the block: its run planes staged first, then as usual
+    const int32_t ts = d.typesize;
+    const int32_t pl = (d.dont_split || lo) ? bsize : bsize / ts;   // bytes per stream of the block
+    const int32_t ns = (d.dont_split || lo) ? 1 : ts;
+    for (int j = 0; j < ns; j++) {
+      if (!((rm >> j) & 1)) continue;
+      const uint8_t v = (uint8_t)(rb >> (8 * j));
+      for (int32_t i = threadIdx.x; i < pl; i += blockDim.x) bufs[0][(int64_t)j * pl + i] = v;
     }
-    return;
+    __syncthreads();
   }
   const uint8_t* s = bufs[d.fsrc[slot]];
   uint8_t* o = bufs[d.fdst[slot]];
@@ -3480,11 +3652,85 @@ __device__ __forceinline__ void dfilter_block(DChunk* __restrict__ ch, const DBl
   }
 }
 
+// (DELTA, SHUFFLE) chunks' blocks in the one-pass form (DChunk::ds_runs + ds_fast_block): un-shuffle
+// and un-delta stage -> dst, run planes synthesised from their csize words (never staged).  pass 1
+// block 0 (an XOR scan), pass 2 the other blocks (XOR with the final block 0).  A kernel of its own:
+// in the generic k_dfilter the bitunshuffle / bytedelta paths held it at 211 VGPRs (2 waves per
+// SIMD), which left this bandwidth pass latency-bound.
+// Block b >= 1 of a chunk of at most kDsFuseBlocks blocks whose output pass 1 writes together with
+// block 0's (every plane a run: the block is a constant element XORed with block 0's output).
+// Decided the same way by pass 1 (for block 0's workgroup) and pass 2 (which then skips it).
+constexpr int32_t kDsFuseBlocks = 4;
+__device__ __forceinline__ bool ds_later_fused(const DChunk& d, const DStream* __restrict__ streams, int32_t c, int32_t b,
+                                               uint8_t* const* __restrict__ dsts, const uint8_t* __restrict__ stage,
+                                               const uint8_t* __restrict__ maskout, int32_t mask_stride, uint64_t* rb) {
+  if (d.delta_self || d.nblocks < 2 || d.nblocks > kDsFuseBlocks || b < 1 || b >= d.nblocks) return false;
+  const int32_t ts = d.typesize;
+  const bool lo0 = d.nblocks == 1 && d.leftover;
+  const int32_t bs0 = lo0 ? d.leftover : d.blocksize;
+  if (maskout && (maskout[(int64_t)c * mask_stride] || maskout[(int64_t)c * mask_stride + b])) return false;
+  if (!ds_fast_block(d, bs0, stage + d.stage_off, dsts[c], dsts[c])) return false;
+  const bool lo = b == d.nblocks - 1 && d.leftover;
+  const int32_t bsize = lo ? d.leftover : d.blocksize;
+  if (bsize != bs0) return false;   // the scan writes block 0's element count
+  const int64_t off = (int64_t)b * d.blocksize;
+  if (!ds_fast_block(d, bsize, stage + d.stage_off + off, dsts[c] + off, dsts[c])) return false;
+  DBlock bk;
+  bk.chunk = c;
+  bk.block = b;
+  return block_run_planes(d, streams, bk, rb) == (1u << ts) - 1u;
+}
+
+__global__ __launch_bounds__(kBlockThreads) void k_dfilter_ds(DChunk* __restrict__ ch, const DBlock* __restrict__ blocks,
+                                                              const DStream* __restrict__ streams,
+                                                              uint8_t* const* __restrict__ dsts, uint8_t* __restrict__ stage,
+                                                              int pass, const DTotals* __restrict__ tot,
+                                                              const uint8_t* __restrict__ maskout, int32_t mask_stride) {
+  if (!tot->any_ds) return;
+  const int32_t nb = tot->nblocks;
+  for (int32_t idx = blockIdx.x; idx < nb; idx += gridDim.x) {
+    const DBlock bk = blocks[idx];
+    if (pass == 1 && bk.block != 0) continue;
+    if (pass == 2 && bk.block == 0) continue;
+    const DChunk d = ch[bk.chunk];
+    if (d.status < 0 || !d.ds_runs) continue;
+    if (maskout && maskout[(int64_t)bk.chunk * mask_stride + bk.block]) continue;
+    const bool lo = (bk.block == d.nblocks - 1) && d.leftover;
+    const int32_t bsize = lo ? d.leftover : d.blocksize;
+    const int64_t off = (int64_t)bk.block * d.blocksize;
+    const uint8_t* img = stage + d.stage_off + off;
+    uint8_t* out = dsts[bk.chunk] + off;
+    if (!ds_fast_block(d, bsize, img, out, dsts[bk.chunk])) continue;
+    uint64_t rb = 0;
+    const uint32_t rm = block_run_planes(d, streams, bk, &rb);
+    const int32_t ne = bsize / d.typesize;
+    if (bk.block == 0 || d.delta_self) {
+      int nx = 0;
+      uint8_t* xout[kDsFuseBlocks - 1];
+      uint64_t xrb[kDsFuseBlocks - 1];
+      if (bk.block == 0)
+        for (int32_t b = 1; b < min(d.nblocks, kDsFuseBlocks); b++)
+          if (ds_later_fused(d, streams, bk.chunk, b, dsts, stage, maskout, mask_stride, &xrb[nx]))
+            xout[nx++] = dsts[bk.chunk] + (int64_t)b * d.blocksize;
+      if (d.typesize == 4) unshuffle_scan_fast<4>(img, out, ne, rm, rb, nx, xout, xrb);
+      else if (d.typesize == 8) unshuffle_scan_fast<8>(img, out, ne, rm, rb, nx, xout, xrb);
+      else unshuffle_scan_fast<2>(img, out, ne, rm, rb, nx, xout, xrb);
+    } else {
+      uint64_t xr;
+      if (ds_later_fused(d, streams, bk.chunk, bk.block, dsts, stage, maskout, mask_stride, &xr)) continue;   // pass 1 wrote it
+      if (d.typesize == 4) unshuffle_xor_fast<4>(img, dsts[bk.chunk], out, ne, rm, rb);
+      else if (d.typesize == 8) unshuffle_xor_fast<8>(img, dsts[bk.chunk], out, ne, rm, rb);
+      else unshuffle_xor_fast<2>(img, dsts[bk.chunk], out, ne, rm, rb);
+    }
+  }
+}
+
 // Grid-stride over the batch's blocks (count and active slots from the device totals, so the
 // sync-free path can launch every slot and pass: the ones with nothing to do exit at once).
 // pass 1 / 2 are the block-0-first halves of a delta pipeline; without any delta chunk pass 1
 // runs every block and pass 2 nothing.
 __global__ __launch_bounds__(kBlockThreads) void k_dfilter(DChunk* __restrict__ ch, const DBlock* __restrict__ blocks,
+                                                           const DStream* __restrict__ streams,
                                                            uint8_t* const* __restrict__ dsts, uint8_t* __restrict__ stage,
                                                            uint8_t* __restrict__ stage2, int slot, int pass,
                                                            const DTotals* __restrict__ tot,
@@ -3496,7 +3742,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_dfilter(DChunk* __restrict__ 
   }
   const int32_t nb = tot->nblocks;
   for (int32_t idx = blockIdx.x; idx < nb; idx += gridDim.x)
-    dfilter_block(ch, blocks, dsts, stage, stage2, slot, pass, idx, maskout, mask_stride);
+    dfilter_block(ch, blocks, streams, dsts, stage, stage2, slot, pass, idx, maskout, mask_stride);
 }
 
 // memcpyed / special chunks (blosc/blosc2.c:1865-1935): grid (pieces, chunks), chunks strided.
@@ -3581,7 +3827,7 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
   const char* fds = getenv("B2H_DEC_FUSE_DS");
   const int ds_off = (d_maskout || !(fds && atoi(fds) == 1)) ? 16 : 0;
   k_dplan_chunks<<<(n + 255) / 256, 256, 0, st>>>(d_src, d_srcsize, d_dstsize, ch, n, mode | no_fuse | ds_off);
-  k_dscan<<<1, 1024, 0, st>>>(ch, n, tot, cap_blocks, cap_streams, cap_stage);
+  k_dscan<<<1, 1024, 0, st>>>(ch, n, tot, cap_blocks, cap_streams, cap_stage, d_dst);
   HIPCHK(hipGetLastError());
   DTotals h{};
   if (bounded) {
@@ -3592,6 +3838,7 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
     h.slot_mask = 0x3f;     // every slot launched; the kernels read the real mask
     h.any_delta = 1;
     h.any_special = 1;
+    h.any_ds = 1;
   } else {
     HIPCHK(hipMemcpyAsync(&h, tot, sizeof h, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -3641,9 +3888,12 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
       const int passes = h.any_delta ? 2 : 1;
       for (int ps = 0; ps < passes; ps++) {
         const int pass = h.any_delta ? ps + 1 : 0;
+        if (pass > 0 && h.any_ds)
+          k_dfilter_ds<<<grid, kBlockThreads, 0, st>>>(ch, blocks, ws->dstreams.as<DStream>(), d_dst, ws->stage.as<uint8_t>(),
+                                                       pass, tot, d_maskout, mask_stride);
         for (int slot = 5; slot >= 0; slot--)
           if ((h.slot_mask >> slot) & 1)
-            k_dfilter<<<grid, kBlockThreads, 0, st>>>(ch, blocks, d_dst, ws->stage.as<uint8_t>(),
+            k_dfilter<<<grid, kBlockThreads, 0, st>>>(ch, blocks, ws->dstreams.as<DStream>(), d_dst, ws->stage.as<uint8_t>(),
                                                      ws->stage2.as<uint8_t>(), slot, pass, tot, d_maskout, mask_stride);
       }
     }

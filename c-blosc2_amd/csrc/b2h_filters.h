@@ -78,6 +78,17 @@ __device__ __forceinline__ void load_planes(const uint8_t* __restrict__ src, int
 #pragma unroll
   for (int plane = 0; plane < TS; plane++) p[plane] = reinterpret_cast<const uint32_t*>(src + (int64_t)plane * pstride)[q];
 }
+// The same with run planes: plane j with bit j of `rm` (wave-uniform) is byte j of `rb` throughout
+// and is not read (the decoder never staged it).
+template <int TS>
+__device__ __forceinline__ void load_planes_r(const uint8_t* __restrict__ src, int32_t q, int64_t pstride, uint32_t (&p)[TS],
+                                              uint32_t rm, uint64_t rb) {
+#pragma unroll
+  for (int plane = 0; plane < TS; plane++) {
+    if ((rm >> plane) & 1u) p[plane] = 0x01010101u * (uint32_t)((rb >> (8 * plane)) & 0xffu);
+    else p[plane] = reinterpret_cast<const uint32_t*>(src + (int64_t)plane * pstride)[q];
+  }
+}
 
 template <int TS>
 __device__ __forceinline__ void store_quad(uint8_t* __restrict__ dst, int32_t q, const uint32_t (&p)[TS]) {
@@ -513,14 +524,14 @@ __device__ __forceinline__ void store_words(uint8_t* __restrict__ dst, int32_t q
 // Decode, blocks >= 1: dst = unshuffle(src) ^ dref (dref = the chunk's decoded block 0).
 template <int TS>
 __device__ void unshuffle_xor_fast(const uint8_t* __restrict__ src, const uint8_t* __restrict__ dref,
-                                   uint8_t* __restrict__ dst, int32_t n) {
+                                   uint8_t* __restrict__ dst, int32_t n, uint32_t rm = 0, uint64_t rb = 0) {
   const int32_t quads = n / 4, T = blockDim.x;
   int32_t q = threadIdx.x;
   for (; q + (kQuadUnroll - 1) * T < quads; q += kQuadUnroll * T) {
     uint32_t p[kQuadUnroll][TS], r[kQuadUnroll][TS];
 #pragma unroll
     for (int u = 0; u < kQuadUnroll; u++) {
-      load_planes<TS>(src, q + u * T, n, p[u]);
+      load_planes_r<TS>(src, q + u * T, n, p[u], rm, rb);
       load_words<TS>(dref, q + u * T, r[u]);
     }
 #pragma unroll
@@ -534,7 +545,7 @@ __device__ void unshuffle_xor_fast(const uint8_t* __restrict__ src, const uint8_
   }
   for (; q < quads; q += T) {
     uint32_t p[TS], r[TS], w[TS];
-    load_planes<TS>(src, q, n, p);
+    load_planes_r<TS>(src, q, n, p, rm, rb);
     load_words<TS>(dref, q, r);
     planes_to_words<TS>(p, w);
 #pragma unroll
@@ -546,7 +557,20 @@ __device__ void unshuffle_xor_fast(const uint8_t* __restrict__ src, const uint8_
 // Decode, block 0: dst = inclusive XOR-scan over elements of unshuffle(src).  The tiles of
 // delta_scan_tiles with a quad (TS / 2 u64 words) as each lane's piece.
 template <int TS>
-__device__ void unshuffle_scan_fast(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t n) {
+__device__ void unshuffle_scan_fast(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t n, uint32_t rm = 0,
+                                    uint64_t rb = 0, int nx = 0, uint8_t* const* xout = nullptr,
+                                    const uint64_t* xrb = nullptr) {
+  // nx (<= 3) more outputs: blocks of the same chunk whose every plane is a run of xrb[i]'s bytes,
+  // i.e. a constant element v_i after the un-shuffle, so their output is v_i ^ this block's
+  // (delta_decoder's other-block rule) -- written here from registers instead of re-reading
+  // this block in a second pass
+  uint32_t xw[3][TS];
+  for (int i = 0; i < 3; i++) {
+    uint32_t pr[TS];
+#pragma unroll
+    for (int j = 0; j < TS; j++) pr[j] = i < nx ? 0x01010101u * (uint32_t)((xrb[i] >> (8 * j)) & 0xffu) : 0u;
+    planes_to_words<TS>(pr, xw[i]);
+  }
   constexpr int U = 2, K = TS / 2;
   __shared__ uint64_t wt[2][U][kBlockThreads / 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
@@ -561,7 +585,7 @@ __device__ void unshuffle_scan_fast(const uint8_t* __restrict__ src, uint8_t* __
     for (int u = 0; u < U; u++) {
       const int32_t q = base + u * T + (int32_t)threadIdx.x;
       if (q < quads) {
-        load_planes<TS>(src, q, n, pn[u]);
+        load_planes_r<TS>(src, q, n, pn[u], rm, rb);
       } else {
 #pragma unroll
         for (int k = 0; k < TS; k++) pn[u][k] = 0u;
@@ -620,6 +644,12 @@ __device__ void unshuffle_scan_fast(const uint8_t* __restrict__ src, uint8_t* __
           w[2 * k + 1] = (uint32_t)(o >> 32);
         }
         store_words<TS>(dst, q, w);
+        for (int i = 0; i < nx; i++) {
+          uint32_t y[TS];
+#pragma unroll
+          for (int k = 0; k < TS; k++) y[k] = w[k] ^ xw[i][k];
+          store_words<TS>(xout[i], q, y);
+        }
       }
       c ^= all;
     }

@@ -65,6 +65,8 @@ struct DChunk {
   int8_t ferr;                 // backward-pipeline error of every decoded block (0, -1, -18)
   uint8_t fuse_unshuffle;      // the lone backward filter is SHUFFLE: undone inside the decode launch
   uint8_t fuse_ds;             // (DELTA, SHUFFLE) at typesize 2/4/8: undone inside the decode launch
+  uint8_t ds_runs;             // (DELTA, SHUFFLE) undone by k_dfilter, whose planes of run streams it
+                               // synthesises from the csize word: k_decode leaves them unwritten
   int32_t dict_off, dict_size; // LZ4 dictionary section (BLOSC2_USEDICT): offset in the chunk, bytes
 };
 

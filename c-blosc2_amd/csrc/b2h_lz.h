@@ -227,29 +227,56 @@ struct GlbTab {
 // `bound` (get_match / get_run semantics, blosc/blosclz.c:119-165).  64 lanes x 16 bytes per step.
 __device__ __forceinline__ int32_t wave_match_end(gin_t in, int32_t x, uint32_t d, int32_t bound) {
   const int lane = lane_id();
-  while (x < bound) {
-    const int32_t q = x + lane * 16;
+  // first mismatch in 16 bytes at q (16: none; bytes at and after `bound` do not count)
+  auto first16 = [&](int32_t q, const uint32_t (&a)[4], const uint32_t (&b)[4]) {
     int32_t first = 16;
-    if (q < bound) {
-      uint32_t a[4], b[4];
-      ld16(in + q, a);
-      ld16(in + q - d, b);
-      const int32_t nb = bound - q;   // bytes at and after `bound` do not count
+    const int32_t nb = bound - q;
 #pragma unroll
-      for (int k = 3; k >= 0; k--) {
-        uint32_t diff = a[k] ^ b[k];
-        const int32_t lo = 4 * k;
-        if (nb <= lo) diff = 0;
-        else if (nb < lo + 4) diff &= (1u << (8 * (nb - lo))) - 1u;
-        if (diff) first = lo + (__builtin_ctz(diff) >> 3);
-      }
+    for (int k = 3; k >= 0; k--) {
+      uint32_t diff = a[k] ^ b[k];
+      const int32_t lo = 4 * k;
+      if (nb <= lo) diff = 0;
+      else if (nb < lo + 4) diff &= (1u << (8 * (nb - lo))) - 1u;
+      if (diff) first = lo + (__builtin_ctz(diff) >> 3);
     }
+    return q < bound ? first : 16;
+  };
+  // 1 KiB per step first (most extensions end there); a match still running after it moves to
+  // 4 KiB steps with every lane's four 16-byte pairs in flight at once -- a step is one memory
+  // round trip, and long runs of repeats (C4's delta planes: one match per 64 KiB stream) would
+  // otherwise pay 64 of them per stream
+  if (x < bound) {
+    const int32_t q = x + lane * 16;
+    uint32_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+    if (q < bound) { ld16(in + q, a); ld16(in + q - d, b); }
+    const int32_t first = first16(q, a, b);
     const uint64_t mm = __ballot(first < 16);
     if (mm) {
       const int l = __builtin_ctzll(mm);
       return x + l * 16 + rdlane(first, l) + 1;
     }
     x += 1024;
+  }
+  while (x < bound) {
+    uint32_t a[4][4], b[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int32_t q = x + u * 1024 + lane * 16;
+#pragma unroll
+      for (int k = 0; k < 4; k++) { a[u][k] = 0; b[u][k] = 0; }
+      if (q < bound) { ld16(in + q, a[u]); ld16(in + q - d, b[u]); }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int32_t q = x + u * 1024 + lane * 16;
+      const int32_t first = first16(q, a[u], b[u]);
+      const uint64_t mm = __ballot(first < 16);
+      if (mm) {
+        const int l = __builtin_ctzll(mm);
+        return x + u * 1024 + l * 16 + rdlane(first, l) + 1;
+      }
+    }
+    x += 4096;
   }
   return bound;
 }

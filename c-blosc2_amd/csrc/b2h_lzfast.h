@@ -110,6 +110,7 @@ struct FastShared {          // per workgroup, after the table and the output ri
   int32_t decide[2];         // the stream's probe decision / run verdict (parser -> both)
   int32_t pull;              // the stream index the workgroup pulled
   int32_t bcast;             // k_encode_fast_fused: claims and hand-off words, lane 0 -> workgroup
+  uint32_t runred;           // k_encode_fast_fused: the (DELTA, SHUFFLE) job's plane-mismatch OR
 };
 
 // Pass limits shared by both roles (blosc/blosclz.c:440-482, get_cratio 320-419).

@@ -384,7 +384,7 @@ def test_gpu_deep_mode_ratio(fast, data):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("lzmode", [1, 2, 0], ids=["fast", "deep", "exact"])
-@pytest.mark.parametrize("shape", ["T", "leftover", "clevel9_ts8", "ds8", "ds2_leftover", "ds4_odd_leftover"])
+@pytest.mark.parametrize("shape", ["T", "leftover", "clevel9_ts8", "ds8", "ds8_ramp", "ds2_leftover", "ds4_odd_leftover"])
 def test_gpu_fused_launch_matches_separate_launches(fast, shape, lzmode, monkeypatch):
     """The one-launch fast-mode encode (byte shuffle, finalize and payload scatter inside the
     encoder launch, k_encode_fast_fused) writes the same chunks as the separate launches
@@ -402,11 +402,15 @@ def test_gpu_fused_launch_matches_separate_launches(fast, shape, lzmode, monkeyp
         chunk, n, kw = 1 << 20, 12, dict(clevel=9, typesize=8)
     elif shape == "ds8":   # C4's pipeline: (DELTA, SHUFFLE) filtered inside the encoder launch
         chunk, n, kw = 1 << 20, 12, dict(clevel=5, typesize=8, filters=(0, 0, 0, 0, 3, 1))
+    elif shape == "ds8_ramp":   # C4 exactly: the blocks after the first are runs in every plane
+        chunk, n, kw = 1 << 20, 12, dict(clevel=5, typesize=8, filters=(0, 0, 0, 0, 3, 1))
     elif shape == "ds2_leftover":   # a leftover block of whole 64-byte groups: still fused
         chunk, n, kw = (1 << 20) + 64 * 3, 12, dict(clevel=5, typesize=2, filters=(0, 0, 0, 0, 3, 1), blocksize=1 << 18)
     else:   # leftover not of whole 64-byte groups: the separate k_ffilter_ds launch
         chunk, n, kw = (1 << 20) + 4 * 37, 12, dict(clevel=5, typesize=4, filters=(0, 0, 0, 0, 3, 1), blocksize=1 << 18)
-    if shape.startswith("ds"):
+    if shape == "ds8_ramp":
+        src = torch.from_numpy(int64_ramp(7, n * chunk // 8).view(np.uint8).copy()).to(dev)
+    elif shape.startswith("ds"):
         rng = np.random.default_rng(11)   # a ramp with jitter: run, raw and LZ streams after the filters
         ramp = int64_ramp(7, n * chunk // 8 + 1) * 3 + rng.integers(0, 8, n * chunk // 8 + 1)
         src = torch.from_numpy(ramp.view(np.uint8)[:n * chunk].copy()).to(dev)
