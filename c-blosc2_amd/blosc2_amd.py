@@ -77,6 +77,39 @@ class Storage(C.Structure):
                 ("dparams", C.c_void_p), ("io", C.c_void_p)]
 
 
+class IO(C.Structure):
+    """blosc2_io (reference include/blosc2.h:1047-1059)."""
+    _fields_ = [("id", C.c_uint8), ("name", C.c_char_p), ("params", C.c_void_p)]
+
+
+OPEN_CB = C.CFUNCTYPE(C.c_void_p, C.c_char_p, C.c_char_p, C.c_void_p)
+CLOSE_CB = C.CFUNCTYPE(C.c_int, C.c_void_p)
+SIZE_CB = C.CFUNCTYPE(C.c_int64, C.c_void_p)
+WRITE_CB = C.CFUNCTYPE(C.c_int64, C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p)
+READ_CB = C.CFUNCTYPE(C.c_int64, C.POINTER(C.c_void_p), C.c_int64, C.c_int64, C.c_int64, C.c_void_p)
+TRUNCATE_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64)
+DESTROY_CB = C.CFUNCTYPE(C.c_int, C.c_void_p)
+
+
+class IOCb(C.Structure):
+    """blosc2_io_cb (reference include/blosc2.h:1018-1041)."""
+    _fields_ = [("id", C.c_uint8), ("name", C.c_char_p), ("is_allocation_necessary", C.c_bool),
+                ("open", OPEN_CB), ("close", CLOSE_CB), ("size", SIZE_CB), ("write", WRITE_CB),
+                ("read", READ_CB), ("truncate", TRUNCATE_CB), ("destroy", DESTROY_CB)]
+
+
+class StdioMmap(C.Structure):
+    """blosc2_stdio_mmap (reference include/blosc2/blosc2-stdio.h:76-116, POSIX layout)."""
+    _fields_ = [("mode", C.c_char_p), ("initial_mapping_size", C.c_size_t), ("needs_free", C.c_bool),
+                ("addr", C.c_void_p), ("urlpath", C.c_char_p), ("file_size", C.c_size_t),
+                ("mapping_size", C.c_size_t), ("is_memory_only", C.c_bool), ("file", C.c_void_p),
+                ("fd", C.c_int), ("access_flags", C.c_int64), ("map_flags", C.c_int64)]
+
+    @classmethod
+    def defaults(cls, mode=b"r"):
+        return cls(mode, 1 << 30, False, None, None, 0, 0, False, None, -1, -1, -1)
+
+
 class Schunk(C.Structure):
     """blosc2_schunk (reference include/blosc2.h:1823-1892), ABI-identical."""
     _fields_ = [
@@ -94,6 +127,17 @@ class Schunk(C.Structure):
 
 SCHUNK_COUNTERS = ("nchunks", "current_nchunk", "nbytes", "cbytes", "chunksize", "flags2", "typesize",
                    "blocksize", "clevel", "compcode", "splitmode", "use_dict", "data_len")
+
+
+_LIBC = None
+
+
+def _libc():
+    global _LIBC
+    if _LIBC is None:
+        _LIBC = C.CDLL(None)
+        _LIBC.free.argtypes = [C.c_void_p]
+    return _LIBC
 
 
 def bind_schunk(lib):
@@ -124,7 +168,13 @@ def bind_schunk(lib):
         "blosc2_schunk_from_buffer": ([vp, i64, C.c_bool], sp),
         "blosc2_schunk_open": ([C.c_char_p], sp),
         "blosc2_schunk_open_offset": ([C.c_char_p, i64], sp),
+        "blosc2_schunk_open_udio": ([C.c_char_p, vp], sp),
+        "blosc2_schunk_open_offset_udio": ([C.c_char_p, i64, vp], sp),
         "blosc2_schunk_to_buffer": ([sp, C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_bool)], i64),
+        "blosc2_schunk_to_file": ([sp, C.c_char_p], i64),
+        "blosc2_schunk_append_file": ([sp, C.c_char_p], i64),
+        "blosc2_register_io_cb": ([vp], C.c_int),
+        "blosc2_get_io_cb": ([C.c_uint8], vp),
         "blosc2_meta_add": ([sp, C.c_char_p, vp, i32], C.c_int),
         "blosc2_vlmeta_add": ([sp, C.c_char_p, vp, i32, vp], C.c_int),
     }
@@ -355,7 +405,10 @@ class SChunk:
         cb = self.L.blosc2_schunk_get_chunk(self.p, n, C.byref(cp), C.byref(nf))
         if cb <= 0:
             return cb
-        return np.ctypeslib.as_array(C.cast(cp, C.POINTER(C.c_uint8)), (cb,)).copy()
+        out = np.ctypeslib.as_array(C.cast(cp, C.POINTER(C.c_uint8)), (cb,)).copy()
+        if nf.value:   # read off a frame file (frame_get_chunk): the caller's to free
+            _libc().free(cp)
+        return out
 
     def decompress_chunk(self, n, nbytes):
         out = np.zeros(max(nbytes, 1), np.uint8)

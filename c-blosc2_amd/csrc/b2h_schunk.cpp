@@ -25,6 +25,7 @@
 #include "../../include/b2h.h"
 #include "../../include/blosc2.h"
 #include "b2h_engine.h"
+#include "b2h_frame.h"
 
 namespace {
 
@@ -273,6 +274,7 @@ blosc2_schunk* blosc2_schunk_new(blosc2_storage* storage) {
 // schunk.c:679-727
 int blosc2_schunk_free(blosc2_schunk* schunk) {
   if (!schunk) return 0;
+  if (schunk->frame) b2h::link_free(schunk);   // an attached handle: its index and its frame link
   if (schunk->data && !schunk->view) {
     for (int64_t i = 0; i < schunk->nchunks; i++) free(schunk->data[i]);
     free(schunk->data);
@@ -297,9 +299,10 @@ int blosc2_schunk_free(blosc2_schunk* schunk) {
 
 // ---------------------------------------------------------------------- chunk index ops ----
 // A handle attached to a contiguous frame (blosc2_schunk_open / _from_buffer(copy = false),
-// b2h_frame.cpp) holds the frame's chunks in host memory; the reference's writes go back to the
-// frame (frame_append_chunk etc.), which this engine does not write.  Such handles are read-only:
-// every write entry point refuses them instead of changing only the in-memory copy.
+// b2h_frame.cpp) reads its chunks from the frame; the reference's writes go back to the frame
+// (frame_append_chunk etc.), which this engine does not write in place.  Such handles are
+// read-only: every write entry point refuses them (blosc2_schunk_to_buffer / _to_file write a
+// new frame instead).
 static int refuse_if_attached(const blosc2_schunk* s, const char* fn) {
   if (s->storage && (s->storage->contiguous || s->storage->urlpath)) {
     TRACE_ERROR("%s: super-chunks attached to a frame are read-only in the MI355X engine", fn);
@@ -393,8 +396,16 @@ int blosc2_schunk_decompress_chunk(blosc2_schunk* schunk, int64_t nchunk, void* 
   int rc = validate_nchunk(schunk, nchunk, false, "blosc2_schunk_decompress_chunk");
   if (rc < 0) return rc;
   schunk->current_nchunk = nchunk;
-  const uint8_t* src = schunk->data[nchunk];
+  uint8_t* src = schunk->data[nchunk];
+  bool needs_free = false;
+  if (!src && schunk->frame) {   // frame_decompress_chunk (frame.c:5248-5290): the chunk off the frame
+    if ((rc = b2h::link_get_chunk(schunk, nchunk, &src, &needs_free)) < 0) return rc;
+  }
   if (!src) return 0;
+  struct Freer {
+    uint8_t* p;
+    ~Freer() { free(p); }
+  } freer{needs_free ? src : nullptr};
   int32_t chunk_nbytes, chunk_cbytes;
   if ((rc = blosc2_cbuffer_sizes(src, &chunk_nbytes, &chunk_cbytes, nullptr)) < 0) return rc;
   if (nbytes < chunk_nbytes) {
@@ -411,12 +422,14 @@ int blosc2_schunk_decompress_chunk(blosc2_schunk* schunk, int64_t nchunk, void* 
   return got;
 }
 
-// schunk.c:1543-1632 (frame-less: the chunk is the super-chunk's own buffer, never to be freed)
+// schunk.c:1543-1632 (frame-less: the chunk is the super-chunk's own buffer, never to be freed;
+// frame-attached: frame_get_chunk, a chunk read off a frame file is the caller's to free)
 static int get_chunk(blosc2_schunk* schunk, int64_t nchunk, uint8_t** chunk, bool* needs_free, const char* fn) {
   if (!schunk || !chunk || !needs_free) return BLOSC2_ERROR_NULL_POINTER;
   int rc = validate_nchunk(schunk, nchunk, false, fn);
   if (rc < 0) return rc;
   schunk->current_nchunk = nchunk;
+  if (schunk->frame) return b2h::link_get_chunk(schunk, nchunk, chunk, needs_free);
   *chunk = schunk->data[nchunk];
   *needs_free = false;
   if (!*chunk) return 0;
@@ -560,8 +573,12 @@ int b2h_schunk_decompress_device(blosc2_schunk* schunk, int64_t nchunk, int32_t 
   if (n == 0) return 0;
   std::vector<int32_t> st((size_t)n);
   schunk->current_nchunk = nchunk + n - 1;
-  const int rc = b2h::ctx_decompress_device(schunk->dctx, schunk->data + nchunk, n, static_cast<uint8_t*>(d_dst),
-                                            dst_stride, dst_capacity, st.data());
+  std::vector<const uint8_t*> ptrs;
+  b2h::ReadBuf hold;
+  int rc = b2h::chunk_ptrs(schunk, nchunk, n, &ptrs, &hold);
+  if (rc < 0) return rc;
+  rc = b2h::ctx_decompress_device(schunk->dctx, ptrs.data(), n, static_cast<uint8_t*>(d_dst), dst_stride,
+                                  dst_capacity, st.data());
   if (status) memcpy(status, st.data(), sizeof(int32_t) * (size_t)n);
   return rc;
 }
@@ -599,8 +616,11 @@ int b2h_schunk_get_slice_device(blosc2_schunk* schunk, int64_t start, int64_t st
   if (f0 >= 0) {
     const int32_t m = (int32_t)(f1 - f0 + 1);
     std::vector<int32_t> st((size_t)m);
-    int rc = b2h::ctx_decompress_device(schunk->dctx, schunk->data + f0, m, dst + (f0 * cs - b0), cs, (int32_t)cs,
-                                        st.data());
+    std::vector<const uint8_t*> ptrs;
+    b2h::ReadBuf hold;
+    int rc = b2h::chunk_ptrs(schunk, f0, m, &ptrs, &hold);
+    if (rc < 0) return rc;
+    rc = b2h::ctx_decompress_device(schunk->dctx, ptrs.data(), m, dst + (f0 * cs - b0), cs, (int32_t)cs, st.data());
     if (rc < 0) return BLOSC2_ERROR_FAILURE;
     schunk->current_nchunk = f1;
   }
@@ -795,6 +815,8 @@ int b2h_schunk_decompress_buffers(blosc2_schunk* schunk, int64_t nchunk, int32_t
     const int32_t G = (int32_t)std::max<int64_t>(1, std::min<int64_t>(i1 - i0, kGroupBytes / std::max<int64_t>(dst_stride, 1)));
     const int32_t ng = (i1 - i0 + G - 1) / G;
     Stage S;
+    b2h::ReadBuf hold;   // a frame-attached handle's chunks, read group by group
+    std::vector<const uint8_t*> ptrs;
     auto lo = [&](int32_t g) { return i0 + g * G; };
     auto cnt = [&](int32_t g) { return std::min(G, i1 - lo(g)); };
     auto unstage = [&](int32_t g) {
@@ -805,8 +827,10 @@ int b2h_schunk_decompress_buffers(blosc2_schunk* schunk, int64_t nchunk, int32_t
     for (int32_t g = 0; g < ng && r == 0; g++) {
       // the device buffer's previous D2H (group g - 2) must be done before the engine rewrites it
       if (g >= 2 && hipEventSynchronize(S.ev[g % 2]) != hipSuccess) { r = BLOSC2_ERROR_FAILURE; break; }
-      const int rr = b2h::ctx_decompress_device(ctx, schunk->data + nchunk + lo(g), cnt(g), S.dev[g % 2], dst_stride,
-                                                dst_capacity, st.data() + lo(g));
+      int rr = b2h::chunk_ptrs(schunk, nchunk + lo(g), cnt(g), &ptrs, &hold);
+      if (rr >= 0)
+        rr = b2h::ctx_decompress_device(ctx, ptrs.data(), cnt(g), S.dev[g % 2], dst_stride, dst_capacity,
+                                        st.data() + lo(g));
       if (rr < 0) { r = rr; break; }
       if (behind.joinable()) behind.join();   // group g - 3's pinned buffer is free again
       if (hipMemcpyAsync(S.p(g), S.dev[g % 2], (size_t)cnt(g) * (size_t)dst_stride, hipMemcpyDeviceToHost, S.cs) != hipSuccess ||

@@ -20,6 +20,7 @@
 #include <stdbool.h>
 #include <stdint.h>
 #include <stddef.h>
+#include <stdio.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -431,10 +432,12 @@ BLOSC_EXPORT int blosc2_getitem_bytes_ctx(blosc2_context *context, const void *s
  * indexed by schunk->data, exactly as the reference's frame-less schunk.  New frame-backed storage
  * (contiguous frames, files, directories) is outside the device engine:
  * blosc2_schunk_new returns NULL for it.  Existing contiguous frames OPEN through the reference's
- * entry points (blosc2_schunk_open / _from_buffer below): their chunks are read into an in-memory
- * super-chunk with the frame's header fields, counters and (vl)metalayers; the offsets index is
- * decoded on the device (include/b2h.h b2h_frame_*).  The device-batch forms (b2h_schunk_append_device / b2h_schunk_decompress_device in
- * include/b2h.h) run one engine launch over many chunks of a super-chunk. ---- */
+ * entry points (blosc2_schunk_open* / _from_buffer below) as read-only, frame-attached handles:
+ * a frame file is read through its IO backend (blosc2_io_cb) lazily, a chunk or a run of adjacent
+ * chunks at a time, as frame_get_chunk reads it; an in-memory frame is used in place.  Any
+ * super-chunk is written out as a contiguous frame with blosc2_schunk_to_buffer / _to_file /
+ * _append_file.  The device-batch forms (b2h_schunk_append_device / b2h_schunk_decompress_device
+ * in include/b2h.h) run one engine launch over many chunks of a super-chunk. ---- */
 enum {   /* include/blosc2.h:994-1005 */
   BLOSC2_IO_FILESYSTEM = 0,
   BLOSC2_IO_FILESYSTEM_MMAP = 1,
@@ -453,6 +456,77 @@ typedef struct {
   void *params;
 } blosc2_io;
 static const blosc2_io BLOSC2_IO_DEFAULTS = {BLOSC2_IO_FILESYSTEM, "filesystem", NULL};
+
+/* IO backends: include/blosc2.h:1007-1078 (registry blosc/blosc2.c:6784-6847).  The registry holds
+ * the filesystem backend (id 0, blosc2_stdio_*) and the memory-mapped one (id 1,
+ * blosc2_stdio_mmap_*); users register ids >= BLOSC2_IO_REGISTERED. */
+typedef void*   (*blosc2_open_cb)(const char *urlpath, const char *mode, void *params);
+typedef int     (*blosc2_close_cb)(void *stream);
+typedef int64_t (*blosc2_size_cb)(void *stream);
+typedef int64_t (*blosc2_write_cb)(const void *ptr, int64_t size, int64_t nitems, int64_t position, void *stream);
+typedef int64_t (*blosc2_read_cb)(void **ptr, int64_t size, int64_t nitems, int64_t position, void *stream);
+typedef int     (*blosc2_truncate_cb)(void *stream, int64_t size);
+typedef int     (*blosc2_destroy_cb)(void *params);
+typedef struct {
+  uint8_t id;
+  char *name;
+  bool is_allocation_necessary;   /* true: read() fills the caller's buffer; false: it returns a pointer */
+  blosc2_open_cb open;
+  blosc2_close_cb close;
+  blosc2_size_cb size;
+  blosc2_write_cb write;
+  blosc2_read_cb read;
+  blosc2_truncate_cb truncate;
+  blosc2_destroy_cb destroy;
+} blosc2_io_cb;
+BLOSC_EXPORT int blosc2_register_io_cb(const blosc2_io_cb *io);
+BLOSC_EXPORT blosc2_io_cb *blosc2_get_io_cb(uint8_t id);
+
+/* The filesystem backend: include/blosc2/blosc2-stdio.h:25-69 (blosc/blosc2-stdio.c:120-300).
+ * Positioned reads and writes (pread / pwrite), so one open handle serves concurrent readers. */
+typedef struct {
+  FILE *file;
+} blosc2_stdio_file;
+typedef struct {
+  bool locking;   /* accepted; the sidecar lock file is not implemented */
+} blosc2_stdio_params;
+static const blosc2_stdio_params BLOSC2_STDIO_PARAMS_DEFAULTS = {false};
+BLOSC_EXPORT void *blosc2_stdio_open(const char *urlpath, const char *mode, void *params);
+BLOSC_EXPORT int blosc2_stdio_close(void *stream);
+BLOSC_EXPORT int64_t blosc2_stdio_size(void *stream);
+BLOSC_EXPORT int64_t blosc2_stdio_write(const void *ptr, int64_t size, int64_t nitems, int64_t position, void *stream);
+BLOSC_EXPORT int64_t blosc2_stdio_read(void **ptr, int64_t size, int64_t nitems, int64_t position, void *stream);
+BLOSC_EXPORT int blosc2_stdio_truncate(void *stream, int64_t size);
+BLOSC_EXPORT int blosc2_stdio_destroy(void *params);
+
+/* The memory-mapped backend: include/blosc2/blosc2-stdio.h:76-135.  Read modes ("r", "c") map the
+ * file; read() hands out pointers into the mapping (no copy).  The writable modes ("r+", "w+")
+ * back frame-backed storage that the engine does not create; open refuses them. */
+typedef struct {
+  const char *mode;
+  size_t initial_mapping_size;
+  bool needs_free;
+  char *addr;
+  char *urlpath;
+  size_t file_size;
+  size_t mapping_size;
+  bool is_memory_only;
+  FILE *file;
+  int fd;
+  int64_t access_flags;
+  int64_t map_flags;
+} blosc2_stdio_mmap;
+static const blosc2_stdio_mmap BLOSC2_STDIO_MMAP_DEFAULTS = {
+  "r", ((size_t)1 << 30), false, NULL, NULL, 0, 0, false, NULL, -1, -1, -1};
+BLOSC_EXPORT blosc2_stdio_mmap blosc2_get_blosc2_stdio_mmap_defaults(void);
+BLOSC_EXPORT void *blosc2_stdio_mmap_open(const char *urlpath, const char *mode, void *params);
+BLOSC_EXPORT int blosc2_stdio_mmap_close(void *stream);
+BLOSC_EXPORT int64_t blosc2_stdio_mmap_size(void *stream);
+BLOSC_EXPORT int64_t blosc2_stdio_mmap_write(const void *ptr, int64_t size, int64_t nitems, int64_t position,
+                                             void *stream);
+BLOSC_EXPORT int64_t blosc2_stdio_mmap_read(void **ptr, int64_t size, int64_t nitems, int64_t position, void *stream);
+BLOSC_EXPORT int blosc2_stdio_mmap_truncate(void *stream, int64_t size);
+BLOSC_EXPORT int blosc2_stdio_mmap_destroy(void *params);
 
 #define BLOSC2_MAX_METALAYERS 16                  /* include/blosc2.h:1744 */
 #define BLOSC2_METALAYER_NAME_MAXLEN 31
@@ -526,15 +600,30 @@ BLOSC_EXPORT blosc2_schunk *blosc2_schunk_new(blosc2_storage *storage);
 BLOSC_EXPORT int blosc2_schunk_free(blosc2_schunk *schunk);
 /* include/blosc2.h:1934 (blosc/schunk.c:731-750, frame_to_schunk frame.c:2941-3245): a contiguous
  * frame in memory; `copy` false gives the frame-attached flavour (storage.contiguous, the header's
- * cbytes and blocksize), true the copy (sum of the chunks' cbytes, their common blocksize).  The
- * chunks are host copies either way: writes to the handle do not reach the frame. */
+ * cbytes and blocksize; the chunks are read in place from `cframe`, which must outlive the handle),
+ * true the copy (sum of the chunks' cbytes, their common blocksize, chunks in malloc'd buffers).
+ * Frame-attached handles are read-only (their mutators return BLOSC2_ERROR_INVALID_PARAM). */
 BLOSC_EXPORT blosc2_schunk *blosc2_schunk_from_buffer(uint8_t *cframe, int64_t len, bool copy);
-/* include/blosc2.h:2008, 2019, 2030, 2043 (blosc/schunk.c:366-470): a contiguous frame file (at
- * `offset`), filesystem backend only (another udio->id returns NULL). */
+/* include/blosc2.h:2008, 2019, 2030, 2043 (blosc/schunk.c:366-470, frame_from_file_offset
+ * frame.c:1720-1870): a contiguous frame file (at `offset`) through the IO backend `udio->id`
+ * (registry above; NULL udio = the filesystem backend).  Open reads the header, the trailer and
+ * the offsets index only; chunks are read when used, through the backend's read callback, which
+ * stays open for the handle's life. */
 BLOSC_EXPORT blosc2_schunk *blosc2_schunk_open(const char *urlpath);
 BLOSC_EXPORT blosc2_schunk *blosc2_schunk_open_offset(const char *urlpath, int64_t offset);
 BLOSC_EXPORT blosc2_schunk *blosc2_schunk_open_udio(const char *urlpath, const blosc2_io *udio);
 BLOSC_EXPORT blosc2_schunk *blosc2_schunk_open_offset_udio(const char *urlpath, int64_t offset, const blosc2_io *udio);
+/* include/blosc2.h:1946, 1957, 1968 (blosc/schunk.c:481-650; frame_from_schunk frame.c:1926-2100,
+ * new_header_frame 591-889, frame_update_trailer 1422-1640): the super-chunk as one contiguous
+ * frame -- header (fields, metalayers), the chunks in order, the offsets index (a Blosc chunk of
+ * int64 offsets, compressed as frame_append_chunk compresses it: BloscLZ, typesize 8, 16 KiB
+ * blocks, no split) and the trailer (vlmetalayers).  to_buffer hands out a malloc'd frame
+ * (*needs_free true), or the attached frame itself for a handle on an in-memory frame; to_file
+ * writes through the filesystem backend and returns the frame length; append_file writes the frame
+ * at the end of the file and returns the offset it starts at (for blosc2_schunk_open_offset). */
+BLOSC_EXPORT int64_t blosc2_schunk_to_buffer(blosc2_schunk *schunk, uint8_t **cframe, bool *needs_free);
+BLOSC_EXPORT int64_t blosc2_schunk_to_file(blosc2_schunk *schunk, const char *urlpath);
+BLOSC_EXPORT int64_t blosc2_schunk_append_file(blosc2_schunk *schunk, const char *urlpath);
 /* include/blosc2.h:2101, 2115, 2129, 2140 (blosc/schunk.c:975-1457) */
 BLOSC_EXPORT int64_t blosc2_schunk_append_chunk(blosc2_schunk *schunk, uint8_t *chunk, bool copy);
 BLOSC_EXPORT int64_t blosc2_schunk_update_chunk(blosc2_schunk *schunk, int64_t nchunk, uint8_t *chunk, bool copy);
