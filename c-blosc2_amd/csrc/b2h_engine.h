@@ -147,6 +147,9 @@ int ctx_append_device(::blosc2_context_s* ctx, const uint8_t* d_src, const int32
                       int64_t src_stride, uint8_t** chunks_out);
 int ctx_decompress_device(::blosc2_context_s* ctx, const uint8_t* const* chunks, int32_t n, uint8_t* d_dst,
                           int64_t dst_stride, int32_t dst_cap, int32_t* status);
+// The staged fan-out decode (b2h_schunk_decompress_buffers) takes a chunk itself when this holds:
+// no postfilter on ctx, no user filter / codec in the chunk, a readable header (sizes returned).
+bool ctx_chunk_on_device(const ::blosc2_context_s* ctx, const uint8_t* chunk, int32_t* nbytes, int32_t* cbytes);
 // The multi-device fan-out (b2h_schunk_append_buffers): a context with ctx's parameters, sticky
 // blocksize and encoder mode, but device state of its own (created on the calling thread's device);
 // and the sticky-blocksize walk of n consecutive compressions, before[i] = the state chunk i starts

@@ -49,6 +49,15 @@ int64_t be(const uint8_t* p, int n) {   // big-endian msgpack integers (frame.c 
 }
 int32_t le32(const uint8_t* p) { int32_t v; memcpy(&v, p, 4); return v; }
 
+// out[i * 32 + j] = the j-th header byte of chunk i (zeros for a special offset).
+__global__ void k_gather_hdrs(const uint8_t* __restrict__ frame, int32_t header_len, const int64_t* __restrict__ offsets,
+                              int64_t n, uint8_t* __restrict__ out) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n * 32; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t o = offsets[t >> 5];
+    out[t] = o >= 0 ? frame[header_len + o + (t & 31)] : 0;
+  }
+}
+
 __global__ void k_fill_pattern(uint8_t* dst, int64_t nbytes, uint64_t pattern, int width) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nbytes; i += (int64_t)gridDim.x * blockDim.x)
     dst[i] = (uint8_t)(pattern >> (8 * (i % width)));
@@ -57,7 +66,8 @@ __global__ void k_fill_pattern(uint8_t* dst, int64_t nbytes, uint64_t pattern, i
 }  // namespace
 
 struct b2h_frame {
-  uint8_t* host = nullptr;      // pinned copy of the whole frame
+  uint8_t* host = nullptr;      // pinned host copy of the whole frame (from_buffer), or none (open)
+  std::vector<uint8_t> chdr;    // per chunk: its 32-byte header (zeros for a special chunk)
   int64_t len = 0;
   uint8_t* dev = nullptr;       // HBM copy (uploaded on first use)
   int32_t header_len = 0;
@@ -109,7 +119,7 @@ int decode_chunks(b2h_frame* f, const std::vector<int64_t>& idx, const std::vect
   for (int32_t k = 0; k < n; k++) {
     const int64_t pos = f->header_len + f->offsets[idx[k]];
     srcs[k] = f->dev + pos;
-    sizes[k] = le32(f->host + pos + 12);   // the chunk's own cbytes field
+    sizes[k] = le32(f->chdr.data() + idx[k] * kChunkHdr + 12);   // the chunk's own cbytes field
     if (sizes[k] < 16 || pos + sizes[k] > f->header_len + f->cbytes) return BLOSC2_ERROR_INVALID_HEADER;
     bound += caps[k];
   }
@@ -188,8 +198,19 @@ int parse_head(const uint8_t* h, FrameHead* H) {
 // The in-memory frame's header, then the offsets index (get_coffsets, 2102-2155) decoded on the
 // device.
 int parse(b2h_frame* f) {
-  const uint8_t* h = f->host;
   if (f->len < kHeaderMin) return BLOSC2_ERROR_READ_BUFFER;
+  int rc = upload(f);
+  if (rc) return rc;
+  // `len` bytes at `pos`: the host copy's, or fetched from the device copy
+  auto bytes_at = [&](int64_t pos, int32_t len, uint8_t* out) {
+    if (f->host) {
+      memcpy(out, f->host + pos, (size_t)len);
+      return 0;
+    }
+    return hipMemcpy(out, f->dev + pos, (size_t)len, hipMemcpyDeviceToHost) == hipSuccess ? 0 : BLOSC2_ERROR_FAILURE;
+  };
+  uint8_t h[kHeaderMin];
+  if ((rc = bytes_at(0, kHeaderMin, h))) return rc;
   FrameHead H;
   int rc0 = parse_head(h, &H);
   if (rc0) return rc0;
@@ -210,10 +231,10 @@ int parse(b2h_frame* f) {
   // offsets index: a Blosc chunk right after the data chunks
   const int64_t off_pos = (int64_t)f->header_len + f->cbytes;
   if (off_pos + kChunkHdr > f->len) return BLOSC2_ERROR_INVALID_HEADER;
-  const int32_t off_nbytes = le32(h + off_pos + 4), off_cbytes = le32(h + off_pos + 12);
+  f->chdr.assign(kChunkHdr, 0);   // the index chunk's header, as "chunk 0" for one decode call
+  if ((rc = bytes_at(off_pos, kChunkHdr, f->chdr.data()))) return rc;
+  const int32_t off_nbytes = le32(f->chdr.data() + 4), off_cbytes = le32(f->chdr.data() + 12);
   if (off_nbytes != f->nchunks * 8 || off_cbytes < 16 || off_pos + off_cbytes > f->len) return BLOSC2_ERROR_INVALID_HEADER;
-  int rc = upload(f);
-  if (rc) return rc;
   uint8_t* d_off = nullptr;
   if (hipMalloc(&d_off, (size_t)off_nbytes) != hipSuccess) return BLOSC2_ERROR_MEMORY_ALLOC;
   // decode the index chunk as a one-chunk batch (its offset relative to the header start is cbytes)
@@ -232,14 +253,32 @@ int parse(b2h_frame* f) {
     f->offsets.resize((size_t)f->nchunks);
     if (hipMemcpy(f->offsets.data(), d_off, (size_t)off_nbytes, hipMemcpyDeviceToHost) != hipSuccess) rc = BLOSC2_ERROR_FAILURE;
   }
-  (void)hipFree(d_off);
-  if (rc) return rc;
-  for (int64_t i = 0; i < f->nchunks; i++) {   // get_coffset bounds (frame.c:3297-3313)
+  for (int64_t i = 0; i < f->nchunks && !rc; i++) {   // get_coffset bounds (frame.c:3297-3313)
     const int64_t o = f->offsets[i];
     if (o >= 0 && (f->header_len + o > f->header_len + f->cbytes - kChunkHdr || f->header_len + o > f->len - kChunkHdr))
-      return BLOSC2_ERROR_INVALID_HEADER;
+      rc = BLOSC2_ERROR_INVALID_HEADER;
   }
-  return 0;
+  // every chunk's header: from the host copy, or gathered on the device in one kernel
+  f->chdr.assign((size_t)f->nchunks * kChunkHdr, 0);
+  if (!rc && f->host) {
+    for (int64_t i = 0; i < f->nchunks; i++)
+      if (f->offsets[i] >= 0) memcpy(f->chdr.data() + i * kChunkHdr, f->host + f->header_len + f->offsets[i], kChunkHdr);
+  } else if (!rc && f->nchunks > 0) {
+    uint8_t* d_hdr = nullptr;
+    if (hipMalloc(&d_hdr, f->chdr.size()) != hipSuccess) rc = BLOSC2_ERROR_MEMORY_ALLOC;
+    if (!rc) {
+      const uint32_t grid = (uint32_t)std::min<int64_t>((f->nchunks * kChunkHdr + 255) / 256, 4096);
+      k_gather_hdrs<<<grid, 256, 0, f->stream>>>(f->dev, f->header_len, reinterpret_cast<const int64_t*>(d_off),
+                                                 f->nchunks, d_hdr);
+      if (hipGetLastError() != hipSuccess ||
+          hipMemcpyAsync(f->chdr.data(), d_hdr, f->chdr.size(), hipMemcpyDeviceToHost, f->stream) != hipSuccess ||
+          hipStreamSynchronize(f->stream) != hipSuccess)
+        rc = BLOSC2_ERROR_FAILURE;
+      (void)hipFree(d_hdr);
+    }
+  }
+  (void)hipFree(d_off);
+  return rc;
 }
 
 b2h_frame* open_pinned(uint8_t* host, int64_t len, int* err) {
@@ -252,6 +291,54 @@ b2h_frame* open_pinned(uint8_t* host, int64_t len, int* err) {
   if (rc) { frame_release(f); f = nullptr; }
   if (err) *err = rc;
   return f;
+}
+
+// A ring of pinned slots the file loader reads through (kept for the process: pinning memory
+// costs far more than reading it).
+constexpr int kLoadSlots = 8;
+constexpr int64_t kLoadPiece = int64_t(32) << 20;
+std::mutex g_load_mu;
+uint8_t* g_load_ring = nullptr;
+
+// Reads [0, len) of an open filesystem-backend stream into HBM (f->dev): kLoadSlots threads each
+// read a piece into their pinned slot and queue its H2D, then wait for the slot's DMA before
+// reading their next piece.  No host copy: parse() fetches the header bytes it needs from HBM.
+int load_file(b2h_frame* f, const blosc2_io_cb* io, void* fp) {
+  std::lock_guard<std::mutex> g(g_load_mu);   // one loader at a time owns the ring
+  if (!g_load_ring && hipHostMalloc(reinterpret_cast<void**>(&g_load_ring), (size_t)(kLoadSlots * kLoadPiece),
+                                    hipHostMallocDefault) != hipSuccess) {
+    g_load_ring = nullptr;
+    return BLOSC2_ERROR_MEMORY_ALLOC;
+  }
+  if (hipMalloc(&f->dev, (size_t)f->len) != hipSuccess) return BLOSC2_ERROR_MEMORY_ALLOC;
+  const int64_t npieces = (f->len + kLoadPiece - 1) / kLoadPiece;
+  const int T = (int)std::min<int64_t>(kLoadSlots, npieces);
+  std::vector<int> trc((size_t)T, 0);
+  auto worker = [&](int t) {
+    uint8_t* slot = g_load_ring + t * kLoadPiece;
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) { trc[(size_t)t] = BLOSC2_ERROR_FAILURE; return; }
+    for (int64_t i = t; i < npieces && !trc[(size_t)t]; i += T) {
+      const int64_t off = i * kLoadPiece, n = std::min(kLoadPiece, f->len - off);
+      if (hipEventSynchronize(ev) != hipSuccess) { trc[(size_t)t] = BLOSC2_ERROR_FAILURE; break; }
+      void* q = slot;
+      if (io->read(&q, 1, n, off, fp) != n) { trc[(size_t)t] = BLOSC2_ERROR_FILE_READ; break; }
+      if (hipMemcpyAsync(f->dev + off, slot, (size_t)n, hipMemcpyHostToDevice, f->stream) != hipSuccess ||
+          hipEventRecord(ev, f->stream) != hipSuccess) {
+        trc[(size_t)t] = BLOSC2_ERROR_FAILURE;
+        break;
+      }
+    }
+    (void)hipEventSynchronize(ev);
+    (void)hipEventDestroy(ev);
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; t++) th.emplace_back(worker, t);
+  worker(0);
+  for (auto& x : th) x.join();
+  for (int r : trc)
+    if (r) return r;
+  return hipStreamSynchronize(f->stream) == hipSuccess ? 0 : BLOSC2_ERROR_FAILURE;
 }
 
 // Special offset (frame.c:3320-3365): byte 7 bit 7 set, kind in bits 0-2 of byte 7.
@@ -273,7 +360,7 @@ int fill_special(b2h_frame* f, int64_t special, uint8_t* d_dst, int32_t nbytes) 
 struct ChunkGeom { int32_t blocksize = 0, nblocks = 0; bool delta = false; };
 ChunkGeom chunk_geom(const b2h_frame* f, int64_t i) {
   ChunkGeom g;
-  const uint8_t* h = f->host + f->header_len + f->offsets[i];
+  const uint8_t* h = f->chdr.data() + i * kChunkHdr;
   const int32_t nb = le32(h + 4), bs = le32(h + 8);
   if (bs <= 0 || nb <= 0) return g;
   g.blocksize = std::min(bs, nb);
@@ -325,20 +412,23 @@ b2h_frame* b2h_frame_open(const char* urlpath, int* err) {
   void* fp = urlpath && io ? io->open(urlpath, "rb", nullptr) : nullptr;
   if (!fp) { if (err) *err = BLOSC2_ERROR_FILE_OPEN; return nullptr; }
   const int64_t len = io->size(fp);
-  uint8_t* host = nullptr;
+  b2h_frame* f = new b2h_frame();
+  f->len = len;
   int rc = len > 0 ? 0 : BLOSC2_ERROR_FILE_READ;
-  if (!rc && hipHostMalloc(reinterpret_cast<void**>(&host), (size_t)len, hipHostMallocDefault) != hipSuccess) {
-    host = nullptr;
-    rc = BLOSC2_ERROR_MEMORY_ALLOC;
-  }
-  if (!rc) rc = b2h::io_read_par(io, fp, 0, len, host, nullptr);
+  if (!rc) rc = hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking) == hipSuccess ? 0 : BLOSC2_ERROR_FAILURE;
+  if (!rc) rc = load_file(f, io, fp);
   io->close(fp);
+  if (!rc) {
+    f->ws = b2h::workspace_create();
+    rc = parse(f);   // the device copy is already there (upload() keeps it)
+  }
   if (rc) {
-    if (host) (void)hipHostFree(host);
+    frame_release(f);
     if (err) *err = rc;
     return nullptr;
   }
-  return open_pinned(host, len, err);
+  if (err) *err = 0;
+  return f;
 }
 
 void b2h_frame_free(b2h_frame* f) { frame_release(f); }

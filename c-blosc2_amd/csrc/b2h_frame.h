@@ -9,6 +9,8 @@
 // missing ones through the frame's IO backend.
 #pragma once
 
+#include <hip/hip_runtime.h>
+
 #include <cstdint>
 #include <cstdlib>
 #include <mutex>
@@ -18,19 +20,37 @@
 
 namespace b2h {
 
-// A growable malloc'd byte buffer that is never zero-filled (a frame read fills it).
+// A growable byte buffer that is never zero-filled (a frame read fills it): malloc'd, or pinned
+// (hipHostMalloc) when the bytes go on to the device -- the staged decode H2Ds a run of chunks
+// read off a frame file straight from it.
 struct ReadBuf {
   uint8_t* p = nullptr;
   size_t cap = 0;
+  bool pinned = false;
   ReadBuf() = default;
+  explicit ReadBuf(bool pin) : pinned(pin) {}
   ReadBuf(const ReadBuf&) = delete;
   ReadBuf& operator=(const ReadBuf&) = delete;
-  ~ReadBuf() { free(p); }
+  ~ReadBuf() { release(); }
+  void release() {
+    if (p && pinned) (void)hipHostFree(p);
+    else free(p);
+    p = nullptr;
+    cap = 0;
+  }
   bool ensure(size_t n) {
     if (n <= cap) return true;
-    uint8_t* q = static_cast<uint8_t*>(realloc(p, n));
-    if (!q) return false;
-    p = q;
+    if (pinned) {
+      release();
+      if (hipHostMalloc(reinterpret_cast<void**>(&p), n, hipHostMallocDefault) != hipSuccess) {
+        p = nullptr;
+        return false;
+      }
+    } else {
+      uint8_t* q = static_cast<uint8_t*>(realloc(p, n));
+      if (!q) return false;
+      p = q;
+    }
     cap = n;
     return true;
   }

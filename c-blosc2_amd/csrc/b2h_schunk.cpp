@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -562,6 +563,11 @@ int64_t b2h_schunk_append_device(blosc2_schunk* schunk, const void* d_src, const
 
 // Chunks [nchunk, nchunk + n) into d_dst + i * dst_stride in one device batch; status[i] (optional)
 // = what blosc2_schunk_decompress_chunk(schunk, nchunk + i, ., dst_capacity) returns.
+namespace {
+int staged_decode(blosc2_schunk* schunk, blosc2_context* ctx, int device, int64_t c0, int32_t n, uint8_t* out_host,
+                  uint8_t* out_dev, int64_t dst_stride, int32_t dst_capacity, int32_t* st);
+}  // namespace
+
 int b2h_schunk_decompress_device(blosc2_schunk* schunk, int64_t nchunk, int32_t n, void* d_dst, int64_t dst_stride,
                                  int32_t dst_capacity, int32_t* status) {
   if (!schunk) return BLOSC2_ERROR_NULL_POINTER;
@@ -573,12 +579,10 @@ int b2h_schunk_decompress_device(blosc2_schunk* schunk, int64_t nchunk, int32_t 
   if (n == 0) return 0;
   std::vector<int32_t> st((size_t)n);
   schunk->current_nchunk = nchunk + n - 1;
-  std::vector<const uint8_t*> ptrs;
-  b2h::ReadBuf hold;
-  int rc = b2h::chunk_ptrs(schunk, nchunk, n, &ptrs, &hold);
-  if (rc < 0) return rc;
-  rc = b2h::ctx_decompress_device(schunk->dctx, ptrs.data(), n, static_cast<uint8_t*>(d_dst), dst_stride,
-                                  dst_capacity, st.data());
+  int device = 0;
+  if (hipGetDevice(&device) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+  const int rc = staged_decode(schunk, schunk->dctx, device, nchunk, n, nullptr, static_cast<uint8_t*>(d_dst),
+                               dst_stride, dst_capacity, st.data());
   if (status) memcpy(status, st.data(), sizeof(int32_t) * (size_t)n);
   return rc;
 }
@@ -784,6 +788,281 @@ int64_t b2h_schunk_append_buffers(blosc2_schunk* schunk, const void* src, const 
   return r;
 }
 
+namespace {
+
+// A decode worker's staging, kept per device between calls (pinned allocations of a few hundred
+// MiB cost tens of ms each): two input slots (packed compressed chunks in pinned and device memory,
+// with the batch's pointer / size tables), two device output slots, three pinned output slots with
+// their status words, a stream per direction plus the compute stream, the events that order them,
+// and the engine workspace.
+struct DecodeStage {
+  int device = -1;
+  size_t in_cap = 0, out_cap = 0, tab_cap = 0;
+  uint8_t *pin_in[2] = {}, *dev_in[2] = {}, *pin_tab[2] = {}, *dev_tab[2] = {}, *dev_out[2] = {};
+  uint8_t* pin_out[3] = {};
+  int32_t* pin_st[3] = {};
+  hipStream_t s_in = nullptr, s_out = nullptr, s_k = nullptr;
+  hipEvent_t e_in[2] = {}, e_dec[2] = {}, e_dout[2] = {}, e_out[3] = {};
+  b2h::Workspace* ws = nullptr;
+  b2h::ReadBuf hold[2] = {b2h::ReadBuf(true), b2h::ReadBuf(true)};   // chunks read off a frame file
+  bool init() {
+    auto ev = [](hipEvent_t* e) { return hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess; };
+    if (hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&s_k, hipStreamNonBlocking) != hipSuccess)
+      return false;
+    for (int i = 0; i < 2; i++)
+      if (!ev(&e_in[i]) || !ev(&e_dec[i]) || !ev(&e_dout[i])) return false;
+    for (int i = 0; i < 3; i++)
+      if (!ev(&e_out[i])) return false;
+    ws = b2h::workspace_create();
+    return ws != nullptr;
+  }
+  static bool grow_pin(uint8_t** p, size_t n) {
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    return hipHostMalloc(reinterpret_cast<void**>(p), n, hipHostMallocDefault) == hipSuccess;
+  }
+  static bool grow_dev(uint8_t** p, size_t n) {
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    return hipMalloc(reinterpret_cast<void**>(p), n) == hipSuccess;
+  }
+  bool ensure(size_t in, size_t out, size_t tab) {   // (an idle stage has nothing in flight)
+    if (in > in_cap) {
+      for (int i = 0; i < 2; i++)
+        if (!grow_pin(&pin_in[i], in) || !grow_dev(&dev_in[i], in)) return false;
+      in_cap = in;
+    }
+    if (out > out_cap) {
+      for (int i = 0; i < 2; i++)
+        if (!grow_dev(&dev_out[i], out)) return false;
+      for (int i = 0; i < 3; i++)
+        if (!grow_pin(&pin_out[i], out)) return false;
+      out_cap = out;
+    }
+    if (tab > tab_cap) {
+      for (int i = 0; i < 2; i++)
+        if (!grow_pin(&pin_tab[i], tab) || !grow_dev(&dev_tab[i], tab)) return false;
+      for (int i = 0; i < 3; i++)
+        if (!grow_pin(reinterpret_cast<uint8_t**>(&pin_st[i]), tab)) return false;
+      tab_cap = tab;
+    }
+    return true;
+  }
+};
+
+std::mutex g_stage_mu;
+std::vector<DecodeStage*> g_stages;   // idle stages, any device
+
+DecodeStage* stage_acquire(int device) {
+  {
+    std::lock_guard<std::mutex> g(g_stage_mu);
+    for (size_t i = 0; i < g_stages.size(); i++) {
+      if (g_stages[i]->device != device) continue;
+      DecodeStage* st = g_stages[i];
+      g_stages.erase(g_stages.begin() + (long)i);
+      return st;
+    }
+  }
+  DecodeStage* st = new DecodeStage();
+  st->device = device;
+  if (!st->init()) {
+    delete st;   // (its streams / events leak: a failed init means a broken device anyway)
+    return nullptr;
+  }
+  return st;
+}
+
+void stage_release(DecodeStage* st) {
+  std::lock_guard<std::mutex> g(g_stage_mu);
+  g_stages.push_back(st);
+}
+
+// Host copies of many separate chunks into one packed buffer, split over a few threads.
+void par_pack(uint8_t* dst, const std::vector<int64_t>& at, const std::vector<const uint8_t*>& src,
+              const std::vector<int32_t>& len, int64_t total) {
+  const int n = (int)src.size();
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>({8, total >> 23, n}));
+  auto part = [&](int t) {
+    for (int i = n * t / T; i < n * (t + 1) / T; i++) memcpy(dst + at[(size_t)i], src[(size_t)i], (size_t)len[(size_t)i]);
+  };
+  if (T == 1) return part(0);
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; t++) th.emplace_back(part, t);
+  part(0);
+  for (auto& x : th) x.join();
+}
+
+// The staged decode of chunks [c0, c0 + n) of `schunk` on the current device, through `ctx` (a
+// decompression context with the super-chunk's dparams), in groups of chunks through a pipeline
+// whose stages each hold their own resource: (1) the host gathers group g + 1's chunks (reading
+// them off the frame file for an attached handle) into a pinned slot and queues their H2D on the
+// input stream; (2) the engine decodes group g on the compute stream -- into a device slot, or
+// straight into `out_dev`; (3) the output stream brings the group's statuses (and, for host
+// output, its bytes) back into a pinned slot; (4) a helper thread copies group g - 1 from pinned
+// memory into `out_host`.  A group holding a chunk the device path does not take (user filters /
+// codecs, a postfilter, a bad header, too small a destination) goes through ctx_decompress_device
+// instead.  st[i] = what blosc2_schunk_decompress_chunk returns for chunk c0 + i.  Returns 0, the
+// first chunk's error, or the pipeline's.
+int staged_decode(blosc2_schunk* schunk, blosc2_context* ctx, int device, int64_t c0, int32_t n, uint8_t* out_host,
+                  uint8_t* out_dev, int64_t dst_stride, int32_t dst_capacity, int32_t* st) {
+  for (int32_t i = 0; i < n; i++) st[i] = BLOSC2_ERROR_FAILURE;
+  const int32_t G = (int32_t)std::max<int64_t>(1, std::min<int64_t>(n, kGroupBytes / std::max<int64_t>(dst_stride, 1)));
+  const int32_t ng = (n + G - 1) / G;
+  auto lo = [&](int32_t g) { return g * G; };
+  auto cnt = [&](int32_t g) { return std::min(G, n - lo(g)); };
+  const size_t tab = (size_t)G * (8 + 8 + 4 + 4 + 4);
+  const size_t in_cap = (size_t)G * ((size_t)dst_capacity + BLOSC2_MAX_OVERHEAD + 64);
+  DecodeStage* S = stage_acquire(device);
+  if (!S) return BLOSC2_ERROR_FAILURE;
+  int r = S->ensure(in_cap, out_dev ? 0 : (size_t)G * (size_t)dst_stride, tab) ? 0 : BLOSC2_ERROR_MEMORY_ALLOC;
+  std::vector<char> staged((size_t)ng, 0);   // per group: the device path took it
+  std::vector<int32_t> nbs((size_t)n, 0);
+  b2h::ReadBuf* hold = S->hold;
+  std::vector<const uint8_t*> ptrs_of[2];      // a fallback group's chunks (held until it ran)
+  auto dst_of = [&](int32_t g, int slot) {
+    return out_dev ? out_dev + (int64_t)lo(g) * dst_stride : S->dev_out[slot];
+  };
+  auto prep = [&](int32_t g) -> int {   // (1)
+    const int slot = g % 2;
+    const int32_t m = cnt(g);
+    if (hipEventSynchronize(S->e_dec[slot]) != hipSuccess) return BLOSC2_ERROR_FAILURE;   // group g - 2 left the slot
+    std::vector<const uint8_t*>& ptrs = ptrs_of[slot];
+    int rr = b2h::chunk_ptrs(schunk, c0 + lo(g), m, &ptrs, &hold[slot]);
+    if (rr < 0) return rr;
+    std::vector<int64_t> at((size_t)m);
+    std::vector<int32_t> cbs((size_t)m);
+    int64_t total = 0;
+    bool ok = true;
+    for (int32_t i = 0; i < m && ok; i++) {
+      int32_t nb = 0, cb = 0;
+      ok = ptrs[(size_t)i] && b2h::ctx_chunk_on_device(ctx, ptrs[(size_t)i], &nb, &cb) && nb <= dst_capacity && nb >= 0;
+      nbs[(size_t)(lo(g) + i)] = nb;
+      cbs[(size_t)i] = cb;
+      at[(size_t)i] = total;
+      total += ((int64_t)cb + 63) & ~int64_t(63);
+    }
+    staged[(size_t)g] = ok && (size_t)total <= S->in_cap;
+    if (!staged[(size_t)g]) return 0;
+    // chunks read off a frame file sit in the pinned read buffer already: its used span goes up
+    // as it is, the chunks keep their places in it; anything else is packed into the pinned slot
+    const uint8_t* hb = hold[slot].p;
+    bool in_hold = hb != nullptr;
+    int64_t span = 0;
+    for (int32_t i = 0; i < m && in_hold; i++) {
+      const uint8_t* c = ptrs[(size_t)i];
+      in_hold = c >= hb && c + cbs[(size_t)i] <= hb + hold[slot].cap;
+      if (in_hold) span = std::max<int64_t>(span, (c - hb) + cbs[(size_t)i]);
+    }
+    in_hold = in_hold && (size_t)span <= S->in_cap;
+    const uint8_t* h2d_src = S->pin_in[slot];
+    if (in_hold) {
+      for (int32_t i = 0; i < m; i++) at[(size_t)i] = ptrs[(size_t)i] - hb;
+      h2d_src = hb;
+      total = span;
+    } else {
+      par_pack(S->pin_in[slot], at, ptrs, cbs, total);
+    }
+    uint8_t* t = S->pin_tab[slot];
+    const uint8_t** h_s = reinterpret_cast<const uint8_t**>(t);
+    uint8_t** h_d = reinterpret_cast<uint8_t**>(t + 8 * (size_t)m);
+    int32_t* h_ss = reinterpret_cast<int32_t*>(t + 16 * (size_t)m);
+    int32_t* h_ds = h_ss + m;
+    uint8_t* base = dst_of(g, slot);
+    for (int32_t i = 0; i < m; i++) {
+      h_s[i] = S->dev_in[slot] + at[(size_t)i];
+      h_d[i] = base + (int64_t)i * dst_stride;
+      h_ss[i] = cbs[(size_t)i];
+      h_ds[i] = dst_capacity;
+    }
+    if (hipMemcpyAsync(S->dev_in[slot], h2d_src, (size_t)total, hipMemcpyHostToDevice, S->s_in) != hipSuccess ||
+        hipMemcpyAsync(S->dev_tab[slot], t, 24 * (size_t)m, hipMemcpyHostToDevice, S->s_in) != hipSuccess ||
+        hipEventRecord(S->e_in[slot], S->s_in) != hipSuccess)
+      return BLOSC2_ERROR_FAILURE;
+    ptrs.clear();   // packed: the chunk bytes are no longer needed
+    return 0;
+  };
+  auto run = [&](int32_t g) -> int {   // (2) + (3)
+    const int slot = g % 2, o = g % 3;
+    const int32_t m = cnt(g);
+    uint8_t* d_out = dst_of(g, slot);
+    if (staged[(size_t)g]) {
+      uint8_t* dt = S->dev_tab[slot];
+      const uint8_t* const* d_s = reinterpret_cast<const uint8_t* const*>(dt);
+      uint8_t* const* d_d = reinterpret_cast<uint8_t* const*>(dt + 8 * (size_t)m);
+      const int32_t* d_ss = reinterpret_cast<const int32_t*>(dt + 16 * (size_t)m);
+      int32_t* d_st = const_cast<int32_t*>(d_ss) + 2 * m;
+      int64_t bound = 0;
+      for (int32_t i = 0; i < m; i++) bound += nbs[(size_t)(lo(g) + i)];
+      if (hipStreamWaitEvent(S->s_k, S->e_in[slot], 0) != hipSuccess ||
+          (!out_dev && hipStreamWaitEvent(S->s_k, S->e_dout[slot], 0) != hipSuccess))
+        return BLOSC2_ERROR_FAILURE;
+      const int rr = b2h::decompress_batch(d_s, d_ss, d_d, d_ss + m, m, bound, d_st, nullptr, S->s_k, S->ws,
+                                           (int64_t)S->in_cap, 0);
+      if (rr < 0) return rr;
+      if (hipEventRecord(S->e_dec[slot], S->s_k) != hipSuccess ||
+          hipStreamWaitEvent(S->s_out, S->e_dec[slot], 0) != hipSuccess ||
+          hipMemcpyAsync(S->pin_st[o], d_st, 4 * (size_t)m, hipMemcpyDeviceToHost, S->s_out) != hipSuccess)
+        return BLOSC2_ERROR_FAILURE;
+    } else {
+      // the context path (synchronous): a device slot's previous output must have left first
+      if (!out_dev && hipEventSynchronize(S->e_dout[slot]) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+      const int rr = b2h::ctx_decompress_device(ctx, ptrs_of[slot].data(), m, d_out, dst_stride, dst_capacity,
+                                                st + lo(g));
+      if (rr < 0) {
+        bool chunk_error = false;   // a chunk's own error is in st[]; anything else stops the pipeline
+        for (int32_t i = 0; i < m; i++) chunk_error |= st[lo(g) + i] == rr;
+        if (!chunk_error) return rr;
+      }
+      ptrs_of[slot].clear();
+    }
+    if (!out_dev &&
+        (hipMemcpyAsync(S->pin_out[o], d_out, (size_t)m * (size_t)dst_stride, hipMemcpyDeviceToHost, S->s_out) != hipSuccess ||
+         hipEventRecord(S->e_dout[slot], S->s_out) != hipSuccess))
+      return BLOSC2_ERROR_FAILURE;
+    return hipEventRecord(S->e_out[o], S->s_out) == hipSuccess ? 0 : BLOSC2_ERROR_FAILURE;
+  };
+  auto unstage = [&](int32_t g) -> int {   // (4)
+    const int o = g % 3;
+    if (hipEventSynchronize(S->e_out[o]) != hipSuccess) return BLOSC2_ERROR_FAILURE;
+    if (staged[(size_t)g]) {
+      for (int32_t i = 0; i < cnt(g); i++) {   // schunk.c:1511-1517
+        const int32_t v = S->pin_st[o][i], nb = nbs[(size_t)(lo(g) + i)];
+        st[lo(g) + i] = v < 0 ? v : (v != nb ? BLOSC2_ERROR_FAILURE : v);
+      }
+    }
+    if (out_host) par_copy(out_host + (int64_t)lo(g) * dst_stride, dst_stride, S->pin_out[o], dst_stride, cnt(g), dst_capacity);
+    return 0;
+  };
+  int behind_rc = 0;
+  std::thread behind;
+  if (r == 0) r = prep(0);
+  for (int32_t g = 0; g < ng && r == 0; g++) {
+    int ahead_rc = 0;
+    std::thread ahead;
+    if (g + 1 < ng) ahead = std::thread([&, g] { ahead_rc = prep(g + 1); });
+    r = run(g);
+    if (behind.joinable()) behind.join();   // group g - 1's copy-out: pinned slot (g + 2) % 3 is free
+    if (r == 0 && behind_rc) r = behind_rc;
+    if (r == 0) behind = std::thread([&, g] { behind_rc = unstage(g); });
+    if (ahead.joinable()) ahead.join();
+    if (r == 0 && ahead_rc) r = ahead_rc;
+  }
+  if (behind.joinable()) behind.join();
+  if (r == 0 && behind_rc) r = behind_rc;
+  (void)hipStreamSynchronize(S->s_in);
+  (void)hipStreamSynchronize(S->s_k);
+  (void)hipStreamSynchronize(S->s_out);
+  stage_release(S);
+  for (int32_t i = 0; i < n && r == 0; i++)
+    if (st[i] < 0) r = st[i];
+  return r;
+}
+
+}  // namespace
+
+// Each worker decodes its contiguous range with staged_decode (above) on its device.
 int b2h_schunk_decompress_buffers(blosc2_schunk* schunk, int64_t nchunk, int32_t n, void* dst, int64_t dst_stride,
                                   int32_t dst_capacity, int32_t* status, int32_t ndevices) {
   if (!schunk || (n > 0 && !dst)) return BLOSC2_ERROR_NULL_POINTER;
@@ -807,49 +1086,12 @@ int b2h_schunk_decompress_buffers(blosc2_schunk* schunk, int64_t nchunk, int32_t
   auto work = [&](int k) {
     const int32_t i0 = (int32_t)((int64_t)n * k / W), i1 = (int32_t)((int64_t)n * (k + 1) / W);
     if (i1 <= i0) return;
-    if (hipSetDevice(k % b2h::device_count()) != hipSuccess) { wrc[k] = BLOSC2_ERROR_FAILURE; return; }
+    const int device = k % b2h::device_count();
+    if (hipSetDevice(device) != hipSuccess) { wrc[k] = BLOSC2_ERROR_FAILURE; return; }
     blosc2_context* ctx = blosc2_create_dctx(dp);
     if (!ctx) { wrc[k] = BLOSC2_ERROR_MEMORY_ALLOC; return; }
-    // groups of G chunks: the engine decodes group g while group g - 1 comes back over PCIe into
-    // a pinned buffer and group g - 2 is copied from pinned memory into the caller's buffer
-    const int32_t G = (int32_t)std::max<int64_t>(1, std::min<int64_t>(i1 - i0, kGroupBytes / std::max<int64_t>(dst_stride, 1)));
-    const int32_t ng = (i1 - i0 + G - 1) / G;
-    Stage S;
-    b2h::ReadBuf hold;   // a frame-attached handle's chunks, read group by group
-    std::vector<const uint8_t*> ptrs;
-    auto lo = [&](int32_t g) { return i0 + g * G; };
-    auto cnt = [&](int32_t g) { return std::min(G, i1 - lo(g)); };
-    auto unstage = [&](int32_t g) {
-      par_copy(out + (int64_t)lo(g) * dst_stride, dst_stride, S.p(g), dst_stride, cnt(g), dst_capacity);
-    };
-    int r = S.init((size_t)G * (size_t)dst_stride) ? 0 : BLOSC2_ERROR_MEMORY_ALLOC;
-    std::thread behind;
-    for (int32_t g = 0; g < ng && r == 0; g++) {
-      // the device buffer's previous D2H (group g - 2) must be done before the engine rewrites it
-      if (g >= 2 && hipEventSynchronize(S.ev[g % 2]) != hipSuccess) { r = BLOSC2_ERROR_FAILURE; break; }
-      int rr = b2h::chunk_ptrs(schunk, nchunk + lo(g), cnt(g), &ptrs, &hold);
-      if (rr >= 0)
-        rr = b2h::ctx_decompress_device(ctx, ptrs.data(), cnt(g), S.dev[g % 2], dst_stride, dst_capacity,
-                                        st.data() + lo(g));
-      if (rr < 0) { r = rr; break; }
-      if (behind.joinable()) behind.join();   // group g - 3's pinned buffer is free again
-      if (hipMemcpyAsync(S.p(g), S.dev[g % 2], (size_t)cnt(g) * (size_t)dst_stride, hipMemcpyDeviceToHost, S.cs) != hipSuccess ||
-          hipEventRecord(S.ev[g % 2], S.cs) != hipSuccess) {
-        r = BLOSC2_ERROR_FAILURE;
-        break;
-      }
-      if (g >= 1) {   // group g - 1 has landed in pinned memory once its event fires
-        const int32_t gp = g - 1;
-        if (hipEventSynchronize(S.ev[gp % 2]) != hipSuccess) { r = BLOSC2_ERROR_FAILURE; break; }
-        behind = std::thread(unstage, gp);
-      }
-    }
-    if (behind.joinable()) behind.join();
-    if (r == 0 && ng >= 1) {
-      if (hipEventSynchronize(S.ev[(ng - 1) % 2]) != hipSuccess) r = BLOSC2_ERROR_FAILURE;
-      else unstage(ng - 1);
-    }
-    wrc[k] = r;
+    wrc[k] = staged_decode(schunk, ctx, device, nchunk + i0, i1 - i0, out + (int64_t)i0 * dst_stride, nullptr,
+                           dst_stride, dst_capacity, st.data() + i0);
     blosc2_free_ctx(ctx);
   };
   std::vector<std::thread> th;

@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/b2h.h"
@@ -1233,15 +1234,39 @@ int ctx_append_device(blosc2_context* ctx, const uint8_t* d_src, const int32_t* 
     if (hipMemcpyAsync(d.host.p, d.in.p, (size_t)total, hipMemcpyDeviceToHost, d.stream) != hipSuccess ||
         hipStreamSynchronize(d.stream) != hipSuccess)
       return fail(BLOSC2_ERROR_FAILURE);
-    for (int32_t k = 0; k < m; k++) {
-      const size_t sz = (size_t)(off[k + 1] - off[k]);
-      uint8_t* c = static_cast<uint8_t*>(malloc(sz));
+    // one malloc'd buffer per chunk (the super-chunk owns them); fresh pages fault in on the first
+    // write, so the copies are split over a few threads
+    const int T = (int)std::max<int64_t>(1, std::min<int64_t>({8, total >> 23, m}));
+    std::vector<char> ok((size_t)T, 1);
+    auto part = [&](int t) {
+      for (int32_t k = m * t / T; k < m * (t + 1) / T; k++) {
+        const size_t sz = (size_t)(off[k + 1] - off[k]);
+        uint8_t* c = static_cast<uint8_t*>(malloc(sz));
+        if (!c) { ok[(size_t)t] = 0; continue; }
+        memcpy(c, d.host.u8() + off[k], sz);
+        chunks_out[g0 + k] = c;
+      }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; t++) th.emplace_back(part, t);
+    part(0);
+    for (auto& x : th) x.join();
+    for (char c : ok)
       if (!c) return fail(BLOSC2_ERROR_MEMORY_ALLOC);
-      memcpy(c, d.host.u8() + off[k], sz);
-      chunks_out[g0 + k] = c;
-    }
   }
   return 0;
+}
+
+// True when `ctx` decodes chunk `c` entirely on the device -- no postfilter, no user filter or
+// codec -- and its header reads; *nbytes / *cbytes from the header.  The fan-out's staged
+// pipeline (b2h_schunk.cpp) queues only such chunks itself and hands the others to
+// ctx_decompress_device.
+bool ctx_chunk_on_device(const blosc2_context* ctx, const uint8_t* c, int32_t* nbytes, int32_t* cbytes) {
+  if (!ctx || !c || ctx->dparams.postfilter) return false;
+  if (blosc2_cbuffer_sizes(c, nbytes, cbytes, nullptr) < 0) return false;
+  ChunkHdr H;
+  if (read_header(c, *cbytes, &H) != 0) return false;
+  return !chunk_needs_host(c, H);
 }
 
 // n host chunks (what blosc2_schunk_decompress_chunk would be handed one by one, schunk.c:1481-1530)

@@ -12,6 +12,7 @@
 #   pmc_c4           FETCH_SIZE / WRITE_SIZE over C4 (fast mode)
 #   configs          tools/bench_configs.py, both modes
 #   smoke            __graft_entry__.smoke()
+#   frame_e2e        tools/frame_e2e.py (T frame file: write, open + decode warm / cold; host fan-out)
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
@@ -31,6 +32,9 @@ for job in "$@"; do
     tests:*)
       timeout -k 10 400 python -u -m pytest tests -m gpu --maxfail=10 -v --timeout 120 --timeout-method thread -k "${job#tests:}" > "$L" 2>&1 || fail "$job" "$L"
       tail -3 "$L" ;;
+    frame_e2e)
+      timeout -k 10 500 python -u tools/frame_e2e.py > "$L" 2>&1 || fail "$job" "$L"
+      cat "$L" | grep measure ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$L" 2>&1 || fail "$job" "$L"
       tail -1 $L ;;
