@@ -1644,8 +1644,11 @@ __host__ __device__ constexpr size_t fused_lds(size_t pos_bytes, int tablog) {
 
 #undef FUSE_TRACE_PTR
 #define FUSE_TRACE_PTR lds_uniform(&A->f.trace)
+#ifndef B2H_FAST_WPE
+#define B2H_FAST_WPE 4   // waves per SIMD the fused fast launch is compiled for (4: <= 128 VGPRs)
+#endif
 template <typename POS, bool DEEP>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4, 8)))   // as k_encode_fast
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(B2H_FAST_WPE, 8)))   // as k_encode_fast
 void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint8_t* __restrict__ sbuf_arg,
                          StreamResult* __restrict__ res_arg, int32_t nstreams_total_arg, int32_t* __restrict__ next_arg,
                          int tablog_arg, const int32_t* __restrict__ porder_arg, EncFuse f_arg) {
