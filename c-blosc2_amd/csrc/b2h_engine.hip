@@ -688,10 +688,13 @@ static int launch_encode_fast_t(Workspace* ws, const CGeom& g0, const uint8_t* f
   return 0;
 }
 
-// u16 positions (half the LDS: twice the waves per CU) while every stream fits 64 KiB
+// u16 table entries (half the LDS: twice the waves per CU): BloscLZ mode 1 at any stream length
+// (positions modulo 2^16, fast_exchange); mode 2 while every stream fits 64 KiB (its prev[] chains
+// keep full positions).
+static bool fast_u16(const CGeom& g) { return g.lzmode != 2 || std::max(g.neblock, g.leftover) <= 65536; }
 static int launch_encode_fast(Workspace* ws, const CGeom& g, const uint8_t* filt, StreamResult* res, int64_t ntot,
                               int32_t* next, const int32_t* porder, hipStream_t st) {
-  const bool small = std::max(g.neblock, g.leftover) <= 65536;
+  const bool small = fast_u16(g);
   if (g.lzmode == 2)
     return small ? launch_encode_fast_t<uint16_t, true>(ws, g, filt, res, ntot, next, porder, st)
                  : launch_encode_fast_t<uint32_t, true>(ws, g, filt, res, ntot, next, porder, st);
@@ -2040,7 +2043,7 @@ static bool fused_encode_ok(const CGeom& g) {
     enc_mode(&nl, &ng);
     return nl == 1 && ng == 3;
   }
-  const bool small = std::max(g.neblock, g.leftover) <= 65536;
+  const bool small = fast_u16(g);
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
   const int tablog = std::min(fast_tablog(), hashlog);
   return (size_t)12 * g.nsc <= ((small ? 2u : 4u) << tablog);
@@ -2048,7 +2051,7 @@ static bool fused_encode_ok(const CGeom& g) {
 static int launch_encode_fast_fused(Workspace* ws, const CGeom& g, const uint8_t* filt, StreamResult* res,
                                     int64_t ntot, int32_t* next, const int32_t* porder, const EncFuse& f,
                                     hipStream_t st) {
-  const bool small = std::max(g.neblock, g.leftover) <= 65536;
+  const bool small = fast_u16(g);
   if (g.lzmode == 2)
     return small ? launch_encode_fast_fused_t<uint16_t, true>(ws, g, filt, res, ntot, next, porder, f, st)
                  : launch_encode_fast_fused_t<uint32_t, true>(ws, g, filt, res, ntot, next, porder, f, st);

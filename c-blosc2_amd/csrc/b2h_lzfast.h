@@ -40,9 +40,14 @@ constexpr int kFastTile = 128, kHalf = 64;
 
 // Table exchange of 64 positions: the lanes with p < loop_end hash in[p..p+3] (v) and swap p into
 // the bucket.  Returns the candidate (the bucket's previous position; 0 for an empty bucket).
-// POS = uint32_t: one ds_wrxchg_rtn_b32.  POS = uint16_t (streams <= 64 KiB, half the LDS, twice
-// the waves per CU): two buckets per dword, exchanged with ds_mskor_rtn_b32 -- the masked-or
-// atomic replaces just the bucket's half ((old & ~mask) | p << sh) and returns the old dword.
+// POS = uint32_t: one ds_wrxchg_rtn_b32.  POS = uint16_t (half the LDS, twice the waves per CU):
+// two buckets per dword, exchanged with ds_mskor_rtn_b32 -- the masked-or atomic replaces just the
+// bucket's half ((old & ~mask) | p << sh) and returns the old dword.  A u16 bucket holds its
+// position modulo 2^16 and the candidate is the latest position below p with those low bits: the
+// bucket's own position while p < 2^16 (every stream of a split chunk), and past it the bucket's
+// position or, for a bucket older than 2^16 positions, a nearer one with the same low bits -- a
+// suggestion like any other, verified byte for byte (tools/fm_model.c, the same rule).  So streams
+// longer than 64 KiB (unsplit blocks: BITSHUFFLE, leftovers) run at the u16 table's occupancy too.
 template <typename POS>
 __device__ __forceinline__ uint32_t fast_exchange(uint32_t v, int32_t p, bool valid, int tablog, B2H_LDS uint8_t* tab) {
   uint32_t old = 0;
@@ -53,11 +58,11 @@ __device__ __forceinline__ uint32_t fast_exchange(uint32_t v, int32_t p, bool va
     } else {
       const uint32_t addr = (uint32_t)reinterpret_cast<uintptr_t>(tab) + ((h >> 1) << 2);
       const uint32_t sh = (h & 1u) << 4;
-      const uint32_t mask = 0xffffu << sh, data = (uint32_t)p << sh;
+      const uint32_t mask = 0xffffu << sh, data = ((uint32_t)p & 0xffffu) << sh;
       uint32_t w;
       asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
                    : "=v"(w) : "v"(addr), "v"(mask), "v"(data) : "memory");
-      old = (w >> sh) & 0xffffu;
+      old = (uint32_t)p - (((uint32_t)p - ((w >> sh) & 0xffffu)) & 0xffffu);
     }
   }
   return old;
@@ -256,6 +261,12 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
     // mismatch lies in word 0 and the other 14 words are neither loaded nor compared
     const B2H_GLB uint32_t* cw[2];
     uint32_t csh[2], c0[2], c1[2];
+    // u16 buckets past 2^16 positions (fast_exchange): a near candidate may stand for one 2^16
+    // positions further back (still within MAX_FARDISTANCE); when the near one's first 4 bytes do
+    // not match, that one is offered instead (tools/fm_model.c insert_tile).  Its first words come
+    // in the same round trip.
+    uint32_t a20[2] = {0u, 0u}, a21[2] = {0u, 0u};
+    bool alt[2] = {false, false};
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       gin_t cq = in + (cok[h] ? (int32_t)cand[h] : (valid[h] ? p[h] : 0));
@@ -264,8 +275,28 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
       c0[h] = cw[h][0];
       c1[h] = cw[h][1];
     }
+    // (uniform: only streams longer than 2^16 positions -- the split planes of T never come here)
+    if (sizeof(POS) == 2 && !DEEP && __builtin_amdgcn_readfirstlane(loop_end) > 65536) {
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        alt[h] = cok[h] && cand[h] >= 65536u && (uint32_t)p[h] - cand[h] < kLzFar - 65536u;
+        if (alt[h]) {
+          a20[h] = cw[h][-16384];   // 2^16 bytes back: the same alignment
+          a21[h] = cw[h][-16383];
+        }
+      }
+    }
     load_a(t + 1, na, nsh);   // issued after the candidate loads: the compare waits for those only
     ant = t + 1;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      if (alt[h] && (v[h] ^ funnel(c0[h], c1[h], csh[h])) != 0) {
+        cand[h] -= 65536u;
+        cw[h] -= 16384;
+        c0[h] = a20[h];
+        c1[h] = a21[h];
+      }
+    }
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const uint32_t x0 = v[h] ^ funnel(c0[h], c1[h], csh[h]);

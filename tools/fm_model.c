@@ -10,6 +10,8 @@
  *
  *   insert_tile(t): for i = 0..127 (p = 128 t + i < loop_end, in order):
  *                     cand[p] = tab[hash(in[p..p+3])]; tab[hash] = p
+ *                   (mode 1 keeps p mod 2^16 per bucket: cand = the latest position below p with
+ *                   the bucket's low 16 bits -- the same while p < 2^16)
  *
  * and the parse consumes tiles: entering tile T (the one holding the parse position) it inserts T
  * if no later tile was inserted yet, then T + 1 (the GPU kernel's matcher wave exchanges and
@@ -67,8 +69,20 @@ static void insert_tile(const uint8_t *in, int32_t t, int32_t loop_end, int32_t 
     const int32_t p = t * TILE + i;
     if (p >= loop_end) break;
     const uint32_t h = lz_hash(ld32(in + p), tablog);
-    const int32_t c1 = (int32_t)tab[h];
-    tab[h] = (uint32_t)p;
+    int32_t c1;
+    if (fm_depth < 2) {
+      /* 16-bit buckets (the kernel's u16 table at any stream length): a bucket keeps p mod 2^16 and
+       * offers the latest position below p with those low bits -- its own position while
+       * p < 2^16, a nearer alias for a bucket older than 2^16 positions */
+      c1 = p - (int32_t)(((uint32_t)p - tab[h]) & 0xffffu);
+      tab[h] = (uint32_t)p & 0xffffu;
+      /* a near candidate may stand for one 2^16 positions further back: offered instead when the
+       * near one's first 4 bytes differ (and the far one is within MAX_FARDISTANCE) */
+      if (c1 >= 65536 && p - c1 < LZ_FAR - 65536 && ld32(in + c1) != ld32(in + p)) c1 -= 65536;
+    } else {
+      c1 = (int32_t)tab[h];
+      tab[h] = (uint32_t)p;
+    }
     prev[p] = c1;
     cand[p] = c1;
     /* a usable first candidate (0 < p - c1 < MAX_FARDISTANCE, the parse's own test) opens the chain;
