@@ -3421,6 +3421,14 @@ __device__ __forceinline__ void ds_wave_first(const uint8_t* __restrict__ src, u
     carry ^= (uint64_t)__shfl((long long)sc, 63);
   }
 }
+// The in-launch (DELTA, SHUFFLE) decode (park/claim protocol below) is a build option, off by
+// default: measured slower than the separate k_dfilter pass, so default builds carry
+// neither the protocol nor ds_finish_block in k_decode.  Build with -DB2H_DEC_FUSE_DS_BUILD=1 and
+// run with B2H_DEC_FUSE_DS=1 to measure it.
+#ifndef B2H_DEC_FUSE_DS_BUILD
+#define B2H_DEC_FUSE_DS_BUILD 0
+#endif
+#if B2H_DEC_FUSE_DS_BUILD
 // (templated on the decoder's ring size: one copy per k_decode instantiation, which then takes
 // that kernel's register budget instead of its own)
 template <int RLOG>
@@ -3476,6 +3484,7 @@ __device__ __noinline__ void ds_finish_block(const DChunk& d, int32_t c, int32_t
       for (int b = 0; b < ts; b++) dst[(int64_t)i * ts + b] = (uint8_t)(v >> (8 * b));
   }
 }
+#endif
 
 template <int RLOG>
 __device__ __forceinline__ void finish_block(const DChunk* __restrict__ ch, const DStream* __restrict__ streams, int32_t s,
@@ -3485,7 +3494,11 @@ __device__ __forceinline__ void finish_block(const DChunk* __restrict__ ch, cons
   asm volatile("" ::: "memory");
   const DStream st = streams[s];
   const DChunk& d = ch[st.chunk];
+#if B2H_DEC_FUSE_DS_BUILD
   const bool fuse_ds = __builtin_amdgcn_readfirstlane(d.fuse_ds) != 0;
+#else
+  constexpr bool fuse_ds = false;   // never planned: the host always sets mode bit 16
+#endif
   if (!__builtin_amdgcn_readfirstlane(d.fuse_unshuffle) && !fuse_ds) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int32_t blk = st.dst_off / d.blocksize;
@@ -3503,6 +3516,7 @@ __device__ __forceinline__ void finish_block(const DChunk* __restrict__ ch, cons
     unshuffle4_wave_lds(stage + d.stage_off + off, dsts[st.chunk] + off, lo ? d.leftover : d.blocksize, ring);
     return;
   }
+#if B2H_DEC_FUSE_DS_BUILD
   // (DELTA, SHUFFLE): block 0 first; a block whose streams finish before block 0 is final parks,
   // and whichever of it and block 0's wave sees the other's mark takes it (exactly once: CLAIM)
   constexpr int32_t kDone = 1 << 30, kPark = 1 << 29, kClaim = 1 << 28;
@@ -3532,6 +3546,7 @@ __device__ __forceinline__ void finish_block(const DChunk* __restrict__ ch, cons
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     ds_finish_block<RLOG>(d, st.chunk, k, dsts, stage, ring);
   }
+#endif
 }
 
 template <int RLOG>
@@ -3826,12 +3841,17 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
     cap_stage = std::max<int64_t>(dst_bound, 0);
   }
   static const int no_fuse = getenv("B2H_FUSE_UNSHUFFLE") && atoi(getenv("B2H_FUSE_UNSHUFFLE")) == 0 ? 8 : 0;
-  // mode bit 16: no in-launch DELTA + SHUFFLE -- with block masks (a masked block 0 never
-  // completes) and unless B2H_DEC_FUSE_DS=1: measured slower than the separate k_dfilter pass on
-  // C4 (decompress 20.2 vs 12.0 ms: one wave per 512 KiB block is latency-bound where k_dfilter's
-  // 256-thread workgroups keep the bytes in flight)
+  // mode bit 16: no in-launch DELTA + SHUFFLE -- always in default builds, and with block masks
+  // (a masked block 0 never completes); a B2H_DEC_FUSE_DS_BUILD build plans it when
+  // B2H_DEC_FUSE_DS=1.  Measured slower than the separate k_dfilter pass on C4 (decompress 20.2
+  // vs 12.0 ms: one wave per 512 KiB block is latency-bound where k_dfilter's 256-thread
+  // workgroups keep the bytes in flight)
+#if B2H_DEC_FUSE_DS_BUILD
   const char* fds = getenv("B2H_DEC_FUSE_DS");
   const int ds_off = (d_maskout || !(fds && atoi(fds) == 1)) ? 16 : 0;
+#else
+  const int ds_off = 16;
+#endif
   k_dplan_chunks<<<(n + 255) / 256, 256, 0, st>>>(d_src, d_srcsize, d_dstsize, ch, n, mode | no_fuse | ds_off);
   k_dscan<<<1, 1024, 0, st>>>(ch, n, tot, cap_blocks, cap_streams, cap_stage, d_dst);
   HIPCHK(hipGetLastError());

@@ -225,6 +225,10 @@ struct GlbTab {
 
 // End of the common prefix of in[x..] and in[x-d..], one past the first mismatch, capped at
 // `bound` (get_match / get_run semantics, blosc/blosclz.c:119-165).  64 lanes x 16 bytes per step.
+#ifndef B2H_MATCH_U
+#define B2H_MATCH_U 4   // 1 KiB sub-steps per round trip of a long match's extension
+#endif
+template <int U = B2H_MATCH_U>
 __device__ __forceinline__ int32_t wave_match_end(gin_t in, int32_t x, uint32_t d, int32_t bound) {
   const int lane = lane_id();
   // first mismatch in 16 bytes at q (16: none; bytes at and after `bound` do not count)
@@ -258,16 +262,16 @@ __device__ __forceinline__ int32_t wave_match_end(gin_t in, int32_t x, uint32_t 
     x += 1024;
   }
   while (x < bound) {
-    uint32_t a[4][4], b[4][4];
+    uint32_t a[U][4], b[U][4];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < U; u++) {
       const int32_t q = x + u * 1024 + lane * 16;
 #pragma unroll
       for (int k = 0; k < 4; k++) { a[u][k] = 0; b[u][k] = 0; }
       if (q < bound) { ld16(in + q, a[u]); ld16(in + q - d, b[u]); }
     }
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < U; u++) {
       const int32_t q = x + u * 1024 + lane * 16;
       const int32_t first = first16(q, a[u], b[u]);
       const uint64_t mm = __ballot(first < 16);
@@ -276,7 +280,7 @@ __device__ __forceinline__ int32_t wave_match_end(gin_t in, int32_t x, uint32_t 
         return x + u * 1024 + l * 16 + rdlane(first, l) + 1;
       }
     }
-    x += 4096;
+    x += U * 1024;
   }
   return bound;
 }

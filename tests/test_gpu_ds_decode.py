@@ -1,8 +1,10 @@
 """GPU tier: (DELTA, SHUFFLE) chunk decode, both by the separate k_dfilter pass (the default) and
-undone inside the decode launch (B2H_DEC_FUSE_DS=1: k_decode finish_block, DChunk::fuse_ds; the
-C4 pipeline, measured slower than the separate pass -- DESIGN.md §3): block 0's completing wave un-shuffles and XOR-scans it, every
-other block is un-shuffled and XORed with the final block 0 once that is published (a block that
-finishes first parks and is taken exactly once).  Checked against the oracle's chunks decoded on
+undone inside the decode launch (k_decode finish_block, DChunk::fuse_ds; the C4 pipeline, measured
+slower than the separate pass -- DESIGN.md §3; compiled in only with -DB2H_DEC_FUSE_DS_BUILD=1 and
+then chosen by B2H_DEC_FUSE_DS=1 -- in a default build the "in-launch" cases check that the variable
+is ignored): block 0's completing wave un-shuffles and XOR-scans it, every other block is
+un-shuffled and XORed with the final block 0 once that is published (a block that finishes first
+parks and is taken exactly once).  Checked against the oracle's chunks decoded on
 the CPU (blosc/delta.c:18-161 + blosc/shuffle-generic.h:34-83 restated in oracle/blosc2_oracle.c):
 typesizes 2 / 4 / 8, several blocksizes, leftover blocks that do and do not fuse (a leftover that
 is not whole quads keeps the chunk on the k_dfilter path), destinations at 16-byte-aligned and at
