@@ -2946,6 +2946,10 @@ __global__ void k_dplan_chunks(const uint8_t* const* __restrict__ srcs, const in
     while (bwd_noop(d.filters[i])) i--;
     const int32_t ts = d.filters_meta[i] ? d.filters_meta[i] : d.typesize;
     d.fuse_unshuffle = d.filters[i] == kShuffle && ts == 4 && (mode & 8) == 0;
+    // a block's streams are its four planes (or one stream holds the whole shuffled image): the
+    // unshuffle reads raw streams where they lie in the chunk and synthesises run streams, so
+    // only LZ planes are staged
+    d.unshuf_direct = d.fuse_unshuffle && (d.dont_split || (d.typesize == 4 && bs % 4 == 0));
   }
   // (DELTA, SHUFFLE) at typesize 2 / 4 / 8 over whole quads (the C4 pipeline): undone inside the
   // decode launch as well -- block 0's completing wave un-shuffles and XOR-scans it, every other
@@ -3175,18 +3179,21 @@ __device__ __forceinline__ bool decode_stream(const uint8_t* const* __restrict__
   // the stream's place in the serial walk, for the error key
   const int32_t blk = st.dst_off / d.blocksize;
   const int32_t step = 1 + (st.dst_off - blk * d.blocksize) / nb;
+  // ds_runs: k_dfilter synthesises run planes; unshuf_direct: finish_block reads raw planes in
+  // place and synthesises run planes -- neither is staged
+  const bool nostage = d.ds_runs || d.unshuf_direct;
   if (st.csize == 0) {
-    if (!d.ds_runs) wave_fill<true>(out, 0, nb);   // ds_runs: k_dfilter synthesises the plane
+    if (!nostage) wave_fill<true>(out, 0, nb);
   } else if (st.csize < 0) {
     const uint8_t token = in[0];
     if (!(token & 1) || st.csize < -255) {
       if (lane == 0) rec_err(ch, c, blk, step, E_RUNLEN);
     } else {
-      if (!d.ds_runs) wave_fill<true>(out, (uint8_t)(-st.csize), nb);
+      if (!nostage) wave_fill<true>(out, (uint8_t)(-st.csize), nb);
       *kind_out = 1;
     }
   } else if (st.csize == nb) {
-    wave_copy<true>(out, in, nb);
+    if (!d.unshuf_direct) wave_copy<true>(out, in, nb);
     *kind_out = 2;
   } else if ((d.flags >> 5) == 1) {   // LZ4 (blosc/blosc2.c:2062-2067)
     const int32_t got = wave_lz4_decode_ring<RLOG>(in, st.csize, out, nb, ring, (gin_t)(srcs[c] + d.dict_off), d.dict_size);
@@ -3217,12 +3224,53 @@ __device__ __forceinline__ bool decode_stream(const uint8_t* const* __restrict__
 #define B2H_UNSHUF_DEPTH 2
 #endif
 constexpr int kUnshufDepth = B2H_UNSHUF_DEPTH;
-__device__ __forceinline__ void unshuffle4_wave_lds(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int32_t bsize,
+// Where each of a block's four planes comes from (DChunk::unshuf_direct): the decoder's staged
+// image (16-byte aligned), a raw stream in place in the chunk (any alignment: aligned dwords and a
+// funnel shift, never a dword past the plane's last byte), or a run (bit j of runm, byte j of
+// runb; never read).  `tail`: the bsize % 4 bytes after the planes (an unsplit image only).
+struct PlaneSrc4 {
+  const uint8_t* p[4];
+  const uint8_t* tail;
+  uint32_t runm, runb;
+};
+__device__ __forceinline__ uint32_t plane_splat(const PlaneSrc4& ps, int j) {
+  return 0x01010101u * ((ps.runb >> (8 * j)) & 0xffu);
+}
+// 16 bytes of plane j at byte offset `off`
+__device__ __forceinline__ u32x4 plane_ld16(const PlaneSrc4& ps, int j, int64_t off) {
+  if ((ps.runm >> j) & 1u) {
+    const uint32_t w = plane_splat(ps, j);
+    return u32x4{w, w, w, w};
+  }
+  const uint8_t* s = ps.p[j] + off;
+  const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(ps.p[j]) & 3);   // wave-uniform
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(s - sh);
+  if (sh == 0) {
+    typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+    const u32x4a4 v = *reinterpret_cast<const u32x4a4*>(q);
+    return u32x4{v.x, v.y, v.z, v.w};
+  }
+  const uint32_t a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
+  return u32x4{funnel(a, b, sh), funnel(b, c, sh), funnel(c, d, sh), funnel(d, e, sh)};
+}
+// the dword of plane j at element quad qd (bytes 4qd .. 4qd + 3)
+__device__ __forceinline__ uint32_t plane_ld4(const PlaneSrc4& ps, int j, int32_t qd) {
+  if ((ps.runm >> j) & 1u) return plane_splat(ps, j);
+  const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(ps.p[j]) & 3);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(ps.p[j] - sh) + qd;
+  return sh ? funnel(q[0], q[1], sh) : q[0];
+}
+__device__ __forceinline__ uint8_t plane_ld1(const PlaneSrc4& ps, int j, int32_t i) {
+  return ((ps.runm >> j) & 1u) ? (uint8_t)(ps.runb >> (8 * j)) : ps.p[j][i];
+}
+
+// The block's typesize-4 unshuffle by one wave, planes -> dst.
+__device__ __forceinline__ void unshuffle4_wave_lds(const PlaneSrc4& ps, uint8_t* __restrict__ dst, int32_t bsize,
                                                     B2H_LDS uint8_t* lds) {
   const int lane = lane_id();
   const int32_t n = bsize / 4;
-  if (!aligned16(src) || !aligned16(dst)) {
-    for (int32_t i = lane; i < n * 4; i += 64) dst[i] = src[(i & 3) * n + (i >> 2)];
+  if (!aligned16(dst)) {
+    for (int32_t i = lane; i < n * 4; i += 64) dst[i] = plane_ld1(ps, i & 3, i >> 2);
   } else {
     const int32_t rows = (n % 4 == 0) ? n / 1024 : 0;   // 1024 elements = 1 KiB per plane
     if (rows > 0) {
@@ -3232,7 +3280,7 @@ __device__ __forceinline__ void unshuffle4_wave_lds(const uint8_t* __restrict__ 
       for (int d = 0; d < kUnshufDepth; d++) {
         if (d < rows) {
 #pragma unroll
-          for (int p = 0; p < 4; p++) v[d][p] = *reinterpret_cast<const u32x4*>(src + (int64_t)p * n + d * 1024 + 16 * lane);
+          for (int p = 0; p < 4; p++) v[d][p] = plane_ld16(ps, p, d * 1024 + 16 * lane);
         }
       }
 #pragma unroll 1
@@ -3247,9 +3295,7 @@ __device__ __forceinline__ void unshuffle4_wave_lds(const uint8_t* __restrict__ 
         }
         if (r + kUnshufDepth < rows) {
 #pragma unroll
-          for (int p = 0; p < 4; p++)
-            v[kUnshufDepth - 1][p] =
-                *reinterpret_cast<const u32x4*>(src + (int64_t)p * n + (int64_t)(r + kUnshufDepth) * 1024 + 16 * lane);
+          for (int p = 0; p < 4; p++) v[kUnshufDepth - 1][p] = plane_ld16(ps, p, (int64_t)(r + kUnshufDepth) * 1024 + 16 * lane);
         }
         uint8_t* row = dst + (int64_t)r * 4096;
 #pragma unroll
@@ -3264,12 +3310,14 @@ __device__ __forceinline__ void unshuffle4_wave_lds(const uint8_t* __restrict__ 
     }
     for (int32_t q = rows * 256 + lane; q < n / 4; q += 64) {   // quads after the whole rows
       uint32_t w[4];
-      load_planes<4>(src, q, n, w);
+#pragma unroll
+      for (int p = 0; p < 4; p++) w[p] = plane_ld4(ps, p, q);
       store_quad<4>(dst, q, w);
     }
-    for (int32_t i = (n / 4) * 16 + lane; i < n * 4; i += 64) dst[i] = src[(i & 3) * n + (i >> 2)];
+    for (int32_t i = (n / 4) * 16 + lane; i < n * 4; i += 64) dst[i] = plane_ld1(ps, i & 3, i >> 2);
   }
-  for (int32_t i = n * 4 + lane; i < bsize; i += 64) dst[i] = src[i];
+  for (int32_t i = n * 4 + lane; i < bsize; i += 64)
+    dst[i] = ps.tail ? ps.tail[i - n * 4] : (uint8_t)ps.runb;
 }
 
 // One (DELTA, SHUFFLE) block by one wave, stage -> dst: block 0 un-shuffled and XOR-scanned over
@@ -3488,6 +3536,7 @@ __device__ __noinline__ void ds_finish_block(const DChunk& d, int32_t c, int32_t
 
 template <int RLOG>
 __device__ __forceinline__ void finish_block(const DChunk* __restrict__ ch, const DStream* __restrict__ streams, int32_t s,
+                                             const uint8_t* const* __restrict__ srcs,
                                              uint8_t* const* __restrict__ dsts, uint8_t* __restrict__ stage,
                                              int32_t* __restrict__ bcnt, B2H_LDS uint8_t* ring) {
   // re-read the plan words here: kept live across the decoder they cost it registers
@@ -3513,7 +3562,36 @@ __device__ __forceinline__ void finish_block(const DChunk* __restrict__ ch, cons
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (!fuse_ds) {
     const int64_t off = (int64_t)blk * d.blocksize;
-    unshuffle4_wave_lds(stage + d.stage_off + off, dsts[st.chunk] + off, lo ? d.leftover : d.blocksize, ring);
+    const int32_t bsize = lo ? d.leftover : d.blocksize, n = bsize / 4;
+    const uint8_t* img = stage + d.stage_off + off;
+    PlaneSrc4 ps;
+    ps.runm = 0;
+    ps.runb = 0;
+    for (int j = 0; j < 4; j++) ps.p[j] = img + (int64_t)j * n;
+    ps.tail = img + 4 * (int64_t)n;
+    if (__builtin_amdgcn_readfirstlane(d.unshuf_direct)) {
+      // the block's streams: one per plane, or one holding the whole shuffled image
+      const int32_t s0 = d.stream_base + blk * (d.dont_split ? 1 : d.typesize);
+      const uint8_t* src = srcs[st.chunk];
+      for (int j = 0; j < ns; j++) {
+        const int32_t cs = __builtin_amdgcn_readfirstlane(streams[s0 + j].csize);
+        const int32_t so = __builtin_amdgcn_readfirstlane(streams[s0 + j].src);
+        const int32_t nb = __builtin_amdgcn_readfirstlane(streams[s0 + j].neblock);
+        if (cs <= 0) {                          // a run (0: zeros; an invalid one failed the chunk)
+          const uint32_t b = (uint8_t)(-cs);
+          if (ns == 1) { ps.runm = 0xfu; ps.runb = b * 0x01010101u; ps.tail = nullptr; }
+          else { ps.runm |= 1u << j; ps.runb |= b << (8 * j); }
+        } else if (cs == nb) {                  // raw: in place
+          if (ns == 1) {
+            for (int k = 0; k < 4; k++) ps.p[k] = src + so + (int64_t)k * n;
+            ps.tail = src + so + 4 * (int64_t)n;
+          } else {
+            ps.p[j] = src + so;
+          }
+        }
+      }
+    }
+    unshuffle4_wave_lds(ps, dsts[st.chunk] + off, bsize, ring);
     return;
   }
 #if B2H_DEC_FUSE_DS_BUILD
@@ -3567,7 +3645,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RLOG == 12 ?
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     int32_t kind = 0;
     if (decode_stream<RLOG>(srcs, dsts, ch, streams[s], stage, maskout, mask_stride, ring, &kind))
-      finish_block<RLOG>(ch, streams, s, dsts, stage, bcnt, ring);
+      finish_block<RLOG>(ch, streams, s, srcs, dsts, stage, bcnt, ring);
     if (dbg && lane_id() == 0) {
       dbg[2 * s] = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
       dbg[2 * s + 1] = kind;

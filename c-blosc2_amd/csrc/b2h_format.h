@@ -67,6 +67,8 @@ struct DChunk {
   uint8_t fuse_ds;             // (DELTA, SHUFFLE) at typesize 2/4/8: undone inside the decode launch
   uint8_t ds_runs;             // (DELTA, SHUFFLE) undone by k_dfilter, whose planes of run streams it
                                // synthesises from the csize word: k_decode leaves them unwritten
+  uint8_t unshuf_direct;       // fuse_unshuffle with planes = streams: raw planes are read in place
+                               // from the chunk and run planes synthesised, neither staged
   int32_t dict_off, dict_size; // LZ4 dictionary section (BLOSC2_USEDICT): offset in the chunk, bytes
 };
 
