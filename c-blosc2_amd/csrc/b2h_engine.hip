@@ -1644,6 +1644,8 @@ struct FusedArgs {
 __host__ __device__ constexpr size_t fused_lds(size_t pos_bytes, int tablog) {
   return fast_lds(pos_bytes, tablog) + ((sizeof(FusedArgs) + 15) & ~size_t(15));
 }
+// eight two-wave workgroups per CU (160 KiB of LDS) at the default u16 table
+static_assert(fused_lds(2, 13) <= 160 * 1024 / 8, "fused fast encoder: more than 20 KiB of LDS per workgroup");
 
 #undef FUSE_TRACE_PTR
 #define FUSE_TRACE_PTR lds_uniform(&A->f.trace)

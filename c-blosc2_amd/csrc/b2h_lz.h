@@ -998,7 +998,50 @@ __device__ __noinline__ int32_t copy_general(B2H_LDS uint8_t* ring, gout_t out, 
   const bool overlap = dist < len;
   const int32_t step = overlap ? 64 % dist : 0;
   int32_t r = overlap ? lane % dist : 0;
+  // A long overlapping match repeats its period `dist`, so any multiple of it is a distance too:
+  // once the first D = a multiple of lcm(dist, 16) >= 1 KiB bytes are out (byte by byte, below),
+  // the rest copies 16 bytes per lane from D back -- 16-byte aligned on both sides of the ring,
+  // one LDS round trip per KiB instead of sixteen (C4's int64 ramp: 64 KiB matches at distance
+  // 256).  D stays within the ring (D + 1 KiB + PIECE <= R: the source slot is never overwritten).
+  int32_t vec_from = len;   // relative output offset where the 16-byte copy takes over
+  int32_t D = 0;
+  if (overlap && len >= 4096 && src >= 0) {
+    int32_t l16 = dist;
+    while (l16 & 15) l16 += dist;   // lcm(dist, 16)
+    D = ((STEP + l16 - 1) / l16) * l16;
+    if (D + STEP + PIECE <= R) {
+      const int32_t a = D + ((16 - ((op + D) & 15)) & 15);   // and the destination 16-byte aligned
+      if (a + STEP < len) vec_from = a;
+    }
+  }
   for (int32_t done = 0; done < len; done += STEP) {
+    if (vec_from < len && done + STEP > vec_from) {
+      if (done < vec_from) {        // the bytes before the 16-byte copy takes over
+        const int32_t n = vec_from - done;
+        while (op + done + n - F > R) { ring_flush<RLOG>(ring, out, F, F + PIECE); F += PIECE; }
+        if (src < F) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        for (int32_t i = done + lane; i < done + n; i += 64) {
+          const int32_t y = src + r;
+          ring[(op + i) & RM] = y >= F ? ring[y & RM] : out[y];
+          r += step;
+          if (r >= dist) r -= dist;
+        }
+        done = vec_from - STEP;   // (the loop adds STEP)
+        continue;
+      }
+      const int32_t n = min(len - done, STEP);
+      while (op + done + n - F > R) { ring_flush<RLOG>(ring, out, F, F + PIECE); F += PIECE; }
+      const int32_t n16 = n >> 4;
+      if (lane < n16) {
+        const int32_t x = op + done + 16 * lane;
+        *reinterpret_cast<B2H_LDS u32x4*>(ring + (x & RM)) = *reinterpret_cast<const B2H_LDS u32x4*>(ring + ((x - D) & RM));
+      }
+      for (int32_t i = (n16 << 4) + lane; i < n; i += 64) {
+        const int32_t x = op + done + i;
+        ring[x & RM] = ring[(x - D) & RM];
+      }
+      continue;
+    }
     const int32_t n = min(len - done, STEP);
     while (op + done + n - F > R) { ring_flush<RLOG>(ring, out, F, F + PIECE); F += PIECE; }
     if (src < F) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");

@@ -234,7 +234,16 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
   };
   // insert tile t (half 0, then half 1: position order), test every position's candidate, hand
   // the records over in slot `slot`
-  auto produce = [&](int32_t t, int slot) {
+  EPROF_DECL;
+  // Two phases per tile: AHEAD(t) inserts tile t and issues its candidates' first-word loads,
+  // FINISH writes t's records.  (Measured and not kept, round 5: AHEAD one step before FINISH, so
+  // the loads land across the barrier -- T 203.5 vs 203.2 GiB/s; and the two waves decoupled
+  // through a 3-slot record ring with every tile inserted -- 203.6.  The matcher's step is not
+  // load-latency-bound and the barrier is not the cost: both waves' chains share the SIMDs.)
+  int32_t pti = 0;   // the tile AHEAD handled, for FINISH
+  uint32_t pv[2], pcand[2], pc0[2], pc1[2], pa20[2] = {0u, 0u}, pa21[2] = {0u, 0u};
+  bool pcok[2], palt[2] = {false, false};
+  auto ahead = [&](int32_t t) {
     uint32_t a0[2][2], ash[2];
     if (t == ant) {
 #pragma unroll
@@ -243,94 +252,174 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
       load_a(t, a0, ash);
     }
     int32_t p[2];
-    uint32_t v[2], cand[2];
+    uint32_t cand[2];
     bool valid[2], cok[2];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       p[h] = t * kFastTile + h * kHalf + lane;
       valid[h] = p[h] < loop_end;
-      v[h] = funnel(a0[h][0], a0[h][1], ash[h]);
+      pv[h] = funnel(a0[h][0], a0[h][1], ash[h]);
     }
 #pragma unroll
     for (int h = 0; h < 2; h++) {   // in order: half 1's positions follow half 0's
-      cand[h] = fast_exchange<POS>(v[h], p[h], valid[h], tablog, tab);
+      cand[h] = fast_exchange<POS>(pv[h], p[h], valid[h], tablog, tab);
       cok[h] = fast_cand_ok(p[h], cand[h], valid[h]);
     }
     if constexpr (DEEP) deep_select(t, p, valid, a0, ash, cand, cok);
-    // the candidate's first word decides most halves: when no lane's 4 bytes match, every first
-    // mismatch lies in word 0 and the other 14 words are neither loaded nor compared
-    const B2H_GLB uint32_t* cw[2];
-    uint32_t csh[2], c0[2], c1[2];
-    // u16 buckets past 2^16 positions (fast_exchange): a near candidate may stand for one 2^16
-    // positions further back (still within MAX_FARDISTANCE); when the near one's first 4 bytes do
-    // not match, that one is offered instead (tools/fm_model.c insert_tile).  Its first words come
-    // in the same round trip.
-    uint32_t a20[2] = {0u, 0u}, a21[2] = {0u, 0u};
-    bool alt[2] = {false, false};
+    // every position's candidate words 0..1 (its first four bytes); lanes without a candidate load
+    // their own bytes
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       gin_t cq = in + (cok[h] ? (int32_t)cand[h] : (valid[h] ? p[h] : 0));
-      cw[h] = align4(cq);
-      csh[h] = (uint32_t)(reinterpret_cast<uintptr_t>(cq) & 3);
-      c0[h] = cw[h][0];
-      c1[h] = cw[h][1];
-    }
-    // (uniform: only streams longer than 2^16 positions -- the split planes of T never come here)
-    if (sizeof(POS) == 2 && !DEEP && __builtin_amdgcn_readfirstlane(loop_end) > 65536) {
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        alt[h] = cok[h] && cand[h] >= 65536u && (uint32_t)p[h] - cand[h] < kLzFar - 65536u;
-        if (alt[h]) {
-          a20[h] = cw[h][-16384];   // 2^16 bytes back: the same alignment
-          a21[h] = cw[h][-16383];
+      const B2H_GLB uint32_t* cw = align4(cq);
+      pc0[h] = cw[0];
+      pc1[h] = cw[1];
+      // u16 buckets past 2^16 positions (fast_exchange): a near candidate may stand for one 2^16
+      // positions further back (still within MAX_FARDISTANCE); when the near one's first 4 bytes
+      // do not match, that one is offered instead (tools/fm_model.c insert_tile).  Its first words
+      // come in the same round trip.  (Uniform: only streams longer than 2^16 positions.)
+      if (sizeof(POS) == 2 && !DEEP && __builtin_amdgcn_readfirstlane(loop_end) > 65536) {
+        palt[h] = cok[h] && cand[h] >= 65536u && (uint32_t)p[h] - cand[h] < kLzFar - 65536u;
+        if (palt[h]) {
+          pa20[h] = cw[-16384];   // 2^16 bytes back: the same alignment
+          pa21[h] = cw[-16383];
         }
       }
+      pcand[h] = cand[h];
+      pcok[h] = cok[h];
     }
-    load_a(t + 1, na, nsh);   // issued after the candidate loads: the compare waits for those only
+    load_a(t + 1, na, nsh);   // the next tile's own words, for the next AHEAD
     ant = t + 1;
+    pti = t;
+  };
+  auto finish = [&](int slot) {
+    const int32_t t = pti;
+    int32_t p[2];
+    uint32_t v[2], cand[2], c0[2], c1[2], csh[2];
+    bool cok[2];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-      if (alt[h] && (v[h] ^ funnel(c0[h], c1[h], csh[h])) != 0) {
+      p[h] = t * kFastTile + h * kHalf + lane;
+      v[h] = pv[h];
+      cand[h] = pcand[h];
+      cok[h] = pcok[h];
+      c0[h] = pc0[h];
+      c1[h] = pc1[h];
+      gin_t cq = in + (cok[h] ? (int32_t)cand[h] : (p[h] < loop_end ? p[h] : 0));
+      csh[h] = (uint32_t)(reinterpret_cast<uintptr_t>(cq) & 3);
+      if (palt[h] && (v[h] ^ funnel(c0[h], c1[h], csh[h])) != 0) {
         cand[h] -= 65536u;
-        cw[h] -= 16384;
-        c0[h] = a20[h];
-        c1[h] = a21[h];
+        c0[h] = pa20[h];
+        c1[h] = pa21[h];
       }
     }
+    // ---- match ends by RUNS (the records are those of a 60-byte compare at every position) ----
+    // E(q) = the first position >= q where in[x] != in[x - d(q)].  If q - 1 has the same distance
+    // and its first four bytes match, E(q) = E(q - 1): a RUN of such positions shares one E, which
+    // the run's LAST position determines -- from its first word when that mismatches (then it
+    // ends the run), else by a 60-byte compare.  On T's smooth plane a tile holds ~23 runs, ~18 of
+    // them needing the compare: one compacted 64-lane compare per tile instead of 128 lanes' worth,
+    // and every position of a run whose end is known learns its exact length, past 60 bytes too
+    // (up to the record's 126), which the parser would otherwise extend from memory.
+    const int32_t P = t * kFastTile;
+    uint32_t dd[2];
+    int32_t mm0[2];
+    bool zq[2];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const uint32_t x0 = v[h] ^ funnel(c0[h], c1[h], csh[h]);
-      int32_t mm;
-      if (__ballot(cok[h] && x0 == 0) == 0) {
-        mm = x0 ? (int32_t)(__builtin_ctz(x0) >> 3) : 4;
-      } else {
-        RawCmp a;
-        uint32_t c[kCmpWords + 1];
-        a.d[0] = a0[h][0];
-        a.d[1] = a0[h][1];
-        a.sh = ash[h];
-        c[0] = c0[h];
-        c[1] = c1[h];
-        const B2H_GLB uint32_t* aw = align4(in + (valid[h] ? p[h] : 0));
+      zq[h] = cok[h] && x0 == 0;
+      mm0[h] = x0 ? (int32_t)(__builtin_ctz(x0) >> 3) : 4;
+      dd[h] = cok[h] ? (uint32_t)(p[h] - (int32_t)cand[h]) : 0u;
+    }
+    const uint64_t zm0 = __ballot(zq[0]), zm1 = __ballot(zq[1]);
+    const uint32_t d63 = (uint32_t)__builtin_amdgcn_readlane((int)dd[0], 63);
+    uint64_t sm[2];
 #pragma unroll
-        for (int i = 2; i < kCmpWords + 1; i++) {
-          c[i] = cw[h][i];
-          a.d[i] = aw[i];
-        }
-        mm = kCmpBytes;
+    for (int h = 0; h < 2; h++) {
+      // the previous position's distance and first-word verdict (tile position 0: none)
+      const uint32_t dprev = (uint32_t)__builtin_amdgcn_update_dpp((int)(h ? d63 : 0xffffffffu), (int)dd[h], 0x138, 0xf, 0xf, false);
+      const uint64_t zmh = h ? zm1 : zm0;
+      const bool zprev = lane > 0 ? ((zmh >> (lane - 1)) & 1ull) != 0 : (h == 1 && (zm0 >> 63) != 0);
+      sm[h] = __ballot(cok[h] && zprev && dprev == dd[h]);
+    }
+    // run ends (the successor does not continue the run; tile position 127 always ends one) and
+    // the compare points among them (first four bytes equal)
+    const uint64_t em0 = ~((sm[0] >> 1) | (sm[1] << 63)), em1 = ~(sm[1] >> 1);
+    const uint64_t cp0 = em0 & zm0, cp1 = em1 & zm1;
+    const int32_t n0 = __builtin_popcountll(cp0), ncp = n0 + __builtin_popcountll(cp1);
+    B2H_LDS uint32_t* scr = sh->rec[slot];   // scratch until the records are written
 #pragma unroll
-        for (int i = kCmpWords - 1; i >= 1; i--) {
-          const uint32_t x = rawc_word(a, i) ^ funnel(c[i], c[i + 1], csh[h]);
-          if (x) mm = 4 * i + (__builtin_ctz(x) >> 3);
-        }
-        if (x0) mm = (int32_t)(__builtin_ctz(x0) >> 3);
+    for (int h = 0; h < 2; h++) {
+      const uint64_t cpm = h ? cp1 : cp0;
+      if ((cpm >> lane) & 1ull) {
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(cpm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cpm, 0u));
+        scr[(h ? n0 : 0) + (int32_t)below] = (uint32_t)(h * kHalf + lane) | (dd[h] << 8);
       }
-      const uint32_t d = cok[h] ? (uint32_t)(p[h] - (int32_t)cand[h]) : 0u;
-      const int32_t e = min(mm < kCmpBytes ? p[h] + mm + 1 : 0x7fffffff, bound);
+    }
+    uint32_t ent[2] = {0u, 0u};
+    if (ncp > 0) {
+      ent[0] = lane < ncp ? scr[lane] : 0u;
+      if (ncp > kHalf) ent[1] = lane + kHalf < ncp ? scr[lane + kHalf] : 0u;
+    }
+    int32_t mmc[2] = {0, 0};
+#pragma unroll
+    for (int g = 0; g < 2; g++) {
+      if (g == 1 && ncp <= kHalf) break;
+      if (g == 0 && ncp == 0) break;
+      const bool act = lane + g * kHalf < ncp;
+      const int32_t pq = P + (int32_t)(ent[g] & 0xffu);
+      const int32_t cqp = pq - (int32_t)(ent[g] >> 8);
+      gin_t aq = in + (act ? pq : 0), cq = in + (act ? cqp : 0);
+      const B2H_GLB uint32_t* awp = align4(aq);
+      const B2H_GLB uint32_t* cwp = align4(cq);
+      RawCmp a;
+      uint32_t c[kCmpWords + 1];
+      a.sh = (uint32_t)(reinterpret_cast<uintptr_t>(aq) & 3);
+      const uint32_t sc = (uint32_t)(reinterpret_cast<uintptr_t>(cq) & 3);
+#pragma unroll
+      for (int i = 0; i < kCmpWords + 1; i++) {
+        a.d[i] = awp[i];
+        c[i] = cwp[i];
+      }
+      int32_t mm = kCmpBytes;
+#pragma unroll
+      for (int i = kCmpWords - 1; i >= 1; i--) {   // word 0 is equal at every compare point
+        const uint32_t x = rawc_word(a, i) ^ funnel(c[i], c[i + 1], sc);
+        if (x) mm = 4 * i + (__builtin_ctz(x) >> 3);
+      }
+      mmc[g] = mm;
+    }
+    // each run end's verdict at its position: compared, or its first word
+    if (ncp > 0) {
+      if (lane < ncp) scr[ent[0] & 0xffu] = (uint32_t)mmc[0];
+      if (ncp > kHalf && lane + kHalf < ncp) scr[ent[1] & 0xffu] = (uint32_t)mmc[1];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint64_t em = h ? em1 : em0, cpm = h ? cp1 : cp0;
+      if (((em & ~cpm) >> lane) & 1ull) scr[h * kHalf + lane] = (uint32_t)mm0[h];
+    }
+    // every position reads its run's end (the first run end at or after it)
+    int32_t k[2], mk[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint64_t rem = (h ? em1 : em0) >> lane;
+      k[h] = rem ? h * kHalf + lane + (int32_t)__builtin_ctzll(rem) : kHalf + (int32_t)__builtin_ctzll(em1);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) mk[h] = (int32_t)scr[k[h]];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int32_t q = h * kHalf + lane;
+      const bool ex = mk[h] < kCmpBytes;                 // E = P + k + mk exactly
+      const int32_t mm = ex ? k[h] + mk[h] - q : kCmpBytes;   // (>= kCmpBytes: exact, or "at least")
+      const uint32_t d = dd[h];
+      const int32_t e = min(ex ? p[h] + mm + 1 : 0x7fffffff, bound);
       const int32_t len = e - 4 - p[h];
-      const bool acc = cok[h] && mm >= 4 && len >= 4 && (PROBE || !(len <= 5 && d - 1 >= kLzNear));
-      const bool known = mm < kCmpBytes || p[h] + kCmpBytes + 1 >= bound;
-      sh->rec[slot][h * kHalf + lane] = rec_pack(acc ? (known ? len : kRecLong) : 0, v[h], d);
+      const bool acc = zq[h] && len >= 4 && (PROBE || !(len <= 5 && d - 1 >= kLzNear));
+      const bool known = (ex || p[h] + kCmpBytes + 1 >= bound) && len < kRecLong;
+      scr[q] = rec_pack(acc ? (known ? len : kRecLong) : 0, v[h], d);
     }
   };
 
@@ -339,12 +428,24 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
   int cur = 0, it = 0;
   const bool any = pos < loop_end;
   __syncthreads();                           // table cleared
-  if (any) produce(T, 0);                    // entering T: T and T + 1
+  if (any) {                                 // entering T: T and T + 1
+    ahead(T);
+    finish(0);
+  }
   __syncthreads();
   while (any) {
-    if (pend >= 0) produce(pend, cur ^ 1);               // the parser jumps to `pend`
-    else if ((T + 1) * kFastTile < loop_end) produce(T + 1, cur ^ 1);
+    EPROF_T(tm0);
+    // the tile whose records are due at this step's barrier: the next one, or the jump target
+    const int32_t X = pend >= 0 ? pend : T + 1;
+    if (X * kFastTile < loop_end) {
+      ahead(X);
+      finish(cur ^ 1);
+    }
+    EPROF_T(tm1);
     __syncthreads();
+    EPROF_T(tm2);
+    EPROF_ADD(0, tm0, tm1);
+    EPROF_ADD(4, tm1, tm2);
     if (pend >= 0) {   // the matcher produced the jump target: the parser takes it next
       T = pend;
       cur ^= 1;
@@ -361,6 +462,7 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
       pend = c;
     }
   }
+  EPROF_FLUSH;
 }
 
 // value of per-half variable x[2] at tile position q (0..127), as a wave-uniform value

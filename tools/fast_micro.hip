@@ -75,9 +75,9 @@ int main(int argc, char** argv) {
            r[0].kind, r[0].size, r[0].windows, mean / (r[0].windows ? r[0].windows : 1));
     uint64_t pr[16];
     hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_enc_prof), sizeof pr);
-    const char* nm[8] = {"M: produce", "P: compare", "P: chain walk", "P: emit", "M: barrier", "P: (match ext)", "P: barrier", "-"};
+    const char* nm[8] = {"M: produce", "P: compare", "P: chain walk", "M: exchange", "M: barrier", "P: (match ext)", "P: barrier", "M: 1st words"};
     for (int pass = 1; pass >= 0; pass--)
-      for (int i = 0; i < 7; i++)
+      for (int i = 0; i < 8; i++)
         printf("   %s %-12s %10.0f cycles/stream\n", pass ? "probe" : "main ", nm[i], pr[8 * pass + i] / (double)nblk);
   }
   return 0;

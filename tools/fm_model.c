@@ -13,9 +13,10 @@
  *                   (mode 1 keeps p mod 2^16 per bucket: cand = the latest position below p with
  *                   the bucket's low 16 bits -- the same while p < 2^16)
  *
- * and the parse consumes tiles: entering tile T (the one holding the parse position) it inserts T
- * if no later tile was inserted yet, then T + 1 (the GPU kernel's matcher wave exchanges and
- * compares T + 1 while the parser wave parses T); tiles a long match jumps over are never
+ * and the parse consumes tiles: entering tile T (the one holding the parse position) it inserts
+ * whichever of T, T + 1 are above the highest tile inserted so far, in order (the GPU kernel's
+ * matcher wave exchanges and compares T + 1 while the parser wave parses T; fm_set_ahead(2): T + 2
+ * as well, the kernel built with B2H_FAST_AHEAD=2); tiles a long match jumps over are never
  * inserted.  A
  * candidate is only a suggestion: every match is verified byte for byte and bounded exactly as in
  * the reference, so any stream this produces decodes with blosclz_decompress (blosclz.c:685-795).
@@ -42,6 +43,11 @@ enum { LZ_MAX_COPY = 32, LZ_NEAR = 8191, LZ_FAR = 65535 + 8191 - 1, LZ_SHIFT = 4
 
 static int fm_depth = 1;
 void fm_set_depth(int d) { fm_depth = d < 1 ? 1 : d; }
+/* tiles inserted ahead of the parse (entering T: T .. T + fm_ahead; the kernel's B2H_FAST_AHEAD) */
+static int fm_ahead = 1;
+static int fm_noskip = 0;
+void fm_set_noskip(int v) { fm_noskip = v; }
+void fm_set_ahead(int a) { fm_ahead = a < 1 ? 1 : a; }
 
 static inline uint32_t ld32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
 static inline uint32_t lz_hash(uint32_t seq, int hashlog) { return (seq * 2654435761U) >> (32 - hashlog); }
@@ -119,8 +125,13 @@ static int fm_parse(const uint8_t *in, int32_t length, int tablog, int probe, in
   int fail = 0;
   while (pos < loop_end && !fail) {
     const int32_t T = pos / TILE;
+    if (fm_noskip) {   /* every tile up to T + fm_ahead, jumped over or not, in order */
+      for (int32_t u = hi + 1; u <= T + fm_ahead; u++)
+        if (u * TILE < loop_end) { insert_tile(in, u, loop_end, limit, tablog, tab, prev, cand); hi = u; }
+    }
     if (T > hi) { insert_tile(in, T, loop_end, limit, tablog, tab, prev, cand); hi = T; }
-    if (T + 1 > hi && (T + 1) * TILE < loop_end) { insert_tile(in, T + 1, loop_end, limit, tablog, tab, prev, cand); hi = T + 1; }
+    for (int32_t u = T + 1; u <= T + fm_ahead; u++)
+      if (u > hi && u * TILE < loop_end) { insert_tile(in, u, loop_end, limit, tablog, tab, prev, cand); hi = u; }
     while (pos < loop_end && pos < (T + 1) * TILE) {
       const int32_t anchor = pos;
       const int32_t ref = cand[anchor];
