@@ -263,12 +263,15 @@ __device__ __forceinline__ int32_t wave_match_end(gin_t in, int32_t x, uint32_t 
   }
   while (x < bound) {
     uint32_t a[U][4], b[U][4];
+    // unconditional loads (a lane past `bound` reads the step's first bytes instead, which
+    // first16 ignores): a branch around each slice's loads had the compiler drain every slice
+    // before the next one's issue -- U round trips per step instead of one
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int32_t q = x + u * 1024 + lane * 16;
-#pragma unroll
-      for (int k = 0; k < 4; k++) { a[u][k] = 0; b[u][k] = 0; }
-      if (q < bound) { ld16(in + q, a[u]); ld16(in + q - d, b[u]); }
+      const int32_t ql = q < bound ? q : x;
+      ld16(in + ql, a[u]);
+      ld16(in + ql - d, b[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
