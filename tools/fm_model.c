@@ -46,6 +46,9 @@ void fm_set_depth(int d) { fm_depth = d < 1 ? 1 : d; }
 /* tiles inserted ahead of the parse (entering T: T .. T + fm_ahead; the kernel's B2H_FAST_AHEAD) */
 static int fm_ahead = 1;
 static int fm_noskip = 0;
+/* fast mode's probe window cap (positions; the reference's is 1 << hashlog) */
+static int fm_probe_cap = 1 << 30;
+void fm_set_probe_cap(int c) { fm_probe_cap = c < 64 ? 64 : c; }
 void fm_set_noskip(int v) { fm_noskip = v; }
 void fm_set_ahead(int a) { fm_ahead = a < 1 ? 1 : a; }
 
@@ -237,7 +240,7 @@ int fm_blosclz_compress(int clevel, const uint8_t *in, int length, uint8_t *out,
   else if (clevel < 4) maxlen /= 4;
   else if (clevel < 7) maxlen /= 2;
   double ratio = 0.0;
-  fm_parse(in + (length - maxlen), maxlen, tablog, 1, 1 << hashlog, NULL, 0, &ratio);
+  fm_parse(in + (length - maxlen), maxlen, tablog, 1, (1 << hashlog) < fm_probe_cap ? (1 << hashlog) : fm_probe_cap, NULL, 0, &ratio);
   if (ratio < min_ratio[clevel] || length < 16 || maxout < 66) return 0;
   return fm_parse(in, length, tablog, 0, 0, out, maxout, NULL);
 }
