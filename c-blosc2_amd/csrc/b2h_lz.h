@@ -1023,6 +1023,7 @@ __device__ __noinline__ int32_t copy_general(B2H_LDS uint8_t* ring, gout_t out, 
         const int32_t n = vec_from - done;
         while (op + done + n - F > R) { ring_flush<RLOG>(ring, out, F, F + PIECE); F += PIECE; }
         if (src < F) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        r = (done + lane) % dist;
         for (int32_t i = done + lane; i < done + n; i += 64) {
           const int32_t y = src + r;
           ring[(op + i) & RM] = y >= F ? ring[y & RM] : out[y];
@@ -1047,7 +1048,29 @@ __device__ __noinline__ int32_t copy_general(B2H_LDS uint8_t* ring, gout_t out, 
     }
     const int32_t n = min(len - done, STEP);
     while (op + done + n - F > R) { ring_flush<RLOG>(ring, out, F, F + PIECE); F += PIECE; }
+    // a ring-resident source in slabs of S <= dist bytes (S = the chunk when the copy does not
+    // overlap): within a slab every source byte precedes the slab, so all its reads go out before
+    // its writes -- one LDS round trip per slab instead of one per 64 bytes (C4's delta planes:
+    // runs of 255-511-byte matches at distance 256 / 512)
+    const int32_t S = overlap ? (dist >= 64 ? min(dist & ~63, STEP) : 0) : STEP;
+    if (S > 0 && src + done >= F) {
+      for (int32_t sub = done; sub < done + n; sub += S) {
+        const int32_t m = min(S, done + n - sub);
+        uint8_t b[16];
+#pragma unroll
+        for (int k = 0; k < 4; k++) b[k] = ring[(src + sub + lane + 64 * k) & RM];
+        if (m > 256) {
+#pragma unroll
+          for (int k = 4; k < 16; k++) b[k] = ring[(src + sub + lane + 64 * k) & RM];
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+          if (lane + 64 * k < m) ring[(op + sub + lane + 64 * k) & RM] = b[k];
+      }
+      continue;
+    }
     if (src < F) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    r = overlap ? (done + lane) % dist : 0;
     for (int32_t i = done + lane; i < done + n; i += 64) {
       const int32_t y = overlap ? src + r : src + i;
       const uint8_t b = y >= F ? ring[y & RM] : (y >= 0 ? out[y] : dict[dsz + y]);
