@@ -333,6 +333,12 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
       dd[h] = cok[h] ? (uint32_t)(p[h] - (int32_t)cand[h]) : 0u;
     }
     const uint64_t zm0 = __ballot(zq[0]), zm1 = __ballot(zq[1]);
+    B2H_LDS uint32_t* scr = sh->rec[slot];   // scratch until the records are written
+    if ((zm0 | zm1) == 0) {   // no position's first four bytes match (incompressible tiles): no match
+#pragma unroll
+      for (int h = 0; h < 2; h++) scr[h * kHalf + lane] = rec_pack(0, v[h], dd[h]);
+      return;
+    }
     const uint32_t d63 = (uint32_t)__builtin_amdgcn_readlane((int)dd[0], 63);
     uint64_t sm[2];
 #pragma unroll
@@ -348,7 +354,6 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
     const uint64_t em0 = ~((sm[0] >> 1) | (sm[1] << 63)), em1 = ~(sm[1] >> 1);
     const uint64_t cp0 = em0 & zm0, cp1 = em1 & zm1;
     const int32_t n0 = __builtin_popcountll(cp0), ncp = n0 + __builtin_popcountll(cp1);
-    B2H_LDS uint32_t* scr = sh->rec[slot];   // scratch until the records are written
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const uint64_t cpm = h ? cp1 : cp0;
@@ -390,25 +395,30 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
       }
       mmc[g] = mm;
     }
-    // each run end's verdict at its position: compared, or its first word
-    if (ncp > 0) {
-      if (lane < ncp) scr[ent[0] & 0xffu] = (uint32_t)mmc[0];
-      if (ncp > kHalf && lane + kHalf < ncp) scr[ent[1] & 0xffu] = (uint32_t)mmc[1];
-    }
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const uint64_t em = h ? em1 : em0, cpm = h ? cp1 : cp0;
-      if (((em & ~cpm) >> lane) & 1ull) scr[h * kHalf + lane] = (uint32_t)mm0[h];
-    }
-    // every position reads its run's end (the first run end at or after it)
+    // every position reads its run's end (the first run end at or after it): through LDS, unless
+    // every position ends its own run and none needed the compare (incompressible tiles: each
+    // position's verdict is its own first word)
     int32_t k[2], mk[2];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const uint64_t rem = (h ? em1 : em0) >> lane;
       k[h] = rem ? h * kHalf + lane + (int32_t)__builtin_ctzll(rem) : kHalf + (int32_t)__builtin_ctzll(em1);
+      mk[h] = mm0[h];
     }
+    if (ncp > 0 || (em0 & em1) != ~0ull) {
+      // each run end's verdict at its position: compared, or its first word
+      if (ncp > 0) {
+        if (lane < ncp) scr[ent[0] & 0xffu] = (uint32_t)mmc[0];
+        if (ncp > kHalf && lane + kHalf < ncp) scr[ent[1] & 0xffu] = (uint32_t)mmc[1];
+      }
 #pragma unroll
-    for (int h = 0; h < 2; h++) mk[h] = (int32_t)scr[k[h]];
+      for (int h = 0; h < 2; h++) {
+        const uint64_t em = h ? em1 : em0, cpm = h ? cp1 : cp0;
+        if (((em & ~cpm) >> lane) & 1ull) scr[h * kHalf + lane] = (uint32_t)mm0[h];
+      }
+#pragma unroll
+      for (int h = 0; h < 2; h++) mk[h] = (int32_t)scr[k[h]];
+    }
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const int32_t q = h * kHalf + lane;
