@@ -37,6 +37,9 @@ namespace b2h {
 // measured 1 600 of 3 100 cycles per 64-position step on T's smooth plane, the chain walk the
 // rest), so both halves go through the same instructions and their chains overlap.
 constexpr int kFastTile = 128, kHalf = 64;
+#ifndef B2H_PASS_PRIO
+#define B2H_PASS_PRIO 1   // 1: issue priority to the probe's matcher and the emitting pass's parser
+#endif
 
 // Table exchange of 64 positions: the lanes with p < loop_end hash in[p..p+3] (v) and swap p into
 // the bucket.  Returns the candidate (the bucket's previous position; 0 for an empty bucket).
@@ -66,6 +69,37 @@ __device__ __forceinline__ uint32_t fast_exchange(uint32_t v, int32_t p, bool va
     }
   }
   return old;
+}
+
+// Both halves of a tile in one round trip (u16 buckets): the two ds_mskor_rtn_b32 go out back to
+// back -- a wave's LDS instructions execute in order, so half 1's exchange still sees half 0's --
+// and one wait covers both.  A lane past loop_end exchanges with an empty mask (a no-op).
+template <typename POS>
+__device__ __forceinline__ void fast_exchange2(const uint32_t (&v)[2], const int32_t (&p)[2], const bool (&valid)[2],
+                                               int tablog, B2H_LDS uint8_t* tab, uint32_t (&cand)[2]) {
+  if constexpr (sizeof(POS) == 4) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) cand[h] = fast_exchange<POS>(v[h], p[h], valid[h], tablog, tab);
+  } else {
+    uint32_t addr[2], mask[2], data[2], sh[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint32_t hh = lz_hash(v[h], tablog);
+      addr[h] = (uint32_t)reinterpret_cast<uintptr_t>(tab) + ((hh >> 1) << 2);
+      sh[h] = (hh & 1u) << 4;
+      mask[h] = valid[h] ? 0xffffu << sh[h] : 0u;
+      data[h] = valid[h] ? ((uint32_t)p[h] & 0xffffu) << sh[h] : 0u;
+    }
+    uint32_t w0, w1;
+    asm volatile("ds_mskor_rtn_b32 %0, %2, %3, %4\n\tds_mskor_rtn_b32 %1, %5, %6, %7\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(w0), "=&v"(w1)
+                 : "v"(addr[0]), "v"(mask[0]), "v"(data[0]), "v"(addr[1]), "v"(mask[1]), "v"(data[1])
+                 : "memory");
+    const uint32_t w[2] = {w0, w1};
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+      cand[h] = valid[h] ? (uint32_t)p[h] - (((uint32_t)p[h] - ((w[h] >> sh[h]) & 0xffffu)) & 0xffffu) : 0u;
+  }
 }
 
 constexpr int kDeepDepth = 8, kDeepSel = 24;
@@ -260,11 +294,9 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
       valid[h] = p[h] < loop_end;
       pv[h] = funnel(a0[h][0], a0[h][1], ash[h]);
     }
+    fast_exchange2<POS>(pv, p, valid, tablog, tab, cand);   // in order: half 1's positions follow half 0's
 #pragma unroll
-    for (int h = 0; h < 2; h++) {   // in order: half 1's positions follow half 0's
-      cand[h] = fast_exchange<POS>(pv[h], p[h], valid[h], tablog, tab);
-      cok[h] = fast_cand_ok(p[h], cand[h], valid[h]);
-    }
+    for (int h = 0; h < 2; h++) cok[h] = fast_cand_ok(p[h], cand[h], valid[h]);
     if constexpr (DEEP) deep_select(t, p, valid, a0, ash, cand, cok);
     // every position's candidate words 0..1 (its first four bytes); lanes without a candidate load
     // their own bytes
@@ -924,6 +956,11 @@ __device__ __forceinline__ StreamResult encode_stream_fast(gin_t __restrict__ in
   if (clevel < 2) maxlen /= 8;
   else if (clevel < 4) maxlen /= 4;
   else if (clevel < 7) maxlen /= 2;
+#if B2H_PASS_PRIO
+  // the probe's critical wave is the matcher (few elements per tile to walk), the emitting
+  // pass's the parser: the wave on the chain issues first on its SIMD
+  if (matcher) __builtin_amdgcn_s_setprio(2); else __builtin_amdgcn_s_setprio(0);
+#endif
   const LzPassOut pr = lz_pass_fast<true, POS, WT, DEEP>(in + (n - maxlen), maxlen, hashlog, tl, out, 0, tab, oring, sh,
                                                       clevel, matcher, chain);
   res.windows = pr.windows;
@@ -934,6 +971,9 @@ __device__ __forceinline__ StreamResult encode_stream_fast(gin_t __restrict__ in
   const bool go = __builtin_amdgcn_readfirstlane(sh->decide[0]) != 0;
   __syncthreads();
   if (!go) return res;
+#if B2H_PASS_PRIO
+  if (matcher) __builtin_amdgcn_s_setprio(0); else __builtin_amdgcn_s_setprio(2);
+#endif
   const LzPassOut em = lz_pass_fast<false, POS, WT, DEEP>(in, n, hashlog, tl, out, n, tab, oring, sh, clevel, matcher, chain);
   res.windows += em.windows;
   if (em.fail) return res;
