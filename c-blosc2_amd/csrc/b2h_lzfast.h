@@ -37,6 +37,10 @@ namespace b2h {
 // measured 1 600 of 3 100 cycles per 64-position step on T's smooth plane, the chain walk the
 // rest), so both halves go through the same instructions and their chains overlap.
 constexpr int kFastTile = 128, kHalf = 64;
+#ifndef B2H_PROBE_AHEAD
+#define B2H_PROBE_AHEAD 0   // 1: the probe's matcher inserts T + 2 while the parser is on T (measured slower)
+#endif
+constexpr bool kProbeAhead = B2H_PROBE_AHEAD != 0;
 #ifndef B2H_PASS_PRIO
 #define B2H_PASS_PRIO 1   // 1: issue priority to the probe's matcher and the emitting pass's parser
 #endif
@@ -469,10 +473,17 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
   int32_t T = pos / kFastTile, pend = -1;
   int cur = 0, it = 0;
   const bool any = pos < loop_end;
+  // B2H_PROBE_AHEAD: the probe's matcher -- its critical wave -- inserting one tile further ahead,
+  // so AHEAD(t + 1)'s candidate loads land across the barrier (tools/fm_model.c
+  // fm_set_ahead_probe(2)); same-box A/B T 209.6 -> 207.6 GiB/s, off
+  constexpr bool LA = PROBE && kProbeAhead;
+  int32_t pt = -1, hi = -1;
   __syncthreads();                           // table cleared
   if (any) {                                 // entering T: T and T + 1
     ahead(T);
     finish(0);
+    hi = T;
+    if (LA && (T + 1) * kFastTile < loop_end) { ahead(T + 1); pt = T + 1; hi = T + 1; }
   }
   __syncthreads();
   while (any) {
@@ -480,8 +491,10 @@ __device__ __forceinline__ void lz_pass_fast_matcher(gin_t __restrict__ in, int3
     // the tile whose records are due at this step's barrier: the next one, or the jump target
     const int32_t X = pend >= 0 ? pend : T + 1;
     if (X * kFastTile < loop_end) {
-      ahead(X);
+      if (!LA || pt != X) { ahead(X); hi = X; }
       finish(cur ^ 1);
+      pt = -1;
+      if (LA && (X + 1) * kFastTile < loop_end && X + 1 > hi) { ahead(X + 1); pt = X + 1; hi = X + 1; }
     }
     EPROF_T(tm1);
     __syncthreads();

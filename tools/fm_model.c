@@ -45,6 +45,9 @@ static int fm_depth = 1;
 void fm_set_depth(int d) { fm_depth = d < 1 ? 1 : d; }
 /* tiles inserted ahead of the parse (entering T: T .. T + fm_ahead; the kernel's B2H_FAST_AHEAD) */
 static int fm_ahead = 1;
+/* the probe pass's (2: the kernel built with B2H_PROBE_AHEAD=1) */
+static int fm_ahead_probe = 1;
+void fm_set_ahead_probe(int a) { fm_ahead_probe = a < 1 ? 1 : a; }
 static int fm_noskip = 0;
 /* fast mode's probe window cap (positions; the reference's is 1 << hashlog) */
 static int fm_probe_cap = 1 << 30;
@@ -129,11 +132,11 @@ static int fm_parse(const uint8_t *in, int32_t length, int tablog, int probe, in
   while (pos < loop_end && !fail) {
     const int32_t T = pos / TILE;
     if (fm_noskip) {   /* every tile up to T + fm_ahead, jumped over or not, in order */
-      for (int32_t u = hi + 1; u <= T + fm_ahead; u++)
+      for (int32_t u = hi + 1; u <= T + (probe ? fm_ahead_probe : fm_ahead); u++)
         if (u * TILE < loop_end) { insert_tile(in, u, loop_end, limit, tablog, tab, prev, cand); hi = u; }
     }
     if (T > hi) { insert_tile(in, T, loop_end, limit, tablog, tab, prev, cand); hi = T; }
-    for (int32_t u = T + 1; u <= T + fm_ahead; u++)
+    for (int32_t u = T + 1; u <= T + (probe ? fm_ahead_probe : fm_ahead); u++)
       if (u > hi && u * TILE < loop_end) { insert_tile(in, u, loop_end, limit, tablog, tab, prev, cand); hi = u; }
     while (pos < loop_end && pos < (T + 1) * TILE) {
       const int32_t anchor = pos;
