@@ -674,12 +674,13 @@ __device__ __forceinline__ LzPassOut lz_pass_fast_parser(gin_t __restrict__ in, 
         const int32_t s0 = pos - P;
         const int32_t lim = min(kFastTile, loop_end - P);
         int32_t dist[2], lenx[2];
-        uint32_t vbyte[2];
+        uint32_t vbyte[2], wrec[2];
         uint64_t am[2];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
           const int32_t q = h * kHalf + lane;
           const uint32_t w = sh->rec[cur][q];
+          wrec[h] = w;
           const int32_t L = rec_len(w);
           vbyte[h] = rec_byte(w);
           dist[h] = (int32_t)rec_dist(w);
@@ -753,8 +754,11 @@ __device__ __forceinline__ LzPassOut lz_pass_fast_parser(gin_t __restrict__ in, 
             uint64_t rem = c > h * kHalf ? am[h] & (~0ull << (c - h * kHalf)) : am[h];
             while (rem) {
               const int32_t m = h * kHalf + __builtin_ctzll(rem);
-              int32_t lm = rdlane(lenx[h], m - h * kHalf);
-              if (lm < 0) {
+              // the element's whole record in one readlane: length and distance unpacked on the
+              // scalar side
+              const uint32_t wm = (uint32_t)rdlane((int32_t)wrec[h], m - h * kHalf);
+              int32_t lm = rec_len(wm);
+              if (lm == kRecLong) {
                 EPROF_T(te0);
                 lm = fast_match_len(m, lenx, dist, P, bound, in);
                 EPROF_T(te1);
@@ -762,7 +766,7 @@ __device__ __forceinline__ LzPassOut lz_pass_fast_parser(gin_t __restrict__ in, 
               }
               if (lm >= 262) { ser = m; ser_len = lm; break; }
               if (m > c) emit_lits(c, m);
-              emit_token(lm, (uint32_t)rdlane(dist[h], m - h * kHalf));
+              emit_token(lm, rec_dist(wm));
               c = m + lm + 2;
               endc2 = c;
               if (c >= (h + 1) * kHalf) break;
