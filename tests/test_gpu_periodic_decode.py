@@ -65,3 +65,23 @@ def test_gpu_periodic_long_matches():
     back = dout.cpu().numpy()
     for i, r in enumerate(raws):
         assert np.array_equal(back[i * dstride:i * dstride + nbytes], r), i
+
+
+@pytest.mark.parametrize("mode", ["exact", "fast"])
+def test_gpu_periodic_long_match_encode(mode):
+    """The encoders' match extension over the same data (b2h_lz.h wave_match_end: 4 KiB steps in
+    one round trip, lanes past the bound reading the step's first bytes): exact-mode chunks are
+    the oracle's byte for byte; fast-mode chunks decode with the oracle to the input."""
+    import blosc2_amd as B
+    from oracle_lib import oracle_compress, oracle_decompress
+    nbytes = 256 * 1024 - 37
+    kw = dict(clevel=9, typesize=1, filters=(0, 0, 0, 0, 0, 0), blocksize=256 * 1024)
+    for i, period in enumerate(PERIODS):
+        for prefix in (0, 13):
+            raw = _periodic(period, prefix, nbytes, 7 * i + prefix)
+            c = B.compress(raw, lz_mode=B.EXACT if mode == "exact" else B.FAST, **kw)
+            assert isinstance(c, np.ndarray), (period, prefix)
+            if mode == "exact":
+                want = oracle_compress(raw, **kw)
+                assert np.array_equal(c, want), (period, prefix)
+            assert np.array_equal(oracle_decompress(c, nbytes), raw), (period, prefix)
