@@ -1220,12 +1220,31 @@ __device__ __noinline__ int32_t ring_put(B2H_LDS uint8_t* ring, gout_t out, int3
 // copied by 64 lanes through the ring.  Returns decoded bytes, or -1.
 // `dict` / `dsz`: the chunk's dictionary (BLOSC2_USEDICT, blosc/blosc2.c:504-508), matches may
 // reach dsz bytes before the output start.
+__device__ __forceinline__ uint32_t win_dword(const InWin& W, int32_t q);
+#ifndef B2H_LZ4_PAR
+#define B2H_LZ4_PAR 1
+#endif
+// (noinline: the LZ4 batch's registers would otherwise count against the BloscLZ decoder's
+// 96-VGPR budget in k_decode -- 4 spills inlined)
 template <int RLOG>
-__device__ __forceinline__ int32_t wave_lz4_decode_ring(gin_t in, int32_t length, gout_t out, int32_t maxout,
+__device__ __noinline__ int32_t wave_lz4_decode_ring(gin_t in, int32_t length, gout_t out, int32_t maxout,
                                                         B2H_LDS uint8_t* ring, gin_t dict = nullptr, int32_t dsz = 0) {
   constexpr int32_t R = 1 << RLOG, RM = R - 1;
   constexpr int32_t kMfLimit = 12, kLastLit = 5;
+  constexpr int32_t WMAX = R - ring_piece(RLOG) < 8192 ? R - ring_piece(RLOG) : 8192;
   const int lane = lane_id();
+  // (a call's arguments arrive in VGPRs: make the wave-uniform ones scalar again)
+  auto upt = [](const void* q) -> uint64_t {
+    const uint64_t a = reinterpret_cast<uintptr_t>(q);
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
+  };
+  in = (gin_t)upt((const void*)in);
+  out = (gout_t)upt((const void*)out);
+  dict = (gin_t)upt((const void*)dict);
+  length = __builtin_amdgcn_readfirstlane(length);
+  maxout = __builtin_amdgcn_readfirstlane(maxout);
+  dsz = __builtin_amdgcn_readfirstlane(dsz);
   if (length <= 0) return -1;
   if (maxout == 0) return (length == 1 && in[0] == 0) ? 0 : -1;
   InWin W;
@@ -1233,6 +1252,118 @@ __device__ __forceinline__ int32_t wave_lz4_decode_ring(gin_t in, int32_t length
   int32_t ip = 0, op = 0, F = 0;
   asm volatile("" : "+s"(ip), "+s"(W.wpos));
   for (;;) {
+#if B2H_LZ4_PAR
+    // ---- window-parallel batch (as wave_lz_decode_par): every lane parses the sequence that would
+    // start at its byte; the true chain from ip is walked; sequences with extension bytes, the
+    // last (literals-only) sequence and any bound or offset the serial code rejects or treats
+    // specially (offset 0, a dictionary source) end the batch and go through the serial code
+    // below, one at a time.  Batched: <= 14 literals, matches with at most one extension byte.
+    {
+      const int32_t k = inwin_seek(W, in, length, ip);
+      const int32_t P = ip + lane;
+      const uint32_t lo32 = win_dword(W, k + lane);
+      const uint32_t t = lo32 & 0xffu;
+      const int32_t L = (int32_t)(t >> 4), M0 = (int32_t)(t & 15u);
+      const uint32_t offw = win_dword(W, k + lane + 1 + L);   // offset (2 bytes) + a match extension byte
+      const int32_t off = (int32_t)(offw & 0xffffu);
+      const int32_t mx = (int32_t)((offw >> 16) & 0xffu);
+      const bool mext = M0 == 15;                  // one extension byte (< 255) is taken in the batch
+      const int32_t M = M0 + (mext ? mx : 0);
+      const int32_t size = 1 + L + 2 + (mext ? 1 : 0), olen = L + M + 4;
+      const bool special = L == 15 || (mext && mx == 255) || P + 1 + L > length - (2 + 1 + kLastLit);
+      const int32_t step = special ? 128 : size;
+      uint64_t chain = 0;
+      int32_t sw = 0;
+      do {
+        chain |= 1ull << sw;
+        sw += __builtin_amdgcn_readlane(step, sw);
+      } while (sw < 64);
+      const uint64_t spec = chain & __ballot(special);
+      int32_t st = spec ? __builtin_ctzll(spec) : 64;
+      uint64_t batch = chain & (st < 64 ? (1ull << st) - 1 : ~0ull);
+      const bool inb = (batch >> lane) & 1ull;
+      const int32_t v = inb ? olen : 0;
+      const int32_t ex = wave_scan_add(v) - v;   // output offset of the lane's sequence - op
+      const int32_t ol = op + ex + L;            // its match's output position
+      const bool viol = inb && (op + ex + L > maxout - kMfLimit || off == 0 || off > ol ||
+                                ol + M + 4 > maxout - kLastLit || ex + olen > WMAX);
+      const uint64_t vm = __ballot(viol);
+      if (vm) {
+        st = min(st, (int32_t)__builtin_ctzll(vm));
+        batch &= (1ull << __builtin_ctzll(vm)) - 1;
+      }
+      if (batch) {
+        const int32_t last = 63 - __builtin_clzll(batch);
+        const int32_t nip = ip + (st < 64 ? st : sw);
+        const int32_t nop = op + __builtin_amdgcn_readlane(ex + v, last);
+        if (nop - F > R) F = flush_to<RLOG>(ring, out, nop, F);
+        // literal bytes: byte lane x belongs to the last batch sequence j <= x, a literal when
+        // j < x <= j + L_j; the last sequence's literals may run past the 64 parsed bytes
+        const bool inbt = (batch >> lane) & 1ull;
+        const int32_t owner = wave_scan_max(inbt ? lane : -1);
+        const uint32_t opk = (uint32_t)(ex << 6) | (uint32_t)L;   // ex < 2^13, L <= 14
+        const uint32_t ow_pk = (uint32_t)__shfl((int)opk, owner & 63);
+        const int32_t oL = (int32_t)(ow_pk & 63u), oex = (int32_t)(ow_pk >> 6);
+        if (owner >= 0 && lane > owner && lane <= owner + oL)
+          ring[(op + oex + (lane - owner - 1)) & RM] = (uint8_t)t;   // t = the byte at ip + lane
+        const uint32_t last_pk = (uint32_t)__builtin_amdgcn_readlane((int)opk, last);
+        const int32_t lL = (int32_t)(last_pk & 63u);
+        if (last + lL >= 64) {
+          const int32_t x = 64 + lane;
+          const uint32_t byte = win_dword(W, k + x) & 0xffu;
+          if (x <= last + lL) ring[(op + (int32_t)(last_pk >> 6) + (x - last - 1)) & RM] = (uint8_t)byte;
+        }
+        // matches: sources wholly before the batch (<= 64 bytes) eight at a time, reads before
+        // writes; the others in order after
+        const int32_t ml = M + 4;
+        const int32_t srcv = ol - off;
+        const bool indep = inbt && ml <= 64 && off >= ex + L + ml && (srcv >= F || srcv + ml <= F);
+        uint64_t im = __ballot(indep);
+        if (__ballot(indep && srcv < F)) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        while (im) {
+          int32_t oj[8], lj[8], sj[8];
+          uint8_t vb[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            lj[u] = 0;
+            oj[u] = 0;
+            sj[u] = 0;
+            if (im) {
+              const int j = __builtin_ctzll(im);
+              im &= im - 1;
+              oj[u] = __builtin_amdgcn_readlane(ol, j);
+              lj[u] = __builtin_amdgcn_readlane(ml, j);
+              sj[u] = oj[u] - __builtin_amdgcn_readlane(off, j);
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 8; u++)
+            vb[u] = lane < lj[u] ? (sj[u] >= F ? ring[(sj[u] + lane) & RM] : out[sj[u] + lane]) : (uint8_t)0;
+#pragma unroll
+          for (int u = 0; u < 8; u++)
+            if (lane < lj[u]) ring[(oj[u] + lane) & RM] = vb[u];
+        }
+        uint64_t mm = batch & ~__ballot(indep);
+        while (mm) {
+          const int j = __builtin_ctzll(mm);
+          mm &= mm - 1;
+          const int32_t oj = __builtin_amdgcn_readlane(ol, j);
+          const int32_t lj = __builtin_amdgcn_readlane(ml, j);
+          const int32_t dj = __builtin_amdgcn_readlane(off, j);
+          const int32_t src = oj - dj;
+          if (lj <= 64 && src >= F) {
+            const int32_t yl = dj < lj ? lane % dj : lane;
+            if (lane < lj) ring[(oj + lane) & RM] = ring[(src + yl) & RM];
+          } else {
+            F = copy_general<RLOG>(ring, out, oj, src, lj, dj, F, dict, dsz);
+          }
+        }
+        ip = nip;
+        op = nop;
+      }
+      if (st >= 64) continue;
+    }
+#endif
     if (ip >= length) return -1;
     const uint32_t token = inwin_byte(W, in, length, ip++);
     int32_t lit = (int32_t)(token >> 4);
