@@ -416,7 +416,7 @@ def lz4t(steps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="C1,C2,C3,C4,E2E")
+    ap.add_argument("--only", default="C1,C2,C3,C4,E2E,LZ4")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--lz-mode", default="exact", choices=["exact", "fast", "deep"])
     args = ap.parse_args()
