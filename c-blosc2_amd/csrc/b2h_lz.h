@@ -709,49 +709,42 @@ __device__ __forceinline__ LzPassOut lz_pass(gin_t __restrict__ in, int32_t leng
   return r;
 }
 
-// Is the whole stream one repeated byte? (blosc/blosc2.c:1184-1206)  4 KiB per step.
-__device__ __forceinline__ bool wave_is_run(gin_t s, int32_t n) {
+// Whether s[from, n) is all `first`: 4 KiB per step (64 lanes x 4 x 16 B).  A whole aligned step
+// issues its four slices' loads unconditionally -- one round trip; under a branch per slice the
+// compiler drained each slice before the next one's issue (four round trips per step)
+__device__ __forceinline__ bool wave_run_span(gin_t s, int32_t from, int32_t n, uint8_t first) {
   const int lane = lane_id();
-  const uint8_t first = s[0];
   const uint32_t rep = first * 0x01010101u;
-  const bool aligned = (reinterpret_cast<uintptr_t>(s) & 15) == 0;
-  for (int32_t base = 0; base < n; base += 64 * 64) {
+  const bool aligned = (reinterpret_cast<uintptr_t>(s + from) & 15) == 0;
+  for (int32_t base = from; base < n; base += 64 * 64) {
     bool bad = false;
+    if (aligned && base + 64 * 64 <= n) {
+      u32x4 w[4];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int32_t i = base + (u * 64 + lane) * 16;
-      if (aligned && i + 16 <= n) {
-        const B2H_GLB uint32_t* w = reinterpret_cast<const B2H_GLB uint32_t*>(s + i);
-        bad |= (w[0] != rep) | (w[1] != rep) | (w[2] != rep) | (w[3] != rep);
-      } else {
-        for (int32_t k = i; k < min(i + 16, n); k++) bad |= s[k] != first;
+      for (int u = 0; u < 4; u++) w[u] = *reinterpret_cast<const B2H_GLB u32x4*>(s + base + (u * 64 + lane) * 16);
+#pragma unroll
+      for (int u = 0; u < 4; u++) bad |= (w[u].x != rep) | (w[u].y != rep) | (w[u].z != rep) | (w[u].w != rep);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int32_t i = base + (u * 64 + lane) * 16;
+        if (aligned && i + 16 <= n) {
+          const B2H_GLB uint32_t* w = reinterpret_cast<const B2H_GLB uint32_t*>(s + i);
+          bad |= (w[0] != rep) | (w[1] != rep) | (w[2] != rep) | (w[3] != rep);
+        } else {
+          for (int32_t k = i; k < min(i + 16, n); k++) bad |= s[k] != first;
+        }
       }
     }
     if (__ballot(bad)) return false;
   }
   return true;
 }
-
+// Is the whole stream one repeated byte? (blosc/blosc2.c:1184-1206)
+__device__ __forceinline__ bool wave_is_run(gin_t s, int32_t n) { return wave_run_span(s, 0, n, s[0]); }
 // Whether s[from, n) is all `first` (the second half of a split run test).
 __device__ __forceinline__ bool wave_is_run_from(gin_t s, int32_t from, int32_t n, uint8_t first) {
-  const int lane = lane_id();
-  const uint32_t rep = first * 0x01010101u;
-  const bool aligned = (reinterpret_cast<uintptr_t>(s + from) & 15) == 0;
-  for (int32_t base = from; base < n; base += 64 * 64) {
-    bool bad = false;
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int32_t i = base + (u * 64 + lane) * 16;
-      if (aligned && i + 16 <= n) {
-        const B2H_GLB uint32_t* w = reinterpret_cast<const B2H_GLB uint32_t*>(s + i);
-        bad |= (w[0] != rep) | (w[1] != rep) | (w[2] != rep) | (w[3] != rep);
-      } else {
-        for (int32_t k = i; k < min(i + 16, n); k++) bad |= s[k] != first;
-      }
-    }
-    if (__ballot(bad)) return false;
-  }
-  return true;
+  return wave_run_span(s, from, n, first);
 }
 
 // Full per-stream encode with maxout = neblock: run test, entropy probe, main pass.
