@@ -1482,6 +1482,57 @@ __device__ void shuffle4_block_wt(const uint8_t* __restrict__ s, uint8_t* __rest
   }
 }
 
+// shuffle4_block_wt deciding the run verdict on the way, as ds_block_runs does for (DELTA,
+// SHUFFLE) -- but in one pass: every plane is stored and the mismatches against each plane's first
+// byte (byte p of the block's first element) ORed in LDS word `red`.  Returns the run planes; the
+// encoder then skips their streams and the run test of the others.  Whole 64-byte groups (the
+// caller checks); the workgroup calls it together.
+__device__ __noinline__ uint32_t shuffle4_block_runs(const uint8_t* __restrict__ s, uint8_t* __restrict__ d, int32_t bsize,
+                                                     B2H_LDS uint32_t* red) {
+  const int32_t tid = threadIdx.x, nth = blockDim.x;
+  const int32_t n = bsize / 4, groups = n / 16;
+  const __amdgpu_buffer_rsrc_t r = wt_rsrc((gout_t)d);
+  const uint4* s4 = reinterpret_cast<const uint4*>(s);
+  uint32_t rep[4];
+#pragma unroll
+  for (int p = 0; p < 4; p++) rep[p] = 0x01010101u * (uint32_t)s[p];
+  if (tid == 0) *red = 0u;
+  __syncthreads();
+  uint32_t mis = 0;
+  constexpr int U = 2;
+  for (int32_t g0 = tid; g0 < groups; g0 += U * nth) {
+    uint4 w[U][4];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int32_t gi = g0 + u * nth;
+#pragma unroll
+      for (int k = 0; k < 4; k++) w[u][k] = gi < groups ? s4[4 * gi + k] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int32_t gi = g0 + u * nth;
+      if (gi >= groups) break;
+      uint32_t o[4][4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) tr4(w[u][k].x, w[u][k].y, w[u][k].z, w[u][k].w, o[k]);
+#pragma unroll
+      for (int p = 0; p < 4; p++) {
+        const u32x4 v = {o[0][p], o[1][p], o[2][p], o[3][p]};
+        mis |= (((v.x != rep[p]) | (v.y != rep[p]) | (v.z != rep[p]) | (v.w != rep[p])) ? 1u : 0u) << p;
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, p * n + 16 * gi, 0, 16);
+      }
+    }
+  }
+  uint32_t wm = 0;
+#pragma unroll
+  for (int p = 0; p < 4; p++) wm |= __ballot((mis >> p) & 1u) ? (1u << p) : 0u;
+  if ((tid & 63) == 0 && wm) __hip_atomic_fetch_or(red, wm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __syncthreads();
+  const uint32_t M = __builtin_amdgcn_readfirstlane(*red);
+  __syncthreads();
+  return ~M & 15u;
+}
+
 // (DELTA, SHUFFLE) of one block by the workgroup (or one wave: tid / nth), the planes' dwords
 // stored write-through: the fused launch's filter job for k_ffilter_ds's pipeline (the same
 // arithmetic as delta_shuffle_fast: block 0 XORs each element with the previous one, the other
@@ -1647,6 +1698,14 @@ __host__ __device__ constexpr size_t fused_lds(size_t pos_bytes, int tablog) {
 // eight two-wave workgroups per CU (160 KiB of LDS) at the default u16 table
 static_assert(fused_lds(2, 13) <= 160 * 1024 / 8, "fused fast encoder: more than 20 KiB of LDS per workgroup");
 
+// Whether the fused filter job decides the run verdict of a block's streams: a split block (one
+// stream per byte plane) of a chunk with run streams (extended header), the (DELTA, SHUFFLE) job or
+// the 4-byte SHUFFLE one over whole 64-byte groups, not the leftover block, not opted out (bit 128)
+__device__ __forceinline__ bool fuse_verdict(const EncFuse& f, const CGeom& g, bool lo) {
+  if (lo || g.overhead != kHdrExt || (f.mode_bits & 128)) return false;
+  return f.ds ? g.spb == f.ds : (g.spb == 4 && (g.bs & 255) == 0);
+}
+
 #undef FUSE_TRACE_PTR
 #define FUSE_TRACE_PTR lds_uniform(&A->f.trace)
 #ifndef B2H_FAST_WPE
@@ -1771,6 +1830,7 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
     gout_t out;
     int32_t len, clevel, tablog;
     int32_t run_byte = -1;   // >= 0: the stream is a run of this byte (decided by the filter job)
+    uint32_t verdict = 0;    // 1: the filter job decided the stream's run test
     bool runs;
     {
       const CGeom g = lds_uniform(&A->g);
@@ -1795,9 +1855,11 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
           // a split (DELTA, SHUFFLE) block of a chunk with run streams (extended header): the run
           // verdict comes with the filter job, published with the block (ready word 1 | runs << 1)
           uint32_t runs = 0;
-          if (fk.ds && !lo && gk.spb == fk.ds && gk.overhead == kHdrExt && (fk.mode_bits & 128) == 0) {
-            runs = fuse_ds_block_runs(fk.raw + (int64_t)cc * fk.raw_stride, fk.filt + (int64_t)cc * gk.wstride + (int64_t)b * gk.bs,
-                                      fk.ds, b, bsize, gk.bs, &sh->runred);
+          if (fuse_verdict(fk, gk, lo)) {
+            uint8_t* fd = fk.filt + (int64_t)cc * gk.wstride + (int64_t)b * gk.bs;
+            runs = fk.ds ? fuse_ds_block_runs(fk.raw + (int64_t)cc * fk.raw_stride, fd, fk.ds, b, bsize, gk.bs, &sh->runred)
+                         : shuffle4_block_runs(fk.raw + (int64_t)cc * fk.raw_stride + (int64_t)b * gk.bs, fd, bsize, &sh->runred);
+            runs |= 1u << 29;   // (bit 30 once published) the verdict is complete: no run test needed
           } else {
             fuse_filter_block(fk, gk, cc, b, bsize, threadIdx.x, blockDim.x);
           }
@@ -1824,14 +1886,15 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
         const int32_t j = l - blk * g.spb;
         if (blk < g.nblocks - (g.leftover ? 1 : 0) && (((uint32_t)rv >> 1) >> j) & 1u) {
           const uint8_t* raw = f.raw + (int64_t)c * f.raw_stride;
-          run_byte = (int32_t)(uint8_t)(raw[(int64_t)blk * g.bs + j] ^ (blk ? raw[j] : 0));
+          run_byte = (int32_t)(uint8_t)(raw[(int64_t)blk * g.bs + j] ^ (blk && f.ds ? raw[j] : 0));
         }
+        verdict = ((uint32_t)rv >> 30) & 1u;
       }
       const CGeom g2 = lds_uniform(&A->g);
       in = (gin_t)(lds_uniform(&A->filt) + (int64_t)c * g2.wstride + off);
       out = (gout_t)(lds_uniform(&A->sbuf) + (int64_t)c * g2.wstride + off);
       clevel = g2.clevel;
-      runs = g2.overhead == kHdrExt;
+      runs = g2.overhead == kHdrExt && __builtin_amdgcn_readfirstlane(verdict) == 0;
       tablog = lds_uniform(&A->tablog);
     }
     FUSE_TRACE(6, s);
