@@ -1486,18 +1486,21 @@ __device__ void shuffle4_block_wt(const uint8_t* __restrict__ s, uint8_t* __rest
 // SHUFFLE) -- but in one pass: every plane is stored and the mismatches against each plane's first
 // byte (byte p of the block's first element) ORed in LDS word `red`.  Returns the run planes; the
 // encoder then skips their streams and the run test of the others.  Whole 64-byte groups (the
-// caller checks); the workgroup calls it together.
+// caller checks).  WG: the workgroup calls it together; else one wave (tid = lane, nth = 64, no
+// LDS word).
+template <bool WG>
 __device__ __noinline__ uint32_t shuffle4_block_runs(const uint8_t* __restrict__ s, uint8_t* __restrict__ d, int32_t bsize,
-                                                     B2H_LDS uint32_t* red) {
-  const int32_t tid = threadIdx.x, nth = blockDim.x;
+                                                     B2H_LDS uint32_t* red, int32_t tid, int32_t nth) {
   const int32_t n = bsize / 4, groups = n / 16;
   const __amdgpu_buffer_rsrc_t r = wt_rsrc((gout_t)d);
   const uint4* s4 = reinterpret_cast<const uint4*>(s);
   uint32_t rep[4];
 #pragma unroll
   for (int p = 0; p < 4; p++) rep[p] = 0x01010101u * (uint32_t)s[p];
-  if (tid == 0) *red = 0u;
-  __syncthreads();
+  if constexpr (WG) {
+    if (tid == 0) *red = 0u;
+    __syncthreads();
+  }
   uint32_t mis = 0;
   constexpr int U = 2;
   for (int32_t g0 = tid; g0 < groups; g0 += U * nth) {
@@ -1526,6 +1529,7 @@ __device__ __noinline__ uint32_t shuffle4_block_runs(const uint8_t* __restrict__
   uint32_t wm = 0;
 #pragma unroll
   for (int p = 0; p < 4; p++) wm |= __ballot((mis >> p) & 1u) ? (1u << p) : 0u;
+  if constexpr (!WG) return ~wm & 15u;
   if ((tid & 63) == 0 && wm) __hip_atomic_fetch_or(red, wm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   __syncthreads();
   const uint32_t M = __builtin_amdgcn_readfirstlane(*red);
@@ -1858,7 +1862,8 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
           if (fuse_verdict(fk, gk, lo)) {
             uint8_t* fd = fk.filt + (int64_t)cc * gk.wstride + (int64_t)b * gk.bs;
             runs = fk.ds ? fuse_ds_block_runs(fk.raw + (int64_t)cc * fk.raw_stride, fd, fk.ds, b, bsize, gk.bs, &sh->runred)
-                         : shuffle4_block_runs(fk.raw + (int64_t)cc * fk.raw_stride + (int64_t)b * gk.bs, fd, bsize, &sh->runred);
+                         : shuffle4_block_runs<true>(fk.raw + (int64_t)cc * fk.raw_stride + (int64_t)b * gk.bs, fd, bsize, &sh->runred,
+                                                   threadIdx.x, blockDim.x);
             runs |= 1u << 29;   // (bit 30 once published) the verdict is complete: no run test needed
           } else {
             fuse_filter_block(fk, gk, cc, b, bsize, threadIdx.x, blockDim.x);
@@ -2165,18 +2170,27 @@ __device__ void encode_loop_fused(const CGeom& g, TAB htab, B2H_LDS uint32_t* db
     const int32_t c = s / g.nsc, l = s - c * g.nsc;
     int32_t off, len, blk;
     stream_locate(g, l, &off, &len, &blk);
+    int32_t rv = 0;   // the block's ready word: 1 | run planes << 1 | verdict << 30
     if (f.raw) {
       const int32_t gb = c * g.nblocks + blk, target = min(gb + 1 + f.lead, nblk);
       int32_t k = claim_block(target);
       while (k >= 0 && k < nblk) {
         const int32_t cc = k / g.nblocks, b = k - cc * g.nblocks;
         const int32_t bsize = (b == g.nblocks - 1 && g.leftover) ? g.leftover : g.bs;
-        fuse_filter_block(f, g, cc, b, bsize, lane, 64);
+        // the 4-byte SHUFFLE job decides its split block's run verdict (as in k_encode_fast_fused)
+        uint32_t runs = 0;
+        if (f.ds == 0 && fuse_verdict(f, g, b == g.nblocks - 1 && g.leftover)) {
+          runs = shuffle4_block_runs<false>(f.raw + (int64_t)cc * f.raw_stride + (int64_t)b * g.bs,
+                                            f.filt + (int64_t)cc * g.wstride + (int64_t)b * g.bs, bsize, nullptr, lane, 64);
+          runs |= 1u << 29;
+        } else {
+          fuse_filter_block(f, g, cc, b, bsize, lane, 64);
+        }
         drain_stores();
-        if (lane == 0) st_agent(blk_ready + k, 1);
+        if (lane == 0) st_agent(blk_ready + k, (int32_t)(1u | (runs << 1)));
         k = claim_block(target);
       }
-      (void)wwait(blk_ready + gb);
+      rv = wwait(blk_ready + gb);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       drain_stores();
     }
@@ -2184,7 +2198,17 @@ __device__ void encode_loop_fused(const CGeom& g, TAB htab, B2H_LDS uint32_t* db
     gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
-    StreamResult r = encode_stream<TAB, true>(in, len, g.clevel, out, htab, dbits, oring, g.overhead == kHdrExt);
+    const uint32_t urv = (uint32_t)__builtin_amdgcn_readfirstlane(rv);
+    const bool verdict = (urv >> 30) & 1u;
+    StreamResult r;
+    if (verdict && ((urv >> 1) >> (l - blk * g.spb)) & 1u) {   // what the run test would return
+      r.windows = 0;
+      r.peak = 0;
+      r.size = f.raw[(int64_t)c * f.raw_stride + (int64_t)blk * g.bs + (l - blk * g.spb)];
+      r.kind = r.size ? kStreamByteRun : kStreamZeroRun;
+    } else {
+      r = encode_stream<TAB, true>(in, len, g.clevel, out, htab, dbits, oring, g.overhead == kHdrExt && !verdict);
+    }
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     if (TAB::kGlobal) r.windows |= 1 << 30;
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
