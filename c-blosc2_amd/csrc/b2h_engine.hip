@@ -2136,18 +2136,12 @@ static int launch_encode_fast_fused(Workspace* ws, const CGeom& g, const uint8_t
 // finalizes it, scatter items once the stream queue is empty.  Every wave-level decision comes
 // from an atomic all 64 lanes take part in (lane 0 adds, the others add 0) and a readfirstlane,
 // never from a value only lane 0 holds (see encode_loop).
+// The arguments (FusedArgs) live in LDS and every phase re-reads the words it needs: kept in
+// registers across the encode they cost ~300 SGPR spills (v_readlane / v_writelane reloads in the
+// parse loops; T exact fused 25.94 ms against 23.03 for k_encode alone).
 template <typename TAB>
-__device__ void encode_loop_fused(const CGeom& g, TAB htab, B2H_LDS uint32_t* dbits, B2H_LDS uint8_t* oring,
-                                  const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
-                                  StreamResult* __restrict__ res, int32_t nstreams_total, int32_t* __restrict__ next,
-                                  const int32_t* __restrict__ porder, const EncFuse& f) {
+__device__ void encode_loop_fused(const B2H_LDS FusedArgs* A, TAB htab, B2H_LDS uint32_t* dbits, B2H_LDS uint8_t* oring) {
   const int lane = lane_id();
-  const int32_t nblk = f.nchunks * g.nblocks;
-  int32_t* blk_ready = f.sync + kFuseHdr;
-  int32_t* chunk_cnt = blk_ready + nblk;
-  int32_t* ready = chunk_cnt + f.nchunks;
-  int32_t* tmo = f.sync + 4;
-  const int32_t ipc = (g.nsc + kFuseSpi - 1) / kFuseSpi, nitems = f.nchunks * ipc;
   auto wadd = [&](int32_t* p, int32_t v) -> int32_t {
     return __builtin_amdgcn_readfirstlane(
         __hip_atomic_fetch_add((gi32_t)p, lane == 0 ? v : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -2160,21 +2154,36 @@ __device__ void encode_loop_fused(const CGeom& g, TAB htab, B2H_LDS uint32_t* db
       if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) break;
       __builtin_amdgcn_s_sleep(8);
     }
-    if (lane == 0) st_agent(tmo, 1);
+    if (lane == 0) st_agent(lds_uniform(&A->f.sync) + 4, 1);
     return 0;
   };
-  auto claim_block = [&](int32_t target) -> int32_t { return wadd(f.sync, 0) < target ? wadd(f.sync, 1) : -1; };
-  int32_t i = wadd(next, 1);
-  while (i < nstreams_total) {
-    const int32_t s = __builtin_amdgcn_readfirstlane(pull_to_stream(g, porder, g.front, i, nstreams_total));
-    const int32_t c = s / g.nsc, l = s - c * g.nsc;
-    int32_t off, len, blk;
-    stream_locate(g, l, &off, &len, &blk);
+  auto claim_block = [&](int32_t target) -> int32_t {
+    int32_t* sync = lds_uniform(&A->f.sync);
+    return wadd(sync, 0) < target ? wadd(sync, 1) : -1;
+  };
+  int32_t i = wadd(lds_uniform(&A->next), 1);
+  while (i < lds_uniform(&A->nstreams_total)) {
+    int32_t s, c, l, off, len, blk;
     int32_t rv = 0;   // the block's ready word: 1 | run planes << 1 | verdict << 30
-    if (f.raw) {
-      const int32_t gb = c * g.nblocks + blk, target = min(gb + 1 + f.lead, nblk);
+    {
+      const CGeom g = lds_uniform(&A->g);
+      s = __builtin_amdgcn_readfirstlane(pull_to_stream(g, lds_uniform(&A->porder), g.front, i, lds_uniform(&A->nstreams_total)));
+      c = s / g.nsc;
+      l = s - c * g.nsc;
+      stream_locate(g, l, &off, &len, &blk);
+    }
+    if (lds_uniform(&A->f.raw)) {
+      int32_t gb, target, nblk;
+      {
+        const CGeom g = lds_uniform(&A->g);
+        nblk = lds_uniform(&A->f.nchunks) * g.nblocks;
+        gb = c * g.nblocks + blk;
+        target = min(gb + 1 + lds_uniform(&A->f.lead), nblk);
+      }
       int32_t k = claim_block(target);
       while (k >= 0 && k < nblk) {
+        const CGeom g = lds_uniform(&A->g);
+        const EncFuse f = lds_uniform(&A->f);
         const int32_t cc = k / g.nblocks, b = k - cc * g.nblocks;
         const int32_t bsize = (b == g.nblocks - 1 && g.leftover) ? g.leftover : g.bs;
         // the 4-byte SHUFFLE job decides its split block's run verdict (as in k_encode_fast_fused)
@@ -2187,75 +2196,101 @@ __device__ void encode_loop_fused(const CGeom& g, TAB htab, B2H_LDS uint32_t* db
           fuse_filter_block(f, g, cc, b, bsize, lane, 64);
         }
         drain_stores();
-        if (lane == 0) st_agent(blk_ready + k, (int32_t)(1u | (runs << 1)));
+        if (lane == 0) st_agent(f.sync + kFuseHdr + k, (int32_t)(1u | (runs << 1)));
         k = claim_block(target);
       }
-      rv = wwait(blk_ready + gb);
+      rv = wwait(lds_uniform(&A->f.sync) + kFuseHdr + gb);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       drain_stores();
     }
-    gin_t in = (gin_t)(filt + (int64_t)c * g.wstride + off);
-    gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
     const uint32_t urv = (uint32_t)__builtin_amdgcn_readfirstlane(rv);
     const bool verdict = (urv >> 30) & 1u;
     StreamResult r;
-    if (verdict && ((urv >> 1) >> (l - blk * g.spb)) & 1u) {   // what the run test would return
+    int32_t run_byte = -1;
+    gin_t in;
+    gout_t out;
+    int clevel;
+    bool runs_test;
+    {
+      const CGeom g = lds_uniform(&A->g);
+      const int32_t j = l - blk * g.spb;
+      if (verdict && ((urv >> 1) >> j) & 1u)   // what the run test would return
+        run_byte = lds_uniform(&A->f.raw)[(int64_t)c * lds_uniform(&A->f.raw_stride) + (int64_t)blk * g.bs + j];
+      in = (gin_t)(lds_uniform(&A->filt) + (int64_t)c * g.wstride + off);
+      out = (gout_t)(lds_uniform(&A->sbuf) + (int64_t)c * g.wstride + off);
+      clevel = g.clevel;
+      runs_test = g.overhead == kHdrExt && !verdict;
+    }
+    if (__builtin_amdgcn_readfirstlane(run_byte) >= 0) {
       r.windows = 0;
       r.peak = 0;
-      r.size = f.raw[(int64_t)c * f.raw_stride + (int64_t)blk * g.bs + (l - blk * g.spb)];
+      r.size = run_byte;
       r.kind = r.size ? kStreamByteRun : kStreamZeroRun;
     } else {
-      r = encode_stream<TAB, true>(in, len, g.clevel, out, htab, dbits, oring, g.overhead == kHdrExt && !verdict);
+      r = encode_stream<TAB, true>(in, len, clevel, out, htab, dbits, oring, runs_test);
     }
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
     if (TAB::kGlobal) r.windows |= 1 << 30;
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
-    if (lane == 0) {
-      res[s] = r;
-      st_agent(f.fin + 3 * s, r.kind);
-      st_agent(f.fin + 3 * s + 1, r.size);
-      st_agent(f.fin + 3 * s + 2, r.peak);
-    }
-    drain_stores();
-    const int32_t done = wadd(chunk_cnt + c, 1);
-    if (done == g.nsc - 1) {   // this wave completed chunk c: finalize it
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      drain_stores();
-      const bool inreg = g.nsc <= 64;   // lane j holds stream j's results
-      const int32_t* fc = f.fin + 3 * (int64_t)c * g.nsc;
-      int32_t fk = 0, fs = 0, fp = 0;
-      if (inreg && lane < g.nsc) {
-        fk = fc[3 * lane];
-        fs = fc[3 * lane + 1];
-        fp = fc[3 * lane + 2];
-      }
+    {
+      const CGeom g = lds_uniform(&A->g);
+      const EncFuse f = lds_uniform(&A->f);
       if (lane == 0) {
-        Place* pl = f.place + (int64_t)c * g.nsc;
-        int32_t cb = 0;
-        const int32_t m = finalize_chunk(
-            g, f.dst + (int64_t)c * g.dst_stride, f.htpl,
-            [&](int32_t j) {
-              StreamResult x;
-              x.kind = inreg ? __builtin_amdgcn_readlane(fk, j) : fc[3 * j];
-              x.size = inreg ? __builtin_amdgcn_readlane(fs, j) : fc[3 * j + 1];
-              x.peak = inreg ? __builtin_amdgcn_readlane(fp, j) : fc[3 * j + 2];
-              return x;
-            },
-            [&](int32_t j, int32_t o, int32_t cs) { st_agent(&pl[j].off, o); st_agent(&pl[j].csize, cs); }, &cb);
-        st_agent(f.mode + c, m);
-        f.cbytes[c] = cb;
+        lds_uniform(&A->res)[s] = r;
+        st_agent(f.fin + 3 * s, r.kind);
+        st_agent(f.fin + 3 * s + 1, r.size);
+        st_agent(f.fin + 3 * s + 2, r.peak);
+      }
+      drain_stores();
+      int32_t* chunk_cnt = f.sync + kFuseHdr + f.nchunks * g.nblocks;
+      int32_t* ready = chunk_cnt + f.nchunks;
+      const int32_t ipc = (g.nsc + kFuseSpi - 1) / kFuseSpi;
+      const int32_t done = wadd(chunk_cnt + c, 1);
+      if (done == g.nsc - 1) {   // this wave completed chunk c: finalize it
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         drain_stores();
-        const int32_t slot = add_agent(f.sync + 2, 1);
-        st_agent(ready + slot, c + 1);
-        drain_stores();
-        add_agent(f.sync + 3, ipc);
+        const bool inreg = g.nsc <= 64;   // lane j holds stream j's results
+        const int32_t* fc = f.fin + 3 * (int64_t)c * g.nsc;
+        int32_t fk = 0, fs = 0, fp = 0;
+        if (inreg && lane < g.nsc) {
+          fk = fc[3 * lane];
+          fs = fc[3 * lane + 1];
+          fp = fc[3 * lane + 2];
+        }
+        if (lane == 0) {
+          Place* pl = f.place + (int64_t)c * g.nsc;
+          int32_t cb = 0;
+          const int32_t m = finalize_chunk(
+              g, f.dst + (int64_t)c * g.dst_stride, f.htpl,
+              [&](int32_t jj) {
+                StreamResult x;
+                x.kind = inreg ? __builtin_amdgcn_readlane(fk, jj) : fc[3 * jj];
+                x.size = inreg ? __builtin_amdgcn_readlane(fs, jj) : fc[3 * jj + 1];
+                x.peak = inreg ? __builtin_amdgcn_readlane(fp, jj) : fc[3 * jj + 2];
+                return x;
+              },
+              [&](int32_t jj, int32_t o, int32_t cs) { st_agent(&pl[jj].off, o); st_agent(&pl[jj].csize, cs); }, &cb);
+          st_agent(f.mode + c, m);
+          f.cbytes[c] = cb;
+          drain_stores();
+          const int32_t slot = add_agent(f.sync + 2, 1);
+          st_agent(ready + slot, c + 1);
+          drain_stores();
+          add_agent(f.sync + 3, ipc);
+        }
       }
     }
-    i = wadd(next, 1);
+    i = wadd(lds_uniform(&A->next), 1);
   }
   // stream queue empty: scatter items
+  const CGeom g = lds_uniform(&A->g);
+  const EncFuse f = lds_uniform(&A->f);
+  const uint8_t* filt = lds_uniform(&A->filt);
+  const uint8_t* sbuf = lds_uniform(&A->sbuf);
+  int32_t* ready = f.sync + kFuseHdr + f.nchunks * g.nblocks + f.nchunks;
+  const int32_t ipc = (g.nsc + kFuseSpi - 1) / kFuseSpi, nitems = f.nchunks * ipc;
   int32_t k = wadd(f.sync + 1, 1);
   while (k < nitems) {
     const int32_t slot = k / ipc, j0 = (k - slot * ipc) * kFuseSpi;
@@ -2287,29 +2322,46 @@ __device__ void encode_loop_fused(const CGeom& g, TAB htab, B2H_LDS uint32_t* db
   }
 }
 
+template <typename POS>
+__host__ __device__ constexpr size_t enc_fused_lds(int hashlog, int nlds, int nglb) {
+  return enc_wg_lds<POS>(hashlog, nlds, nglb) + ((sizeof(FusedArgs) + 15) & ~size_t(15));
+}
+// three 4-wave workgroups per CU (the VGPR limit) at hashlog 14 with u16 positions
+static_assert(enc_fused_lds<uint16_t>(14, 1, 3) <= 160 * 1024 / 3, "exact fused encoder: LDS for fewer than 3 workgroups per CU");
+
 template <typename POS, int NLDS, int NGLB>
 __global__ __launch_bounds__(64 * (NLDS + NGLB)) __attribute__((amdgpu_waves_per_eu(3, 8)))
-void k_encode_fused(CGeom g, const uint8_t* __restrict__ filt,
-                                                                     uint8_t* __restrict__ sbuf,
-                                                                     StreamResult* __restrict__ res,
-                                                                     int32_t nstreams_total, int32_t* __restrict__ next,
-                                                                     POS* __restrict__ gtab,
-                                                                     const int32_t* __restrict__ porder, EncFuse f) {
+void k_encode_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint8_t* __restrict__ sbuf_arg,
+                    StreamResult* __restrict__ res_arg, int32_t nstreams_total_arg, int32_t* __restrict__ next_arg,
+                    POS* __restrict__ gtab, const int32_t* __restrict__ porder_arg, EncFuse f_arg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
+  const int hashlog = g_arg.clevel == 1 ? 12 : (g_arg.clevel == 2 ? 13 : 14);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const size_t tabsz = sizeof(POS) << hashlog;
+  B2H_LDS FusedArgs* A = (B2H_LDS FusedArgs*)(smem + enc_wg_lds<POS>(hashlog, NLDS, NGLB));
+  if (threadIdx.x == 0) {
+    lds_store(&A->g, g_arg);
+    lds_store(&A->f, f_arg);
+    A->filt = filt_arg;
+    A->sbuf = sbuf_arg;
+    A->res = res_arg;
+    A->next = next_arg;
+    A->porder = porder_arg;
+    A->nstreams_total = nstreams_total_arg;
+    A->tablog = hashlog;
+  }
+  __syncthreads();
   B2H_LDS uint8_t* mine = (B2H_LDS uint8_t*)(smem + NLDS * tabsz + w * enc_wave_lds(hashlog));
   B2H_LDS uint32_t* dbits = (B2H_LDS uint32_t*)mine;
   B2H_LDS uint8_t* oring = mine + ((size_t(1) << hashlog) >> 3);
   if (NLDS > 0 && w < NLDS) {
     LdsTab<POS> t;
     t.t = (volatile B2H_LDS POS*)(smem + w * tabsz);
-    encode_loop_fused(g, t, dbits, oring, filt, sbuf, res, nstreams_total, next, porder, f);
+    encode_loop_fused(static_cast<const B2H_LDS FusedArgs*>(A), t, dbits, oring);
   } else if (NGLB > 0) {
     GlbTab<POS> t;
     t.t = (B2H_GLB POS*)(gtab + (((size_t)blockIdx.x * NGLB + (w - NLDS)) << hashlog));
-    encode_loop_fused(g, t, dbits, oring, filt, sbuf, res, nstreams_total, next, porder, f);
+    encode_loop_fused(static_cast<const B2H_LDS FusedArgs*>(A), t, dbits, oring);
   }
 }
 
@@ -2320,7 +2372,7 @@ static int launch_encode_exact_fused(Workspace* ws, const CGeom& g, int hashlog,
                                      hipStream_t st) {
   constexpr int NL = 1, NG = 3;
   const void* fn = reinterpret_cast<const void*>(&k_encode_fused<POS, NL, NG>);
-  const size_t lds = enc_wg_lds<POS>(hashlog, NL, NG);
+  const size_t lds = enc_fused_lds<POS>(hashlog, NL, NG);
   static bool attr_set = false;
   if (!attr_set) {
     HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
