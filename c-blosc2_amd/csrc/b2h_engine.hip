@@ -2032,8 +2032,11 @@ static int64_t fuse_grid_cap(int64_t slots) {
   const char* e = getenv("B2H_FUSE_GRID");
   return e && atoi(e) > 0 ? std::min<int64_t>(slots, atoi(e)) : slots;
 }
+// How far (in blocks) the fused launch's shuffle claims run ahead of the block a workgroup's stream
+// needs.  T fast, same box (profiles/r5_ab_shuf_lead.txt): 512 214.9, 256 215.1, 128 215.8,
+// 64 215.9, 32 215.7 GiB/s -- less shuffle traffic ahead of the encoders; C3 / C4 unchanged.
 static int fuse_lead() {
-  static const int v = [] { const char* e = getenv("B2H_SHUF_LEAD"); return e ? std::max(1, atoi(e)) : 512; }();
+  static const int v = [] { const char* e = getenv("B2H_SHUF_LEAD"); return e ? std::max(1, atoi(e)) : 64; }();
   return v;
 }
 
