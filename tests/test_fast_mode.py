@@ -384,7 +384,8 @@ def test_gpu_deep_mode_ratio(fast, data):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("lzmode", [1, 2, 0], ids=["fast", "deep", "exact"])
-@pytest.mark.parametrize("shape", ["T", "leftover", "clevel9_ts8", "ds8", "ds8_ramp", "ds2_leftover", "ds4_odd_leftover"])
+@pytest.mark.parametrize("shape", ["T", "ts4_runplanes", "leftover", "clevel9_ts8", "ds8", "ds8_ramp", "ds2_leftover",
+                                   "ds4_odd_leftover"])
 def test_gpu_fused_launch_matches_separate_launches(fast, shape, lzmode, monkeypatch):
     """The one-launch fast-mode encode (byte shuffle, finalize and payload scatter inside the
     encoder launch, k_encode_fast_fused) writes the same chunks as the separate launches
@@ -396,6 +397,8 @@ def test_gpu_fused_launch_matches_separate_launches(fast, shape, lzmode, monkeyp
     dev = torch.device("cuda")
     if shape == "T":
         chunk, n, kw = 4 << 20, 24, dict(clevel=5, typesize=4)
+    elif shape == "ts4_runplanes":   # the SHUFFLE job's run verdict (b2h_engine.hip shuffle4_block_runs)
+        chunk, n, kw = 1 << 20, 12, dict(clevel=5, typesize=4)
     elif shape == "leftover":
         chunk, n, kw = (1 << 20) + 4 * 37, 12, dict(clevel=5, typesize=4, blocksize=1 << 18)
     elif shape == "clevel9_ts8":
@@ -408,7 +411,17 @@ def test_gpu_fused_launch_matches_separate_launches(fast, shape, lzmode, monkeyp
         chunk, n, kw = (1 << 20) + 64 * 3, 12, dict(clevel=5, typesize=2, filters=(0, 0, 0, 0, 3, 1), blocksize=1 << 18)
     else:   # leftover not of whole 64-byte groups: the separate k_ffilter_ds launch
         chunk, n, kw = (1 << 20) + 4 * 37, 12, dict(clevel=5, typesize=4, filters=(0, 0, 0, 0, 3, 1), blocksize=1 << 18)
-    if shape == "ds8_ramp":
+    if shape == "ts4_runplanes":
+        # planes 2 and 3 runs of 0x0B / 0x0A, planes 0 and 1 noise; in every third 256 KiB block
+        # one byte of plane 2 differs (one block near its end, the others anywhere)
+        rng = np.random.default_rng(13)
+        v = rng.integers(0, 1 << 16, n * chunk // 4, dtype=np.uint32) | np.uint32(0x0A0B0000)
+        per = (1 << 18) // 4
+        for b in range(0, n * chunk // (1 << 18), 3):
+            e = b * per + (per - 1 if b % 2 else int(rng.integers(0, per)))
+            v[e] ^= np.uint32(0x00010000)
+        src = torch.from_numpy(v.view(np.uint8).copy()).to(dev)
+    elif shape == "ds8_ramp":
         src = torch.from_numpy(int64_ramp(7, n * chunk // 8).view(np.uint8).copy()).to(dev)
     elif shape.startswith("ds"):
         rng = np.random.default_rng(11)   # a ramp with jitter: run, raw and LZ streams after the filters
