@@ -1096,7 +1096,12 @@ blosc2_schunk* schunk_from_link(std::unique_ptr<FrameLink> L, bool copy, const c
       s->blocksize = common_bs;   // cbytes: the appended chunks' sum already
     }
   }
-  if (rc < 0 && !s->frame && io_destroy) io_destroy(io_params);   // an attached handle's free does it
+  if (rc < 0 && !s->frame) {
+    // the stream closes before its params go (schunk.c:698-705 order); an attached handle's
+    // free does both
+    L.reset();
+    if (io_destroy) io_destroy(io_params);
+  }
   if (rc < 0) {
     blosc2_schunk_free(s);   // an attached handle's link goes with it
     return nullptr;

@@ -490,6 +490,136 @@ int blosc2_schunk_get_slice_buffer(blosc2_schunk* schunk, int64_t start, int64_t
   return BLOSC2_ERROR_SUCCESS;
 }
 
+// blosc2_schunk_get_sparse_buffer (blosc/schunk.c:1922-2110).  The argument checks are the
+// reference's, in its order.  Under DELTA, with a postfilter, or for a single coordinate it takes
+// one getitem per coordinate (schunk_get_sparse_getitem, schunk.c:1866-1900): the bounds check
+// of a coordinate only when its turn comes.  Otherwise every coordinate is checked first, the
+// coordinates are sorted by (coord, output index) and grouped by chunk and block, every touched
+// chunk is fetched, and then -- where the reference decodes each touched block with
+// blosc2_decompress_block_ctx on its thread pool -- a chunk with several touched blocks is decoded
+// once on the device with the other blocks masked (one device call per chunk).  A chunk whose
+// masked decode fails, or whose own blocksize is not the super-chunk's, takes the reference's
+// per-block calls, so the error code is the one its serial walk meets first.
+int blosc2_schunk_get_sparse_buffer(blosc2_schunk* schunk, int64_t ncoords, const int64_t* coords, void* buffer) {
+  if (!schunk) return BLOSC2_ERROR_INVALID_PARAM;
+  if (ncoords < 0) return BLOSC2_ERROR_INVALID_PARAM;
+  if (ncoords == 0) return BLOSC2_ERROR_SUCCESS;
+  if (!coords || !buffer) return BLOSC2_ERROR_INVALID_PARAM;
+  if (schunk->typesize <= 0) return BLOSC2_ERROR_INVALID_PARAM;
+  if (schunk->chunksize <= 0) {
+    TRACE_ERROR("blosc2_schunk_get_sparse_buffer does not support variable-length chunks yet.");
+    return BLOSC2_ERROR_INVALID_PARAM;
+  }
+  if (schunk->blocksize <= 0 || (schunk->flags2 & BLOSC2_VL_BLOCKS)) {
+    TRACE_ERROR("blosc2_schunk_get_sparse_buffer does not support variable-length blocks yet.");
+    return BLOSC2_ERROR_INVALID_PARAM;
+  }
+  const int64_t ts = schunk->typesize, cs = schunk->chunksize, bs = schunk->blocksize;
+  if (cs % ts || bs % ts) return BLOSC2_ERROR_INVALID_PARAM;
+  const int64_t nitems = schunk->nbytes / ts, chunk_nitems = cs / ts;
+  uint8_t* out = static_cast<uint8_t*>(buffer);
+
+  bool per_item = ncoords <= 1;
+  for (int i = 0; i < BLOSC2_MAX_FILTERS; i++) per_item |= schunk->filters[i] == BLOSC_DELTA;
+  blosc2_dparams dp;
+  per_item |= schunk->dctx && blosc2_ctx_get_dparams(schunk->dctx, &dp) == 0 && dp.postfilter;
+  if (per_item) {
+    for (int64_t i = 0; i < ncoords; i++) {
+      const int64_t coord = coords[i];
+      if (coord < 0 || coord >= nitems) return BLOSC2_ERROR_INVALID_PARAM;
+      uint8_t* chunk;
+      bool needs_free = false;
+      const int cbytes = blosc2_schunk_get_lazychunk(schunk, coord / chunk_nitems, &chunk, &needs_free);
+      if (cbytes <= 0) return BLOSC2_ERROR_FAILURE;
+      const int got = blosc2_getitem_bytes_ctx(schunk->dctx, chunk, cbytes, (int32_t)((coord % chunk_nitems) * ts),
+                                               (int32_t)ts, out + i * ts, (int32_t)ts);
+      if (needs_free) free(chunk);
+      if (got != ts) return BLOSC2_ERROR_FAILURE;
+    }
+    return BLOSC2_ERROR_SUCCESS;
+  }
+
+  for (int64_t i = 0; i < ncoords; i++)
+    if (coords[i] < 0 || coords[i] >= nitems) return BLOSC2_ERROR_INVALID_PARAM;
+  if (chunk_nitems > INT32_MAX) return BLOSC2_ERROR_INVALID_PARAM;
+  std::vector<std::pair<int64_t, int64_t>> e((size_t)ncoords);   // (coord, output index)
+  for (int64_t i = 0; i < ncoords; i++) e[(size_t)i] = {coords[i], i};
+  std::sort(e.begin(), e.end());
+  struct Fetched {
+    uint8_t* chunk;
+    int cbytes;
+    bool needs_free;
+    size_t first, last;   // its entries [first, last)
+  };
+  std::vector<Fetched> chunks;
+  struct Freer {
+    std::vector<Fetched>* v;
+    ~Freer() {
+      for (auto& f : *v)
+        if (f.needs_free) free(f.chunk);
+    }
+  } freer{&chunks};
+  for (size_t i = 0; i < e.size();) {   // every touched chunk fetched before any decode
+    const int64_t nchunk = e[i].first / chunk_nitems;
+    size_t j = i;
+    while (j < e.size() && e[j].first / chunk_nitems == nchunk) j++;
+    Fetched f{nullptr, 0, false, i, j};
+    f.cbytes = blosc2_schunk_get_lazychunk(schunk, nchunk, &f.chunk, &f.needs_free);
+    if (f.cbytes <= 0) {
+      TRACE_ERROR("Cannot get lazychunk ('%lld').", (long long)nchunk);
+      return BLOSC2_ERROR_FAILURE;
+    }
+    chunks.push_back(f);
+    i = j;
+  }
+  std::vector<uint8_t> img, blk((size_t)bs);
+  auto block_of = [&](int64_t coord) { return (int32_t)(((coord % chunk_nitems) * ts) / bs); };
+  auto put = [&](const uint8_t* b, int32_t nbytes, size_t first, size_t last) {
+    for (size_t k = first; k < last; k++) {
+      const int32_t off = (int32_t)(((e[k].first % chunk_nitems) * ts) % bs);
+      if (off > nbytes - ts) return (int)BLOSC2_ERROR_DATA;
+      memcpy(out + e[k].second * ts, b + off, (size_t)ts);
+    }
+    return 0;
+  };
+  for (const Fetched& f : chunks) {
+    int32_t nblocks_touched = 0;
+    for (size_t k = f.first; k < f.last; k++)
+      nblocks_touched += k == f.first || block_of(e[k].first) != block_of(e[k - 1].first);
+    int32_t c_nbytes = 0, c_bs = 0;
+    bool whole = nblocks_touched > 1 && blosc2_cbuffer_sizes(f.chunk, &c_nbytes, nullptr, &c_bs) >= 0 &&
+                 c_bs == bs && c_nbytes > 0;
+    if (whole) {
+      const int32_t nb = (int32_t)((c_nbytes + bs - 1) / bs);
+      std::vector<uint8_t> mask((size_t)nb, 1);
+      bool fits = true;
+      for (size_t k = f.first; k < f.last; k++) {
+        const int32_t b = block_of(e[k].first);
+        fits &= b < nb;
+        if (b < nb) mask[(size_t)b] = 0;
+      }
+      img.resize((size_t)c_nbytes);
+      whole = fits && blosc2_set_maskout(schunk->dctx, reinterpret_cast<bool*>(mask.data()), nb) == 0 &&
+              blosc2_decompress_ctx(schunk->dctx, f.chunk, f.cbytes, img.data(), c_nbytes) == c_nbytes;
+    }
+    for (size_t k = f.first; k < f.last;) {   // one task per touched block, in order
+      const int32_t b = block_of(e[k].first);
+      size_t k2 = k;
+      while (k2 < f.last && block_of(e[k2].first) == b) k2++;
+      int rc;
+      if (whole) {
+        rc = put(img.data() + (int64_t)b * bs, (int32_t)std::min<int64_t>(bs, c_nbytes - (int64_t)b * bs), k, k2);
+      } else {
+        const int nbytes = blosc2_decompress_block_ctx(schunk->dctx, f.chunk, f.cbytes, b, blk.data(), (int32_t)bs);
+        rc = nbytes < 0 ? nbytes : put(blk.data(), nbytes, k, k2);
+      }
+      if (rc < 0) return rc;
+      k = k2;
+    }
+  }
+  return BLOSC2_ERROR_SUCCESS;
+}
+
 // schunk.c:70-105
 int blosc2_schunk_get_cparams(blosc2_schunk* schunk, blosc2_cparams** cparams) {
   if (!schunk || !cparams) return BLOSC2_ERROR_NULL_POINTER;
@@ -828,24 +958,49 @@ struct DecodeStage {
     *p = nullptr;
     return hipMalloc(reinterpret_cast<void**>(p), n) == hipSuccess;
   }
+  // Frees every slot and zeroes the capacities: after a failed grow some slots are freed or null,
+  // and a stage going back to the pool must not claim room it no longer has.
+  void drop() {
+    for (int i = 0; i < 2; i++) {
+      for (uint8_t** p : {&pin_in[i], &pin_tab[i]}) {
+        if (*p) (void)hipHostFree(*p);
+        *p = nullptr;
+      }
+      for (uint8_t** p : {&dev_in[i], &dev_tab[i], &dev_out[i]}) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+      }
+    }
+    for (int i = 0; i < 3; i++) {
+      if (pin_out[i]) (void)hipHostFree(pin_out[i]);
+      if (pin_st[i]) (void)hipHostFree(pin_st[i]);
+      pin_out[i] = nullptr;
+      pin_st[i] = nullptr;
+    }
+    in_cap = out_cap = tab_cap = 0;
+  }
   bool ensure(size_t in, size_t out, size_t tab) {   // (an idle stage has nothing in flight)
+    auto fail = [&] {
+      drop();
+      return false;
+    };
     if (in > in_cap) {
       for (int i = 0; i < 2; i++)
-        if (!grow_pin(&pin_in[i], in) || !grow_dev(&dev_in[i], in)) return false;
+        if (!grow_pin(&pin_in[i], in) || !grow_dev(&dev_in[i], in)) return fail();
       in_cap = in;
     }
     if (out > out_cap) {
       for (int i = 0; i < 2; i++)
-        if (!grow_dev(&dev_out[i], out)) return false;
+        if (!grow_dev(&dev_out[i], out)) return fail();
       for (int i = 0; i < 3; i++)
-        if (!grow_pin(&pin_out[i], out)) return false;
+        if (!grow_pin(&pin_out[i], out)) return fail();
       out_cap = out;
     }
     if (tab > tab_cap) {
       for (int i = 0; i < 2; i++)
-        if (!grow_pin(&pin_tab[i], tab) || !grow_dev(&dev_tab[i], tab)) return false;
+        if (!grow_pin(&pin_tab[i], tab) || !grow_dev(&dev_tab[i], tab)) return fail();
       for (int i = 0; i < 3; i++)
-        if (!grow_pin(reinterpret_cast<uint8_t**>(&pin_st[i]), tab)) return false;
+        if (!grow_pin(reinterpret_cast<uint8_t**>(&pin_st[i]), tab)) return fail();
       tab_cap = tab;
     }
     return true;

@@ -414,19 +414,18 @@ int call_postfilter(blosc2_context* ctx, const ChunkHdr& H, const uint8_t* in, u
   return 0;
 }
 
-// The chunk's block images without the postfilter (the caller holds ctx->mu).
-struct NoPostfilter {
-  blosc2_context* c;
-  blosc2_postfilter_fn f;
-  explicit NoPostfilter(blosc2_context* ctx) : c(ctx), f(ctx->dparams.postfilter) { ctx->dparams.postfilter = nullptr; }
-  ~NoPostfilter() { c->dparams.postfilter = f; }
-};
+// decompress_host mode bit (host only, never reaches the device): decode the chunk's block images
+// without running the postfilter.  A flag instead of clearing ctx->dparams.postfilter for the call:
+// other threads read that field (the fan-out's staged decode classifies chunks concurrently).
+constexpr int kHostNoPost = 1 << 16;
 
 // Decompress one host chunk through the engine.  With a block mask only unmasked blocks are
 // copied back so masked regions of `dest` keep the caller's bytes (blosc/blosc2.c:1734-1737).
 // `mode`: b2h::kDecDeltaSelf for the per-block entry points (getitem, decompress_block).
 int decompress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void* dest, int32_t destsize,
                     const std::vector<uint8_t>* mask, int mode = 0) {
+  const bool run_post = ctx->dparams.postfilter && !(mode & kHostNoPost);
+  mode &= ~kHostNoPost;
   ChunkHdr H;
   int rc = read_header(src, srcsize, &H);
   if (rc < 0) return rc;
@@ -438,15 +437,12 @@ int decompress_host(blosc2_context* ctx, const void* src, int32_t srcsize, void*
                 mask->size(), nblocks);
     return BLOSC2_ERROR_DATA;
   }
-  if (ctx->dparams.postfilter) {
+  if (run_post) {
     // The engine decodes the chunk (every backward filter) into a host image; the callback then
     // runs per unmasked block, in block order, writing `dest` (blosc_d with a postfilter never
     // writes dest itself: 1880-1883, 1960-1965, 1489, 1581).
     std::vector<uint8_t> img((size_t)std::max(nbytes, 1));
-    {
-      NoPostfilter np(ctx);
-      rc = decompress_host(ctx, src, srcsize, img.data(), nbytes, mask, mode);
-    }
+    rc = decompress_host(ctx, src, srcsize, img.data(), nbytes, mask, mode | kHostNoPost);
     if (rc < 0) return rc;
     for (int32_t b = 0; b < nblocks; b++) {
       if (mask && (*mask)[(size_t)b]) continue;
@@ -1406,6 +1402,36 @@ int blosc2_free_resources(void) {
 
 const char* blosc2_get_version_string(void) { return BLOSC2_VERSION_STRING; }
 
+// blosc/blosc2.c:6916-6995
+const char* blosc2_error_string(int error_code) {
+  static const char* const msg[] = {
+      "Success",   // (never returned: 0 is not an error, see below)
+      "Generic failure", "Bad stream", "Invalid data", "Memory alloc/realloc failure", "Not enough space to read",
+      "Not enough space to write", "Codec not supported", "Invalid parameter supplied to codec",
+      "Codec dictionary error", "Version not supported", "Invalid value in header",
+      "Invalid parameter supplied to function", "File read failure", "File write failure", "File open failure",
+      "Not found", "Bad run length encoding", "Filter pipeline error", "Chunk insert failure",
+      "Chunk append failure", "Chunk update failure", "Sizes larger than 2gb not supported",
+      "Super-chunk copy failure", "Wrong type for frame", "File truncate failure",
+      "Thread or thread context creation failure", "Postfilter failure", "Special frame failure",
+      "Special super-chunk failure", "IO plugin error", "Remove file failure", "Pointer is null", "Invalid index",
+      "Metalayer has not been found", "Maximum buffersize exceeded", "Tuner failure", "Frame lock failure"};
+  // codes -1 .. -37 index the table; BLOSC2_ERROR_SUCCESS has no case in the reference's switch
+  if (error_code < 0 && error_code >= BLOSC2_ERROR_LOCK) return msg[-error_code];
+  return "Unknown error";
+}
+
+// blosc/timestamp.c (the POSIX branch): CLOCK_MONOTONIC, differences in ns and s
+void blosc_set_timestamp(blosc_timestamp_t* timestamp) { clock_gettime(CLOCK_MONOTONIC, timestamp); }
+
+double blosc_elapsed_nsecs(blosc_timestamp_t start_time, blosc_timestamp_t end_time) {
+  return 1e9 * (double)(end_time.tv_sec - start_time.tv_sec) + (double)(end_time.tv_nsec - start_time.tv_nsec);
+}
+
+double blosc_elapsed_secs(blosc_timestamp_t start_time, blosc_timestamp_t end_time) {
+  return 1e-9 * blosc_elapsed_nsecs(start_time, end_time);
+}
+
 // blosc/blosc2.c:6040-6251 (validation + environment overrides)
 blosc2_context* blosc2_create_cctx(blosc2_cparams cparams) {
   blosc2_context* c = new blosc2_context_s();
@@ -1587,7 +1613,7 @@ static void carve_items(const uint8_t* s, const ChunkHdr& H, int64_t off, int32_
 }
 
 static int blosc2_decompress_block_unlocked(blosc2_context* context, const void* src, int32_t srcsize, int32_t nblock,
-                                            void* dest, int32_t destsize, const ChunkHdr& H);
+                                            void* dest, int32_t destsize, const ChunkHdr& H, int host_mode);
 
 // blosc2_decompress_block_ctx (blosc/blosc2.c:4580-4687; declared in blosc-private.h:29 and used
 // by the sparse reader, schunk.c:1858): block `nblock` of a chunk into dest, returning its size.
@@ -1630,19 +1656,16 @@ int blosc2_decompress_block_ctx(blosc2_context* context, const void* src, int32_
     // blosc_d(dest, dest_offset 0) with the postfilter: the block's image, then the callback
     // writes dest (blosc/blosc2.c:4678-4682, 1586-1606, 1910-1931)
     std::vector<uint8_t> blk((size_t)bsize);
-    {
-      NoPostfilter np(context);
-      rc = blosc2_decompress_block_unlocked(context, src, srcsize, nblock, blk.data(), bsize, H);
-    }
+    rc = blosc2_decompress_block_unlocked(context, src, srcsize, nblock, blk.data(), bsize, H, kHostNoPost);
     if (rc < 0) return rc;
     if ((rc = call_postfilter(context, H, blk.data(), static_cast<uint8_t*>(dest), nblock)) < 0) return rc;
     return bsize;
   }
-  return blosc2_decompress_block_unlocked(context, src, srcsize, nblock, dest, destsize, H);
+  return blosc2_decompress_block_unlocked(context, src, srcsize, nblock, dest, destsize, H, 0);
 }
 
 static int blosc2_decompress_block_unlocked(blosc2_context* context, const void* src, int32_t srcsize, int32_t nblock,
-                                            void* dest, int32_t destsize, const ChunkHdr& H) {
+                                            void* dest, int32_t destsize, const ChunkHdr& H, int host_mode) {
   const uint8_t* s = static_cast<const uint8_t*>(src);
   const bool leftover = nblock == H.nblocks - 1 && H.leftover > 0;
   const int32_t bsize = leftover ? H.leftover : H.blocksize;
@@ -1658,13 +1681,14 @@ static int blosc2_decompress_block_unlocked(blosc2_context* context, const void*
     if (H.special == BLOSC2_SPECIAL_UNINIT) return bsize;
     std::vector<uint8_t> one;
     carve_items(s, H, (int64_t)nblock * H.blocksize, bsize, one);
-    rc = decompress_host(context, one.data(), (int32_t)one.size(), dest, destsize, nullptr);
+    rc = decompress_host(context, one.data(), (int32_t)one.size(), dest, destsize, nullptr, host_mode);
     return rc < 0 ? rc : bsize;
   }
   std::vector<uint8_t> mask((size_t)H.nblocks, 1);
   mask[nblock] = 0;
   std::vector<uint8_t> full((size_t)H.nbytes);
-  rc = decompress_host(context, src, srcsize, full.data(), H.nbytes, &mask, b2h::kDecDeltaSelf | b2h::kDecNoDict);
+  rc = decompress_host(context, src, srcsize, full.data(), H.nbytes, &mask,
+                       b2h::kDecDeltaSelf | b2h::kDecNoDict | host_mode);
   if (rc < 0) return rc;
   memcpy(dest, full.data() + (int64_t)nblock * H.blocksize, (size_t)bsize);
   return bsize;
@@ -1711,10 +1735,8 @@ int blosc2_getitem_ctx(blosc2_context* context, const void* src, int32_t srcsize
       if (hi > sb && lo < stop * ts) mask[b] = 0;
     }
     std::vector<uint8_t> full((size_t)std::max(H.nbytes, 1)), blk((size_t)H.blocksize);
-    {
-      NoPostfilter np(context);
-      rc = decompress_host(context, src, srcsize, full.data(), H.nbytes, &mask, b2h::kDecDeltaSelf | b2h::kDecNoDict);
-    }
+    rc = decompress_host(context, src, srcsize, full.data(), H.nbytes, &mask,
+                         b2h::kDecDeltaSelf | b2h::kDecNoDict | kHostNoPost);
     if (rc < 0) return rc;
     int64_t nt = 0;
     for (int32_t b = 0; b < H.nblocks; b++) {

@@ -21,6 +21,8 @@
 #include <stdint.h>
 #include <stddef.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <time.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -34,6 +36,74 @@ extern "C" {
 #define BLOSC2_VERSION_RELEASE 3
 #define BLOSC2_VERSION_STRING "3.3.3.dev"
 #define BLOSC2_VERSION_DATE "$Date:: 2026-08-06 #$"
+
+/* ---- the Blosc 1.x spellings (include/blosc2.h:43-80): macros onto the exported names ---- */
+#ifdef BLOSC1_COMPAT
+#define BLOSC_VERSION_MAJOR BLOSC2_VERSION_MAJOR
+#define BLOSC_VERSION_MINOR BLOSC2_VERSION_MINOR
+#define BLOSC_VERSION_RELEASE BLOSC2_VERSION_RELEASE
+#define BLOSC_VERSION_STRING BLOSC2_VERSION_STRING
+#define BLOSC_VERSION_DATE BLOSC2_VERSION_DATE
+#define blosc_compress blosc1_compress
+#define blosc_decompress blosc1_decompress
+#define blosc_getitem blosc1_getitem
+#define blosc_get_compressor blosc1_get_compressor
+#define blosc_set_compressor blosc1_set_compressor
+#define blosc_cbuffer_sizes blosc1_cbuffer_sizes
+#define blosc_cbuffer_validate blosc1_cbuffer_validate
+#define blosc_cbuffer_metainfo blosc1_cbuffer_metainfo
+#define blosc_get_blocksize blosc1_get_blocksize
+#define blosc_set_blocksize blosc1_set_blocksize
+#define blosc_set_splitmode blosc1_set_splitmode
+#define blosc_init blosc2_init
+#define blosc_destroy blosc2_destroy
+#define blosc_free_resources blosc2_free_resources
+#define blosc_get_nthreads blosc2_get_nthreads
+#define blosc_set_nthreads blosc2_set_nthreads
+#define blosc_compcode_to_compname blosc2_compcode_to_compname
+#define blosc_compname_to_compcode blosc2_compname_to_compcode
+#define blosc_list_compressors blosc2_list_compressors
+#define blosc_get_version_string blosc2_get_version_string
+#define blosc_get_complib_info blosc2_get_complib_info
+#define blosc_cbuffer_versions blosc2_cbuffer_versions
+#define blosc_cbuffer_complib blosc2_cbuffer_complib
+#endif
+
+/* ---- tracing / error macros user code (plugins, examples) expands (include/blosc2.h:92-125,
+ * include/blosc2/blosc2-common.h:28) ---- */
+#define BLOSC_UNUSED_PARAM(x) ((void)(x))
+#define BLOSC_ATTRIBUTE_UNUSED __attribute__((unused))
+#define BLOSC_TRACE(cat, msg, ...)                                                        \
+  do {                                                                                    \
+    const char *__e = getenv("BLOSC_TRACE");                                              \
+    if (!__e) { break; }                                                                  \
+    fprintf(stderr, "[%s] - " msg " (%s:%d)\n", #cat, ##__VA_ARGS__, __FILE__, __LINE__); \
+  } while (0)
+#define BLOSC_TRACE_ERROR(msg, ...) BLOSC_TRACE(error, msg, ##__VA_ARGS__)
+#define BLOSC_TRACE_WARNING(msg, ...) BLOSC_TRACE(warning, msg, ##__VA_ARGS__)
+#define BLOSC_TRACE_INFO(msg, ...) BLOSC_TRACE(info, msg, ##__VA_ARGS__)
+#define BLOSC_ERROR_NULL(pointer, rc)           \
+  do {                                          \
+    if ((pointer) == NULL) {                    \
+      BLOSC_TRACE_ERROR("Pointer is null");     \
+      return (rc);                              \
+    }                                           \
+  } while (0)
+#define BLOSC_ERROR(rc)                          \
+  do {                                           \
+    int rc_ = (rc);                              \
+    if (rc_ < BLOSC2_ERROR_SUCCESS) {            \
+      char *error_msg = print_error(rc_);        \
+      BLOSC_TRACE_ERROR("%s", error_msg);        \
+      return rc_;                                \
+    }                                            \
+  } while (0)
+#define BLOSC_INFO(msg, ...)                              \
+  do {                                                    \
+    const char *__e = getenv("BLOSC_INFO");               \
+    if (!__e) { break; }                                  \
+    fprintf(stderr, "[INFO] - " msg "\n", ##__VA_ARGS__); \
+  } while (0)
 
 /* ---- format constants (include/blosc2.h:128-196) ---- */
 enum {
@@ -226,6 +296,20 @@ enum {
   BLOSC2_ERROR_TUNER = -36,
   BLOSC2_ERROR_LOCK = -37,
 };
+
+/* include/blosc2.h:510 (blosc2_error_string, blosc/blosc2.c:6916-6995): a static string for every
+ * BLOSC2_ERROR_* code, "Unknown error" for anything else. */
+BLOSC_EXPORT const char *blosc2_error_string(int error_code);
+/* include/blosc2.h:524-528: the legacy spelling, header-inline as in the reference. */
+static char *print_error(int rc) __attribute__((unused));
+static char *print_error(int rc) { return (char *)blosc2_error_string(rc); }
+
+/* ---- timing helpers the reference's benchmarks use (include/blosc2.h:2600-2636,
+ * blosc/timestamp.c): a CLOCK_MONOTONIC timestamp and differences in ns / s. ---- */
+typedef struct timespec blosc_timestamp_t;
+BLOSC_EXPORT void blosc_set_timestamp(blosc_timestamp_t *timestamp);
+BLOSC_EXPORT double blosc_elapsed_nsecs(blosc_timestamp_t start_time, blosc_timestamp_t end_time);
+BLOSC_EXPORT double blosc_elapsed_secs(blosc_timestamp_t start_time, blosc_timestamp_t end_time);
 
 /* ---- context and parameter structs (ABI-identical to include/blosc2.h:1125-1248) ---- */
 typedef struct blosc2_context_s blosc2_context;
@@ -639,6 +723,13 @@ BLOSC_EXPORT int blosc2_schunk_get_lazychunk(blosc2_schunk *schunk, int64_t nchu
                                              bool *needs_free);
 /* include/blosc2.h:2275 (blosc/schunk.c:1662-1783) */
 BLOSC_EXPORT int blosc2_schunk_get_slice_buffer(blosc2_schunk *schunk, int64_t start, int64_t stop, void *buffer);
+/* include/blosc2.h:2290 (blosc/schunk.c:1922-2110): the items at `coords` (any order, repeats
+ * allowed) into buffer[i * typesize].  Same argument checks and error codes as the reference;
+ * under DELTA, a postfilter or one coordinate, one getitem per coordinate (schunk.c:1866-1900),
+ * otherwise every touched chunk is decoded once -- only its touched blocks, through a block mask
+ * (one device call per chunk instead of one per block). */
+BLOSC_EXPORT int blosc2_schunk_get_sparse_buffer(blosc2_schunk *schunk, int64_t ncoords, const int64_t *coords,
+                                                 void *buffer);
 /* include/blosc2.h:2304 (blosc/schunk.c:2146-2216): items [start, stop) of the super-chunk replaced by
  * `buffer`, every touched chunk recompressed through the super-chunk's cctx and updated in place. */
 BLOSC_EXPORT int blosc2_schunk_set_slice_buffer(blosc2_schunk *schunk, int64_t start, int64_t stop, void *buffer);

@@ -127,3 +127,71 @@ def test_special_chunk_creators_match_reference(ts, nbytes, blocksize):
             (getattr(R, fn)(rcp(typesize=ts), nbytes + (1 if ts > 1 else 0), C.c_void_p(a.ctypes.data), 64))
         assert getattr(L, fn)(B.cparams(typesize=ts), nbytes, C.c_void_p(a.ctypes.data), 31) == \
             getattr(R, fn)(rcp(typesize=ts), nbytes, C.c_void_p(a.ctypes.data), 31)
+
+
+def test_error_strings_match_reference():
+    """blosc2_error_string (reference blosc/blosc2.c:6916-6995) for every BLOSC2_ERROR_* code and
+    a few codes outside the table; print_error is the header-inline alias (include/blosc2.h)."""
+    from oracle_lib import ref
+    R = ref()
+    if R is None:
+        pytest.skip("reference build absent")
+    L = B.lib()
+    for lib in (L, R):
+        lib.blosc2_error_string.argtypes, lib.blosc2_error_string.restype = [C.c_int], C.c_char_p
+    for code in range(-45, 3):
+        assert L.blosc2_error_string(code) == R.blosc2_error_string(code), code
+    assert L.blosc2_error_string(-37) == b"Frame lock failure"
+    assert L.blosc2_error_string(0) == b"Unknown error"
+
+
+def test_timestamp_helpers_match_reference():
+    """blosc_set_timestamp / blosc_elapsed_nsecs / blosc_elapsed_secs (reference
+    include/blosc2.h:2600-2636, blosc/timestamp.c) on a struct timespec."""
+    from oracle_lib import ref
+    R = ref()
+    if R is None:
+        pytest.skip("reference build absent")
+
+    class TS(C.Structure):
+        _fields_ = [("tv_sec", C.c_long), ("tv_nsec", C.c_long)]
+    L = B.lib()
+    for lib in (L, R):
+        lib.blosc_set_timestamp.argtypes, lib.blosc_set_timestamp.restype = [C.POINTER(TS)], None
+        for fn in ("blosc_elapsed_nsecs", "blosc_elapsed_secs"):
+            getattr(lib, fn).argtypes, getattr(lib, fn).restype = [TS, TS], C.c_double
+    a, b = TS(5, 999_999_000), TS(7, 1_500)
+    for fn in ("blosc_elapsed_nsecs", "blosc_elapsed_secs"):
+        assert getattr(L, fn)(a, b) == getattr(R, fn)(a, b), fn
+        assert getattr(L, fn)(b, a) == getattr(R, fn)(b, a), fn
+    assert L.blosc_elapsed_nsecs(a, b) == 1_000_002_500.0
+    t0, t1 = TS(), TS()
+    L.blosc_set_timestamp(C.byref(t0))
+    L.blosc_set_timestamp(C.byref(t1))
+    assert 0.0 <= L.blosc_elapsed_secs(t0, t1) < 1.0
+
+
+# The reference's own C callers on the hot path (SURVEY §8b): each must compile against
+# include/blosc2.h and link against libblosc2.so with no undefined symbol.  b2bench.c is C1's
+# harness (bench/b2bench.c:171-231 times blosc1_compress / blosc1_decompress with
+# blosc_set_timestamp / blosc_elapsed_*).  Build container only: nothing of the reference travels.
+REF_CALLERS = ["bench/b2bench.c", "bench/delta_schunk.c", "bench/trunc_prec_schunk.c", "bench/sum_openmp.c",
+               "examples/simple.c", "examples/contexts.c", "examples/multithread.c", "examples/noinit.c",
+               "examples/schunk_simple.c", "examples/schunk_postfilter.c", "examples/delta_schunk_ex.c",
+               "examples/get_set_slice.c", "examples/urfilters.c", "examples/urcodecs.c",
+               "examples/get_blocksize.c", "examples/find_roots.c", "examples/frame_roundtrip.c",
+               "examples/frame_offset.c", "examples/frame_backed_schunk.c", "examples/compress_file.c",
+               "examples/decompress_file.c"]
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/bench"), reason="reference sources absent")
+@pytest.mark.parametrize("src", REF_CALLERS)
+def test_reference_callers_compile_and_link(src, tmp_path):
+    import subprocess
+    out = tmp_path / "a.out"
+    cmd = ["gcc", "-O1", "-Wall", "-Werror=implicit-function-declaration", "-I", os.path.join(REPO, "include"),
+           os.path.join("/root/reference", src), "-o", str(out), "-L", os.path.dirname(B.LIB_PATH), "-lblosc2",
+           "-lm", "-lpthread", "-fopenmp"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert out.exists()

@@ -125,3 +125,44 @@ def test_gpu_fanout_argument_errors():
     r0, _ = sc.decompress_chunk(0, 1000)
     assert st[0] == r0 < 0
     sc.free()
+
+
+@pytest.mark.parametrize("workers", [1, 2])
+def test_gpu_fanout_postfilter_over_groups(workers):
+    """A decompression context with a postfilter: every chunk of a range spanning
+    several 128 MiB staging groups must go through the postfilter (out = in * 2, the callback of
+    tests/plugins/b2h_prepost.c), none through the device-only staged path.  The staged decode
+    classifies group g + 1 on a helper thread while group g runs the postfilter path; the
+    postfilter field of the shared context is never rewritten during a call."""
+    import blosc2_amd as B
+    from b2ctypes import REPO
+    L = B.lib()
+    PP = C.CDLL(os.path.join(REPO, "tests", "plugins", "libb2h_prepost.so"))
+
+    class PPUser(C.Structure):
+        _fields_ = [("mode", C.c_int32), ("fail_block", C.c_int32), ("inputs", C.c_void_p * 2),
+                    ("nrec", C.c_int32), ("cap", C.c_int32), ("rec", C.c_void_p)]
+
+    class PostParams(C.Structure):
+        _fields_ = [("user_data", C.c_void_p), ("input", C.c_void_p), ("output", C.c_void_p),
+                    ("size", C.c_int32), ("typesize", C.c_int32), ("offset", C.c_int32),
+                    ("nchunk", C.c_int64), ("nblock", C.c_int32), ("tid", C.c_int32), ("ttmp", C.c_void_p),
+                    ("ttmp_nbytes", C.c_size_t), ("ctx", C.c_void_p)]
+    user = PPUser(0, -1, (C.c_void_p * 2)(None, None), 0, 0, None)   # no call record (threads)
+    post = PostParams()
+    post.user_data = C.cast(C.pointer(user), C.c_void_p)
+    dp = B.dparams()
+    dp.postfilter, dp.postparams = C.cast(PP.b2h_postfilter, C.c_void_p), C.cast(C.pointer(post), C.c_void_p)
+    chunk, n = 4 << 20, 72                     # 288 MiB: 3 groups for one worker
+    raw = (np.arange(n * chunk // 4, dtype=np.int32) % 100_003).view(np.uint8)
+    sizes = np.full(n, chunk, np.int32)
+    sc = B.SChunk(B.cparams(clevel=5, typesize=4, lz_mode=1), dp)
+    assert L.b2h_schunk_append_buffers(sc.p, _p(raw), _p(sizes), n, chunk, workers) == n
+    out = np.zeros(n * chunk, np.uint8)
+    st = np.zeros(n, np.int32)
+    assert L.b2h_schunk_decompress_buffers(sc.p, 0, n, _p(out), chunk, chunk, _p(st), workers) == 0
+    assert (st == chunk).all()
+    want = (raw.view(np.int32) * 2).view(np.uint8)
+    bad = [i for i in range(n) if not np.array_equal(out[i * chunk:(i + 1) * chunk], want[i * chunk:(i + 1) * chunk])]
+    assert not bad, bad[:8]
+    sc.free()

@@ -227,3 +227,80 @@ def test_frame_sparse_matches_reference(libs, frame):
         R.blosc2_schunk_get_sparse_buffer(frame["sc"], -1, None, p(out)) == -12
     assert L.b2h_frame_get_sparse_buffer(frame["fr"], 0, None, None) == 0
     assert L.b2h_frame_get_sparse_buffer(frame["fr"], 3, None, p(out)) == -12
+
+
+def test_schunk_sparse_buffer_matches_reference(libs, frame):
+    """blosc2_schunk_get_sparse_buffer on the reference's handle type (include/blosc2.h:2290,
+    blosc/schunk.c:1922-2110): this library's frame-attached handle (from_buffer copy=False) and
+    its in-memory copy (copy=True) against the reference's frame-backed handle on the same frame
+    -- the items, and the error codes of schunk.c:1923-1953."""
+    B, L, R = libs
+    vp, i64 = C.c_void_p, C.c_int64
+    L.blosc2_schunk_from_buffer.argtypes, L.blosc2_schunk_from_buffer.restype = [vp, i64, C.c_bool], vp
+    L.blosc2_schunk_free.argtypes, L.blosc2_schunk_free.restype = [vp], C.c_int
+    L.blosc2_schunk_get_sparse_buffer.argtypes = [vp, i64, vp, vp]
+    L.blosc2_schunk_get_sparse_buffer.restype = C.c_int
+    ts, data, fb = frame["ts"], frame["data"], frame["fbytes"]
+    nitems, cs = data.nbytes // ts, frame["chunksize"] // ts
+    rng = np.random.default_rng(31)
+    sets = [
+        rng.integers(0, nitems, 1),                                               # one: the getitem path
+        rng.integers(0, nitems, 1500),                                            # random, duplicates
+        np.concatenate([np.arange(cs - 40, cs + 40), [0, nitems - 1, 5, 5]]),     # clustered + repeats
+        np.arange(nitems - 1, -1, -max(1, nitems // 501)),                        # strided, descending
+        np.arange(0, nitems, 3),                                                  # every block of every chunk
+    ]
+    for copy in (False, True):
+        sc = L.blosc2_schunk_from_buffer(p(fb), fb.nbytes, copy)
+        assert sc
+        for coords in sets:
+            rc, got = _sparse(L, "blosc2_schunk_get_sparse_buffer", sc, coords, ts)
+            rrc, exp = _sparse(R, "blosc2_schunk_get_sparse_buffer", frame["sc"], coords, ts)
+            assert rc == rrc == 0, (copy, rc, rrc)
+            assert np.array_equal(got, exp), copy
+            assert np.array_equal(got, data.reshape(-1, ts)[np.asarray(coords, np.int64)].reshape(-1)), copy
+        for coords in ([nitems], [-1], [0, nitems + 5], [3, 4, -2]):
+            rc, _ = _sparse(L, "blosc2_schunk_get_sparse_buffer", sc, coords, ts)
+            rrc, _ = _sparse(R, "blosc2_schunk_get_sparse_buffer", frame["sc"], coords, ts)
+            assert rc == rrc == -12, (coords, rc, rrc)
+        out = np.zeros(64, np.uint8)
+        c3 = np.arange(3, dtype=np.int64)
+        for args in ((-1, None, p(out)), (0, None, None), (3, None, p(out)), (3, p(c3), None)):
+            assert L.blosc2_schunk_get_sparse_buffer(sc, *args) == R.blosc2_schunk_get_sparse_buffer(frame["sc"], *args), args
+        assert L.blosc2_schunk_free(sc) == 0
+    assert L.blosc2_schunk_get_sparse_buffer(None, 3, p(np.arange(3, dtype=np.int64)), p(np.zeros(64, np.uint8))) == \
+        R.blosc2_schunk_get_sparse_buffer(None, 3, p(np.arange(3, dtype=np.int64)), p(np.zeros(64, np.uint8))) == -12
+
+
+@pytest.mark.parametrize("filters", [(0, 0, 0, 0, 0, 1), (0, 0, 0, 0, 2, 1), (0, 0, 0, 0, 0, 2)],
+                         ids=["shuffle", "delta_shuffle", "bitshuffle"])
+def test_inmemory_schunk_sparse_buffer_matches_reference(libs, filters):
+    """The in-memory super-chunk (blosc2_schunk_new, sparse storage, append_buffer) of both
+    libraries, same cparams: sparse reads equal, including a zero-special chunk and a short last
+    chunk; DELTA takes the per-item getitem path (schunk.c:1944-1948)."""
+    B, L, R = libs
+    vp, i64 = C.c_void_p, C.c_int64
+    L.blosc2_schunk_get_sparse_buffer.argtypes = [vp, i64, vp, vp]
+    L.blosc2_schunk_get_sparse_buffer.restype = C.c_int
+    ts, chunk = 8, 1 << 17
+    raw = int64_ramp(41, 5 * chunk // 8 + 777).view(np.uint8).copy()
+    raw[2 * chunk:3 * chunk] = 0
+    kw = dict(typesize=ts, blocksize=16384, filters=filters, clevel=5)
+    ours = B.SChunk(B.cparams(**kw), B.dparams())
+    rst = Storage(False, None, C.pointer(ref_cparams(nthreads=1, **kw)), C.pointer(ref_dparams(nthreads=1)), None)
+    theirs = R.blosc2_schunk_new(C.byref(rst))
+    for pos in range(0, raw.nbytes, chunk):
+        a = raw[pos:pos + chunk].copy()
+        assert ours.append_buffer(a) > 0
+        assert R.blosc2_schunk_append_buffer(theirs, p(a), a.nbytes) > 0
+    nitems = raw.nbytes // ts
+    rng = np.random.default_rng(5)
+    for coords in (rng.integers(0, nitems, 2000), np.arange(nitems - 1, 0, -97), [7]):
+        rc, got = _sparse(L, "blosc2_schunk_get_sparse_buffer", ours.p, coords, ts)
+        rrc, exp = _sparse(R, "blosc2_schunk_get_sparse_buffer", theirs, coords, ts)
+        assert rc == rrc == 0, (rc, rrc)
+        assert np.array_equal(got, exp)
+        if 2 not in filters:
+            assert np.array_equal(got, raw.reshape(-1, ts)[np.asarray(coords, np.int64)].reshape(-1))
+    ours.free()
+    R.blosc2_schunk_free(theirs)
