@@ -232,8 +232,9 @@ def test_frame_sparse_matches_reference(libs, frame):
 def test_schunk_sparse_buffer_matches_reference(libs, frame):
     """blosc2_schunk_get_sparse_buffer on the reference's handle type (include/blosc2.h:2290,
     blosc/schunk.c:1922-2110): this library's frame-attached handle (from_buffer copy=False) and
-    its in-memory copy (copy=True) against the reference's frame-backed handle on the same frame
-    -- the items, and the error codes of schunk.c:1923-1953."""
+    its in-memory copy (copy=True) against the reference's handle of the same flavour on the same
+    frame -- the items, and the error codes of schunk.c:1923-1953 (a copy whose chunks have
+    different blocksizes has blocksize 0: INVALID_PARAM in both)."""
     B, L, R = libs
     vp, i64 = C.c_void_p, C.c_int64
     L.blosc2_schunk_from_buffer.argtypes, L.blosc2_schunk_from_buffer.restype = [vp, i64, C.c_bool], vp
@@ -252,22 +253,28 @@ def test_schunk_sparse_buffer_matches_reference(libs, frame):
     ]
     for copy in (False, True):
         sc = L.blosc2_schunk_from_buffer(p(fb), fb.nbytes, copy)
-        assert sc
+        rsc = R.blosc2_schunk_from_buffer(p(fb), fb.nbytes, copy)
+        assert sc and rsc
         for coords in sets:
             rc, got = _sparse(L, "blosc2_schunk_get_sparse_buffer", sc, coords, ts)
-            rrc, exp = _sparse(R, "blosc2_schunk_get_sparse_buffer", frame["sc"], coords, ts)
-            assert rc == rrc == 0, (copy, rc, rrc)
+            rrc, exp = _sparse(R, "blosc2_schunk_get_sparse_buffer", rsc, coords, ts)
+            assert rc == rrc, (copy, rc, rrc)
+            if rc < 0:
+                continue
             assert np.array_equal(got, exp), copy
             assert np.array_equal(got, data.reshape(-1, ts)[np.asarray(coords, np.int64)].reshape(-1)), copy
+        if not copy:   # the attached handle always has the frame's blocksize: every set decodes
+            assert _sparse(L, "blosc2_schunk_get_sparse_buffer", sc, sets[1], ts)[0] == 0
         for coords in ([nitems], [-1], [0, nitems + 5], [3, 4, -2]):
             rc, _ = _sparse(L, "blosc2_schunk_get_sparse_buffer", sc, coords, ts)
-            rrc, _ = _sparse(R, "blosc2_schunk_get_sparse_buffer", frame["sc"], coords, ts)
+            rrc, _ = _sparse(R, "blosc2_schunk_get_sparse_buffer", rsc, coords, ts)
             assert rc == rrc == -12, (coords, rc, rrc)
         out = np.zeros(64, np.uint8)
         c3 = np.arange(3, dtype=np.int64)
         for args in ((-1, None, p(out)), (0, None, None), (3, None, p(out)), (3, p(c3), None)):
-            assert L.blosc2_schunk_get_sparse_buffer(sc, *args) == R.blosc2_schunk_get_sparse_buffer(frame["sc"], *args), args
+            assert L.blosc2_schunk_get_sparse_buffer(sc, *args) == R.blosc2_schunk_get_sparse_buffer(rsc, *args), args
         assert L.blosc2_schunk_free(sc) == 0
+        R.blosc2_schunk_free(rsc)
     assert L.blosc2_schunk_get_sparse_buffer(None, 3, p(np.arange(3, dtype=np.int64)), p(np.zeros(64, np.uint8))) == \
         R.blosc2_schunk_get_sparse_buffer(None, 3, p(np.arange(3, dtype=np.int64)), p(np.zeros(64, np.uint8))) == -12
 
