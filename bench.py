@@ -274,7 +274,7 @@ def parse(argv=None):
     ap.add_argument("--chunks", type=int, default=None, help="chunks per GPU (T) / in the super-chunk (C5)")
     ap.add_argument("--chunk-mib", type=int, default=None)
     ap.add_argument("--clevel", type=int, default=5)
-    ap.add_argument("--lz-mode", default="both", choices=["exact", "fast", "deep", "both"],
+    ap.add_argument("--lz-mode", default="both", choices=["exact", "fast", "deep", "seg", "both"],
                     help="BloscLZ encoder: exact (byte-identical to the reference), fast (cparams.codec_params), "
                          "or both (exact measured beside the fast headline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -366,7 +366,7 @@ def run(args):
     cbytes = torch.zeros(nch, dtype=torch.int32, device=dev)
     out = torch.empty(shard, dtype=torch.uint8, device=dev)
     status = torch.zeros(nch, dtype=torch.int32, device=dev)
-    cps = {m: B.cparams(**kw, lz_mode=m) for m in (0, 1, 2)}   # per-context encoder (cparams.codec_params)
+    cps = {m: B.cparams(**kw, lz_mode=m) for m in (0, 1, 2, 3)}   # per-context encoder (cparams.codec_params)
     cp = cps[0]
     ncpu = nch if args.workload == "T" else min(nch, 1000)
     pick = np.linspace(0, max(0, ncpu - 1), min(ncpu, 128)).astype(np.int64)   # chunks the CPU leg checks
@@ -424,7 +424,7 @@ def run(args):
         return {"elapsed": float(el.item()), "t_c": float(np.mean(spans[0::2])), "t_d": float(np.mean(spans[1::2])),
                 "enc": float(np.mean(enc_ms)), "dec": float(np.mean(dec_ms)), "total_c": total_c, "sample": sample}
 
-    modes = {"exact": [0], "fast": [1], "deep": [2], "both": [0, 1]}[args.lz_mode]
+    modes = {"exact": [0], "fast": [1], "deep": [2], "seg": [3], "both": [0, 1]}[args.lz_mode]
     meas = {m: measure(m) for m in modes}
     head = meas[modes[-1]]                     # the headline: fast when measured
     total_c = head["total_c"]
@@ -455,13 +455,15 @@ def run(args):
                     "encode_ms": round(m["enc"], 3), "decode_ms": round(m["dec"], 3)}
         enc, dec, Cb = head["enc"], head["dec"], head["total_c"]
         t_c, t_d = head["t_c"], head["t_d"]
-        MODE_NAMES = {0: "exact", 1: "fast", 2: "deep"}
+        MODE_NAMES = {0: "exact", 1: "fast", 2: "deep", 3: "seg"}
         lz_name = MODE_NAMES[modes[-1]]
         # the encoder kernel of the headline mode (rocprof names: k_encode_fast / k_encode)
         # fast mode runs shuffle + encode + finalize + scatter as ONE launch, k_encode_fast_fused
         # (B2H_FUSE, c-blosc2_amd/csrc/b2h_engine.hip); B2H_FUSE=0 restores the separate launches
         fused = lz_name != "exact" and int(os.environ.get("B2H_FUSE", "83")) & 1
         enc_name = ("k_encode_fast_fused" if fused else "k_encode_fast") if lz_name != "exact" else "k_encode"
+        if lz_name == "seg":
+            enc_name = "k_encode_seg"
         dominant = enc_name if enc >= dec else "k_decode"
         kms = enc if enc >= dec else dec
         achieved = (N + Cb) / (kms * 1e-3) / 1e9     # algorithmic bytes of one launch: N + C
@@ -506,7 +508,7 @@ def run(args):
         if world == 1 and not args.no_cpu_baseline:
             host = src_u8.cpu().numpy()
             ex = meas.get(0, {}).get("sample", {})
-            res["cpu_baseline"] = cpu_baseline(host, chunk, ncpu, kw, ex, meas.get(1, meas.get(2, {})).get("sample", {}),
+            res["cpu_baseline"] = cpu_baseline(host, chunk, ncpu, kw, ex, meas.get(1, meas.get(2, meas.get(3, {}))).get("sample", {}),
                                                reps=5 if args.workload == "T" else 3)
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -39,7 +39,7 @@ class DParams(C.Structure):
 
 
 B2H_CODEC_PARAMS_MAGIC = 0x68623262
-EXACT, FAST, DEEP = 0, 1, 2   # BloscLZ encoder modes (include/b2h.h b2h_codec_params)
+EXACT, FAST, DEEP, SEG = 0, 1, 2, 3   # BloscLZ encoder modes (include/b2h.h b2h_codec_params)
 
 
 class CodecParams(C.Structure):

@@ -131,6 +131,7 @@ void enable_timing(bool on);
 int debug_stream_results(void* host, int32_t n);
 int debug_decode_cycles(void* host, int32_t n);
 int debug_fuse_timed_out();
+int debug_seg_prof(uint64_t* host);
 KernelTimes last_times();   // the latest batch (waits for its events)
 KernelTimes mean_times();   // mean over every batch since enable_timing(true)
 

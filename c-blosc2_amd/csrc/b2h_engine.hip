@@ -26,6 +26,7 @@
 
 #include "b2h_engine.h"
 #include "b2h_filters.h"
+#include "b2h_lzseg.h"
 #include "b2h_format.h"
 #include "b2h_lz.h"
 #include "b2h_lzfast.h"
@@ -180,6 +181,21 @@ int debug_stream_results(void* host, int32_t n) {
   if (ws->used && ws->done) HIPCHK(hipEventSynchronize(ws->done));
   HIPCHK(hipMemcpy(host, ws->res.p, (size_t)n * sizeof(StreamResult), hipMemcpyDeviceToHost));
   return n;
+}
+
+// Diagnostics: BloscLZ mode 3's per-phase cycle sums (a -DB2H_SEG_PROF build; zeros otherwise), reset after
+// the copy.  [0..7] probe pass, [8..15] emitting pass: candidates, counting walks, emitting walk,
+// rounds, passes, max steps per lane; [16] run tests, [17] streams.
+int debug_seg_prof(uint64_t* host) {
+#ifdef B2H_SEG_PROF
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_seg_prof), 32 * sizeof(uint64_t)));
+  static const uint64_t zero[32] = {};
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_seg_prof), zero, sizeof zero));
+#else
+  memset(host, 0, 32 * sizeof(uint64_t));
+#endif
+  return 32;
 }
 
 // Diagnostics: whether the last fused encode launch on this device's default workspace hit a
@@ -639,13 +655,13 @@ static int g_lz_mode = -1;
 static int lz_mode() {
   if (g_lz_mode < 0) {
     const char* e = getenv("B2H_LZ_MODE");
-    g_lz_mode = (e && !strcmp(e, "fast")) ? 1 : (e && !strcmp(e, "deep")) ? 2 : 0;
+    g_lz_mode = (e && !strcmp(e, "fast")) ? 1 : (e && !strcmp(e, "deep")) ? 2 : (e && !strcmp(e, "seg")) ? 3 : 0;
   }
   return g_lz_mode;
 }
 int set_blosclz_mode(int mode) {
   const int old = lz_mode();
-  if (mode >= 0 && mode <= 2) g_lz_mode = mode;
+  if (mode >= 0 && mode <= 3) g_lz_mode = mode;
   return old;
 }
 static int fast_tablog() {
@@ -700,6 +716,89 @@ static int launch_encode_fast(Workspace* ws, const CGeom& g, const uint8_t* filt
                  : launch_encode_fast_t<uint32_t, true>(ws, g, filt, res, ntot, next, porder, st);
   return small ? launch_encode_fast_t<uint16_t, false>(ws, g, filt, res, ntot, next, porder, st)
                : launch_encode_fast_t<uint32_t, false>(ws, g, filt, res, ntot, next, porder, st);
+}
+
+// ----------------------------------------------------- BloscLZ mode 3: segmented parse ----
+// One wave per workgroup and stream (b2h_lzseg.h): the LDS holds the stream's u16 table only while
+// the candidates are exchanged; the distances and masks live in this workgroup's global scratch.
+// W waves per workgroup, each encoding its own streams; they share the workgroup's one candidate
+// table under an LDS lock (b2h_lzseg.h seg_lock).
+template <bool CHK, int W>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_encode_seg(CGeom g, const uint8_t* __restrict__ filt, uint8_t* __restrict__ sbuf,
+                                                       StreamResult* __restrict__ res, int32_t nstreams_total,
+                                                       int32_t* __restrict__ next, int tablog,
+                                                       const int32_t* __restrict__ porder) {
+  if (gated_off(g)) return;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  B2H_LDS uint8_t* tab = (B2H_LDS uint8_t*)smem;
+  const int64_t sb = seg_scratch_bytes(chain_len(g));
+  int32_t* lock = reinterpret_cast<int32_t*>(g.chain + (int64_t)gridDim.x * W * sb) + 64 * blockIdx.x;
+  if (threadIdx.x == 0) atomicExch(lock, 0);
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* mine = g.chain + ((int64_t)blockIdx.x * W + wave) * sb;
+  B2H_GLB uint32_t* dist = (B2H_GLB uint32_t*)mine;
+  B2H_GLB uint64_t* mask = (B2H_GLB uint64_t*)(mine + seg_dist_bytes(chain_len(g)));
+  B2H_GLB uint32_t* snv = (B2H_GLB uint32_t*)(mine + seg_dist_bytes(chain_len(g)) + seg_mask_bytes(chain_len(g)));
+  auto pull = [&]() {
+    int32_t v = 0;
+    if (lane_id() == 0) v = atomicAdd(next, 1);
+    return __shfl(v, 0);
+  };
+  for (int32_t i = pull(); i < nstreams_total; i = pull()) {
+    const int32_t s = __builtin_amdgcn_readfirstlane(pull_to_stream(g, porder, g.front, i, nstreams_total));
+    const int32_t c = s / g.nsc, l = s - c * g.nsc;
+    int32_t off, len, blk;
+    stream_locate(g, l, &off, &len, &blk);
+    gin_t in = (gin_t)(filt + (int64_t)c * g.wstride + off);
+    gout_t out = (gout_t)(sbuf + (int64_t)c * g.wstride + off);
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+    StreamResult r = encode_stream_seg<false, CHK>(in, len, g.clevel, out, tab, tablog, dist, mask, snv,
+                                                   g.overhead == kHdrExt, lock);
+    r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
+    r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
+    if (lane_id() == 0) res[s] = r;
+  }
+}
+
+template <bool CHK, int W>
+static int launch_encode_seg_t(Workspace* ws, const CGeom& g0, const uint8_t* filt, StreamResult* res, int64_t ntot,
+                               int32_t* next, const int32_t* porder, hipStream_t st, int tablog) {
+  CGeom g = g0;
+  const size_t lds = CHK ? (size_t)4 << tablog : (size_t)2 << tablog;
+  const void* fn = reinterpret_cast<const void*>(&k_encode_seg<CHK, W>);
+  const int slots = resident_slots(fn, lds, 64 * W);
+  const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>((ntot + W - 1) / W, slots));
+  const int64_t sb = seg_scratch_bytes(chain_len(g));
+  if (ws->fchain.ensure((size_t)grid * W * (size_t)sb + (size_t)grid * 256 + 256)) return E_MEMORY;   // + lock words
+  g.chain = ws->fchain.as<uint8_t>();
+  k_encode_seg<CHK, W><<<grid, 64 * W, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog, porder);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// BloscLZ mode 3.  Streams of <= 2^16 positions: u32 table entries with a check of the hashed value
+// (no candidate reads); longer streams: u16 entries (their aliasing rule reads the candidates).
+// B2H_SEG_WAVES (1..4, default 3): waves per workgroup sharing one table.
+static int launch_encode_seg(Workspace* ws, const CGeom& g, const uint8_t* filt, StreamResult* res, int64_t ntot,
+                             int32_t* next, const int32_t* porder, hipStream_t st) {
+  const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
+  const int tablog = std::min(fast_tablog(), hashlog);
+  static const int W = [] { const char* e = getenv("B2H_SEG_WAVES"); return e ? std::max(1, std::min(4, atoi(e))) : 3; }();
+  const bool chk = chain_len(g) <= 65536;
+#define B2H_SEG_LAUNCH(C, WW) return launch_encode_seg_t<C, WW>(ws, g, filt, res, ntot, next, porder, st, tablog)
+  if (chk) {
+    if (W == 1) B2H_SEG_LAUNCH(true, 1);
+    if (W == 2) B2H_SEG_LAUNCH(true, 2);
+    if (W == 3) B2H_SEG_LAUNCH(true, 3);
+    B2H_SEG_LAUNCH(true, 4);
+  }
+  if (W == 1) B2H_SEG_LAUNCH(false, 1);
+  if (W == 2) B2H_SEG_LAUNCH(false, 2);
+  if (W == 3) B2H_SEG_LAUNCH(false, 3);
+  B2H_SEG_LAUNCH(false, 4);
+#undef B2H_SEG_LAUNCH
 }
 
 // ------------------------------------------------------------------------ LZ4 encoder ----
@@ -2109,7 +2208,7 @@ static int launch_encode_fast_fused_t(Workspace* ws, const CGeom& g0, const uint
 // results fit the LDS table (the finalizing workgroup stages them there).
 static void enc_mode(int* nlds, int* nglb);
 static bool fused_encode_ok(const CGeom& g) {
-  if (!fuse_enabled() || g.compcode != 0 || g.dict_size) return false;
+  if (!fuse_enabled() || g.compcode != 0 || g.dict_size || g.lzmode == 3) return false;
   if (g.lzmode == 0) {   // exact mode: only with bit 4 (measured slower), the default k_encode shape
     if (!(fuse_bits() & 4)) return false;
     int nl, ng;
@@ -2594,7 +2693,7 @@ static CGeom make_geom(const CompressPlan& P, int64_t src_stride, int64_t dst_st
   g.overhead = P.overhead;
   g.compcode = P.compcode;
   g.dict_size = P.use_dict ? P.dict_size : 0;
-  g.lzmode = (P.lz_mode >= 0 && P.lz_mode <= 2) ? P.lz_mode : lz_mode();
+  g.lzmode = (P.lz_mode >= 0 && P.lz_mode <= 3) ? P.lz_mode : lz_mode();
   g.src_stride = src_stride;
   g.dst_stride = dst_stride;
   g.wstride = ((int64_t)n + 255) / 256 * 256 + 256;
@@ -2835,7 +2934,8 @@ static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const ui
       if (g.lzmode != 0) rc = launch_encode_fast_fused(ws, g, filt, res, ntot, next, porder, f, st);
       else rc = small ? launch_encode_exact_fused<uint16_t>(ws, g, hashlog, filt, res, ntot, next, porder, f, st)
                       : launch_encode_exact_fused<uint32_t>(ws, g, hashlog, filt, res, ntot, next, porder, f, st);
-    } else if (g.lzmode != 0) rc = launch_encode_fast(ws, g, filt, res, ntot, next, porder, st);
+    } else if (g.lzmode == 3) rc = launch_encode_seg(ws, g, filt, res, ntot, next, porder, st);
+    else if (g.lzmode != 0) rc = launch_encode_fast(ws, g, filt, res, ntot, next, porder, st);
     else rc = small ? launch_encode<uint16_t>(ws, g, hashlog, filt, res, ntot, next, porder, st)
                     : launch_encode<uint32_t>(ws, g, hashlog, filt, res, ntot, next, porder, st);
     if (rc) return rc;

@@ -181,7 +181,7 @@ int codec_params_lz_mode(const void* codec_params) {
   if (!codec_params) return -1;
   const b2h_codec_params* p = static_cast<const b2h_codec_params*>(codec_params);
   if (p->magic != B2H_CODEC_PARAMS_MAGIC) return -1;
-  return (p->blosclz_mode >= 0 && p->blosclz_mode <= 2) ? p->blosclz_mode : -1;
+  return (p->blosclz_mode >= 0 && p->blosclz_mode <= 3) ? p->blosclz_mode : -1;
 }
 }  // namespace b2h
 
@@ -2247,6 +2247,7 @@ void b2h_mean_times(float out[5]) {
 }
 const char* b2h_last_error(void) { return b2h::last_error(); }
 int b2h_debug_stream_results(void* host, int32_t n) { return b2h::debug_stream_results(host, n); }
+int b2h_debug_seg_prof(uint64_t* host) { return b2h::debug_seg_prof(host); }
 int b2h_debug_decode_cycles(void* host, int32_t n) { return b2h::debug_decode_cycles(host, n); }
 int b2h_debug_fuse_timed_out(void) { return b2h::debug_fuse_timed_out(); }
 int b2h_device_count(void) { return b2h::device_count(); }

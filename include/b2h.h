@@ -202,6 +202,9 @@ BLOSC_EXPORT const char *b2h_last_error(void);
 /* Diagnostics: per-stream encoder records of the last compression batch on this device
  * ({kind, size, peak, windows, int64 cycles} x n). Returns n or < 0. Synchronous. */
 BLOSC_EXPORT int b2h_debug_stream_results(void *host, int32_t n);
+/* Diagnostics: BloscLZ mode 3's per-phase cycle sums since the last call (32 x uint64; zeros unless
+ * the library was built with -DB2H_SEG_PROF).  Returns 32. Synchronous. */
+BLOSC_EXPORT int b2h_debug_seg_prof(uint64_t *host);
 /* Diagnostics (B2H_DECODE_DEBUG=1 only): {int64 cycles, int64 kind} per stream of the last
  * decompression batch.  Returns n or < 0. Synchronous. */
 BLOSC_EXPORT int b2h_debug_decode_cycles(void *host, int32_t n);

@@ -39,19 +39,23 @@ def fm():
     L.fm_probe_ratio.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_int]
     L.fm_probe_ratio.restype = C.c_double
     L.fm_set_depth.argtypes = [C.c_int]
+    L.fm_set_noskip.argtypes = [C.c_int]
     return L
 
 
-def fm_compress(stream, clevel, maxout=None, tablog=TABLOG, depth=1):
-    """The model's stream; depth 8 = the engine's BloscLZ mode 2 (deep candidates)."""
+def fm_compress(stream, clevel, maxout=None, tablog=TABLOG, depth=1, noskip=False):
+    """The model's stream; depth 8 = the engine's BloscLZ mode 2 (deep candidates); noskip = mode 3
+    (every position inserted in order: the serial parse the segmented walk reproduces)."""
     n = stream.nbytes
     out = np.zeros(n + 64, np.uint8)
     L = fm()
     L.fm_set_depth(depth)
+    L.fm_set_noskip(1 if noskip else 0)
     try:
         m = L.fm_blosclz_compress(clevel, p(stream), n, p(out), n if maxout is None else maxout, tablog)
     finally:
         L.fm_set_depth(1)
+        L.fm_set_noskip(0)
     return out[:m] if m > 0 else None
 
 
@@ -267,10 +271,11 @@ CASES = [
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", [1, 2], ids=["fast", "deep"])
+@pytest.mark.parametrize("mode", [1, 2, 3], ids=["fast", "deep", "seg"])
 @pytest.mark.parametrize("name,mk,kw", CASES, ids=[c[0] for c in CASES])
 def test_gpu_fast_streams_match_model(fast, name, mk, kw, mode):
-    """Every LZ stream the kernel writes equals the model's (mode 2: the model at depth 8)."""
+    """Every LZ stream the kernel writes equals the model's (mode 2: the model at depth 8; mode 3:
+    the model with every position inserted in order, fm_set_noskip)."""
     B = fast
     src = mk()
     raw = src.view(np.uint8).reshape(-1)
@@ -288,7 +293,7 @@ def test_gpu_fast_streams_match_model(fast, name, mk, kw, mode):
     n_lz = 0
     for k, ((nb, cs, pl), s) in enumerate(zip(streams, filt)):
         assert nb == s.nbytes
-        model = fm_compress(s, kw["clevel"], depth=8 if mode == 2 else 1)
+        model = fm_compress(s, kw["clevel"], depth=8 if mode == 2 else 1, noskip=mode == 3)
         if 0 < cs < nb:
             n_lz += 1
             assert model is not None and np.array_equal(pl, model), (name, k, cs)
@@ -309,8 +314,9 @@ def test_gpu_fast_streams_match_model(fast, name, mk, kw, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lzmode", [1, 3], ids=["fast", "seg"])
 @pytest.mark.parametrize("seed", range(4))
-def test_gpu_fast_random_chunks_roundtrip(fast, seed):
+def test_gpu_fast_random_chunks_roundtrip(fast, seed, lzmode):
     """Random pipelines / sizes / clevels (the exact-mode grid of test_gpu_parity) in fast mode:
     round trip through the oracle decoder and the device; tight destsize keeps the serial
     maxout rule working (0 / memcpy fallbacks, never an overrun)."""
@@ -318,7 +324,7 @@ def test_gpu_fast_random_chunks_roundtrip(fast, seed):
     B = fast
     for src, kw in _cases(100 + seed, 10):
         raw = src.view(np.uint8).reshape(-1)
-        got = B.compress(src, **kw, lz_mode=B.FAST)
+        got = B.compress(src, **kw, lz_mode=lzmode)
         assert isinstance(got, np.ndarray), kw
         lossless = kw["filters"][4] != 4
         dec = oracle_decompress(got, raw.nbytes)
@@ -345,7 +351,7 @@ def test_gpu_fast_ratio_T(fast):
     cap = chunk + 32
     stride = (cap + 255) // 256 * 256
     sizes = {}
-    for mode in (0, 1):
+    for mode in (0, 1, 3):
         cp = B.cparams(clevel=5, typesize=4, lz_mode=mode)
         comp = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
         cb = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -357,6 +363,7 @@ def test_gpu_fast_ratio_T(fast):
         assert torch.equal(out, src) and bool((st == chunk).all())
         sizes[mode] = int(cb.to(torch.int64).sum())
     assert sizes[1] <= sizes[0] * 1.001, sizes
+    assert sizes[3] <= sizes[0] * 1.001, sizes
 
 
 @pytest.mark.gpu
@@ -653,3 +660,32 @@ def test_gpu_fused_uniform_stream_batches(fast, lzmode, kind, grid, monkeypatch)
     for i, (a, b) in enumerate(zip(out["83"], out["0"])):
         assert np.array_equal(a, b), i
     assert np.array_equal(B.decompress(np.concatenate([out["83"][0]]), chunk), host[:chunk])
+
+
+@pytest.mark.parametrize("data", ["T", "C3", "C1", "C4"])
+def test_model_noskip_ratio_and_decode(data):
+    """BloscLZ mode 3's semantics (every position inserted in order, fm_set_noskip) against exact
+    mode's stream bytes: T <= 1.001 x exact (measured 1.0004), C3 <= 1.0025 x (1.0019), C1 / C4 as
+    the ratio-pinning tests above allow; every stream decodes with the reference decoder's
+    restatement."""
+    from datagen import b2bench_values
+    O = oracle()
+    if data == "T":
+        streams, cap = shuffled_planes(gen_f32(0, 2 << 20).view(np.uint8)), 1.001
+    elif data == "C3":
+        streams, cap = _bitshuffled_blocks(gen_f32(77, 1 << 20).view(np.uint8)), 1.0025
+    elif data == "C1":
+        streams, cap = shuffled_planes(b2bench_values(1 << 19, 19).view(np.uint8)), 1.75
+    else:
+        raw = int64_ramp(0, 1 << 17).view(np.uint8)
+        streams, cap = shuffled_planes(raw, ts=8), 1.01
+    ex = fa = 0
+    for s in streams:
+        z = fm_compress(s, 5, noskip=True)
+        ex += _exact_size(s)
+        fa += (z.nbytes if z is not None else s.nbytes) + 4
+        if z is not None:
+            back = np.zeros(s.nbytes, np.uint8)
+            assert O.or_blosclz_decompress(p(z), z.nbytes, p(back), s.nbytes) == s.nbytes
+            assert np.array_equal(back, s)
+    assert fa <= ex * cap, (data, ex, fa, fa / ex)

@@ -261,3 +261,146 @@ double fm_probe_ratio(int clevel, const uint8_t *in, int length, int tablog_max)
   fm_parse(in + (length - maxlen), maxlen, tablog, 1, 1 << hashlog, NULL, 0, &ratio);
   return ratio;
 }
+
+/* ==================================================================== segmented fast mode ====
+ * fm_set_segment(S), S > 0 (the engine's BloscLZ mode 3, "segmented"): the parse no longer walks
+ * the stream as one greedy chain.  Candidates: EVERY position p < loop_end is inserted in order
+ * (cand[p] = the bucket's previous position, the u16 rule above), so the candidate array is a
+ * function of the input alone.  The stream is cut into segments of S bytes; segment k covers
+ * [k S, min((k + 1) S, limit)) and is parsed greedily on its own (the GPU kernel gives each
+ * segment a lane): it starts a fresh literal run at its first byte (segment 0: the reference's
+ * four initial literals), a match never covers bytes past the segment's end (its length is cut
+ * there: e <= seg_end + 2, and a cut match shorter than LZ_MINLEN becomes a literal), and every
+ * rule inside a segment is fm_parse's.  The segments' token streams, each closed as the reference
+ * closes a stream (an open literal run's header written, an unused reserved header dropped), are
+ * concatenated: BloscLZ tokens are self-delimiting and a match may reference any earlier byte, so
+ * blosclz_decompress decodes the result (a literal run may now be followed by another one).
+ * The probe counts the same way per segment over the probe window; its ratio is the window's
+ * parsed length over the summed counts.  Output: 0 when the concatenation is longer than maxout. */
+static int fm_segment = 0;
+void fm_set_segment(int s) { fm_segment = s < 0 ? 0 : s; }
+
+static int fm3_parse(const uint8_t *in, int32_t length, int tablog, int probe, int32_t probe_limit, uint8_t *out,
+                     int32_t maxout, double *ratio) {
+  int32_t limit = length;
+  if (probe && limit > probe_limit) limit = probe_limit;
+  const int32_t bound = limit - 1, loop_end = limit - 12, S = fm_segment;
+  uint32_t *tab = (uint32_t *)calloc((size_t)1 << tablog, sizeof(uint32_t));
+  int32_t *cand = (int32_t *)calloc((size_t)(limit > 0 ? limit : 1), sizeof(int32_t));
+  for (int32_t p = 0; p < loop_end; p++) {   /* every position, in order */
+    const uint32_t h = lz_hash(ld32(in + p), tablog);
+    int32_t c1 = p - (int32_t)(((uint32_t)p - tab[h]) & 0xffffu);
+    tab[h] = (uint32_t)p & 0xffffu;
+    if (c1 >= 65536 && p - c1 < LZ_FAR - 65536 && ld32(in + c1) != ld32(in + p)) c1 -= 65536;
+    cand[p] = c1;
+  }
+  free(tab);
+  uint8_t *seg = probe ? NULL : (uint8_t *)malloc((size_t)S + (size_t)S / 16 + 64);
+  int64_t total = 0;
+  int32_t last_pos = 0;
+  int fail = 0;
+  const int32_t nseg = limit > 0 ? (limit + S - 1) / S : 0;
+  for (int32_t k = 0; k < nseg && !fail; k++) {
+    const int32_t s0 = k * S, s1 = (k + 1) * S < limit ? (k + 1) * S : limit;
+    const int32_t walk_end = s1 < loop_end ? s1 : loop_end;
+    const int32_t emax = s1 + 2 < bound ? s1 + 2 : bound;
+    int32_t o, lit, pos;
+    if (k == 0) {
+      o = 5; lit = 4; pos = probe ? 0 : 4;
+      if (!probe) { seg[0] = LZ_MAX_COPY - 1; for (int i = 0; i < 4; i++) seg[1 + i] = in[i]; }
+    } else {
+      o = 1; lit = 0; pos = s0;
+      if (!probe) seg[0] = LZ_MAX_COPY - 1;
+    }
+    while (pos < walk_end) {
+      const int32_t anchor = pos;
+      const int32_t ref = cand[anchor];
+      uint32_t dist = (uint32_t)(anchor - ref);
+      int literal = (dist == 0 || dist >= LZ_FAR) || ld32(in + ref) != ld32(in + anchor);
+      int32_t len = 0;
+      if (!literal) {
+        dist--;
+        len = lz_match_end(in, anchor + 4, ref + 4, emax) - LZ_SHIFT - anchor;
+        if (len < LZ_MINLEN) literal = 1;
+        else if (!probe && len <= 5 && dist >= LZ_NEAR) literal = 1;
+      }
+      if (literal) {
+        if (probe) o++; else seg[o++] = in[anchor];
+        pos = anchor + 1;
+        if (++lit == LZ_MAX_COPY) {
+          lit = 0;
+          if (probe) o++; else seg[o++] = LZ_MAX_COPY - 1;
+        }
+        continue;
+      }
+      if (probe) {
+        if (!lit) o--;
+      } else {
+        if (lit) seg[o - lit - 1] = (uint8_t)(lit - 1);
+        else o--;
+      }
+      lit = 0;
+      const uint32_t ulen = (uint32_t)len;
+      if (probe) {
+        if (ulen >= 7) o += (int32_t)((ulen - 7) / 255) + 1;
+        o += dist < LZ_NEAR ? 2 : 4;
+        o++;
+      } else {
+        const int far = dist >= LZ_NEAR;
+        const uint32_t d = far ? dist - LZ_NEAR : dist;
+        if (ulen < 7) {
+          seg[o++] = (uint8_t)((ulen << 5) + (far ? 31 : (d >> 8)));
+        } else {
+          seg[o++] = (uint8_t)((7u << 5) + (far ? 31 : (d >> 8)));
+          uint32_t rem = ulen - 7;
+          for (; rem >= 255; rem -= 255) seg[o++] = 255;
+          seg[o++] = (uint8_t)rem;
+        }
+        if (far) { seg[o++] = 255; seg[o++] = (uint8_t)(d >> 8); }
+        seg[o++] = (uint8_t)(d & 255);
+        seg[o++] = LZ_MAX_COPY - 1;
+      }
+      pos = anchor + len + 2;
+    }
+    if (probe) {
+      total += o;
+      last_pos = pos;
+      continue;
+    }
+    for (; pos < s1; pos++) {   /* the stream's tail (past loop_end): literals */
+      seg[o++] = in[pos];
+      if (++lit == LZ_MAX_COPY) { lit = 0; seg[o++] = LZ_MAX_COPY - 1; }
+    }
+    if (lit) seg[o - lit - 1] = (uint8_t)(lit - 1);
+    else o--;
+    if (total + o > maxout) { fail = 1; break; }
+    memcpy(out + total, seg, (size_t)o);
+    total += o;
+  }
+  free(cand);
+  free(seg);
+  if (probe) {
+    *ratio = total > 0 ? (double)last_pos / (double)total : 0.0;
+    return 0;
+  }
+  if (fail || total == 0) return 0;
+  out[0] |= 1u << 5;
+  return (int)total;
+}
+
+/* fm_blosclz_compress with the segmented parse (fm_set_segment(S) first). */
+int fm3_blosclz_compress(int clevel, const uint8_t *in, int length, uint8_t *out, int maxout, int tablog_max) {
+  static const uint8_t hashlogs[10] = {0, 12, 13, 14, 14, 14, 14, 14, 14, 14};
+  static const double min_ratio[10] = {0, 2, 1.5, 1.2, 1.2, 1.2, 1.2, 1.15, 1.1, 1.0};
+  if (clevel < 1 || clevel > 9 || fm_segment <= 0) return 0;
+  const int hashlog = hashlogs[clevel];
+  const int tablog = hashlog < tablog_max ? hashlog : tablog_max;
+  int32_t maxlen = length;
+  if (clevel < 2) maxlen /= 8;
+  else if (clevel < 4) maxlen /= 4;
+  else if (clevel < 7) maxlen /= 2;
+  double ratio = 0.0;
+  fm3_parse(in + (length - maxlen), maxlen, tablog, 1, (1 << hashlog) < fm_probe_cap ? (1 << hashlog) : fm_probe_cap, NULL, 0, &ratio);
+  if (ratio < min_ratio[clevel] || length < 16 || maxout < 66) return 0;
+  return fm3_parse(in, length, tablog, 0, 0, out, maxout, NULL);
+}
