@@ -300,7 +300,7 @@ def e2e(steps, group_chunks=64, nstreams=3):
         dup_exact = dup_exact and C2 == C and bool(torch.equal(h_out, h_src)) and bool((statuses == chunk).all()) \
             and bool(torch.equal(h_packed[:C], h_from)) and all(torch.equal(a, b) for a, b in zip(h_off, h_off2))
     tdupm = float(np.median(tdup))
-    mode = {0: "exact", 1: "fast", 2: "deep"}[B.lib().b2h_set_blosclz_mode(-1)]
+    mode = {0: "exact", 1: "fast", 2: "deep", 3: "seg"}[B.lib().b2h_set_blosclz_mode(-1)]
     return {"config": f"E2E: T from/to pinned host memory, {nstreams} streams x groups of {group_chunks} chunks "
                       "(H2D + compress + pack + D2H of the packed bytes; H2D of the packed bytes + unpack + "
                       "decompress + D2H)", "blosclz_mode": mode,
@@ -418,10 +418,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="C1,C2,C3,C4,E2E,LZ4")
     ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--lz-mode", default="exact", choices=["exact", "fast", "deep"])
+    ap.add_argument("--lz-mode", default="exact", choices=["exact", "fast", "deep", "seg"])
     args = ap.parse_args()
     torch.cuda.set_device(0)
-    B.lib().b2h_set_blosclz_mode({"exact": 0, "fast": 1, "deep": 2}[args.lz_mode])
+    B.lib().b2h_set_blosclz_mode({"exact": 0, "fast": 1, "deep": 2, "seg": 3}[args.lz_mode])
     for name in args.only.split(","):
         r = {"C1": c1, "C2": c2, "C3": c3, "C4": c4, "E2E": e2e, "LZ4": lz4t}[name](args.steps)
         print(json.dumps(r), flush=True)
