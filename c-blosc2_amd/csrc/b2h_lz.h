@@ -1433,6 +1433,13 @@ __device__ __forceinline__ uint32_t win_dword(const InWin& W, int32_t q) {
 //   4. all literal bytes of the batch are written at once (each byte lane finds its token with a
 //      max-scan), then the matches are copied in order (sources always precede the token, so
 //      literals-first is safe).
+// B2H_DEC_STRIP=1 (build option, off by default): the batch's dependent matches are copied one
+// output byte per lane over 64-byte strips (pointer doubling for in-strip sources) instead of one
+// match at a time.  Bit-exact (the whole decoder tier passes with it), measured slower on T
+// (fast decode 4.1 -> 5.5 ms), kept for the record.
+#ifndef B2H_DEC_STRIP
+#define B2H_DEC_STRIP 0
+#endif
 #ifdef B2H_DEC_PROF   // diagnostics build only (tools/dec_micro.hip): per-phase s_memtime sums
 __device__ uint64_t g_dec_prof[8];
 #define DPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
@@ -1447,7 +1454,11 @@ __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, 
                                                       B2H_LDS uint8_t* ring) {
   // a batch's output must fit the ring next to the unflushed tail (F moves in whole pieces and
   // never past op): WMAX + PIECE <= R
-  constexpr int32_t R = 1 << RLOG, RM = R - 1, WMAX = R - ring_piece(RLOG) < 8192 ? R - ring_piece(RLOG) : 8192;
+  // (B2H_DEC_STRIP: kMk more bytes past the batch hold the strip markers, see 4b)
+  // (and the strip keys hold (ex + 1) << 18 in a positive int: a batch's output stays < 8128)
+  constexpr int32_t kMk = B2H_DEC_STRIP ? 260 : 0, kWcap = B2H_DEC_STRIP ? 8128 : 8192;
+  constexpr int32_t R = 1 << RLOG, RM = R - 1,
+                    WMAX = R - ring_piece(RLOG) - kMk < kWcap ? R - ring_piece(RLOG) - kMk : kWcap;
   const int lane = lane_id();
   if (length == 0) return 0;
   InWin W;
@@ -1508,7 +1519,7 @@ __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, 
     }
     DPROF_T(t3);
     if (batch) {
-      if (nop - F > R) F = flush_to<RLOG>(ring, out, nop, F);
+      if (nop + kMk - F > R) F = flush_to<RLOG>(ring, out, nop + kMk, F);
       // ---- 4a. literal bytes: byte lane x belongs to the last batch token at or before it ----
       const bool inbt = (batch >> lane) & 1ull;   // `batch` after the violation cut (`inb` is before it)
       const int32_t owner = wave_scan_max(inbt ? lane : -1);
@@ -1526,6 +1537,100 @@ __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, 
         if (x <= last + lrun) ring[(op + (int32_t)(last_pk >> 6) + (x - last - 1)) & RM] = (uint8_t)byte;
       }
       DPROF_T(t4);
+#if B2H_DEC_STRIP
+      // ---- 4b. matches ----
+      // Matches whose whole source precedes the batch (src + len <= op, <= 64 bytes) read nothing
+      // this batch writes: their reads go out eight at a time, ahead of the writes -- from the
+      // ring (62 % of T's fast-mode matches), or from `out` when the source has already left the
+      // ring (src + len <= F: far matches, 41 % of T's exact-mode matches, which one at a time
+      // through copy_general cost a global round trip each); the others follow in order, after.
+      const int32_t srcv = op + ex - dist;
+      const bool indep = inbt && !lit && olen <= 64 && dist >= ex + olen && (srcv >= F || srcv + olen <= F);
+      uint64_t im = __ballot(indep);
+      if (__ballot(indep && srcv < F)) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // as copy_general
+      while (im) {
+        int32_t oj[8], lj[8], sj[8];
+        uint8_t vb[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          lj[u] = 0;
+          oj[u] = 0;
+          sj[u] = 0;
+          if (im) {
+            const int j = __builtin_ctzll(im);
+            im &= im - 1;
+            oj[u] = op + __builtin_amdgcn_readlane(ex, j);
+            lj[u] = __builtin_amdgcn_readlane(olen, j);
+            sj[u] = oj[u] - __builtin_amdgcn_readlane(dist, j);
+          }
+        }
+        // (measured round 5: every lane reading the ring for all eight, then the far ones from
+        // memory together, was slower -- T decode 4.12 -> 4.29 ms fast, 4.33 -> 4.66 exact)
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+          vb[u] = lane < lj[u] ? (sj[u] >= F ? ring[(sj[u] + lane) & RM] : out[sj[u] + lane]) : (uint8_t)0;
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+          if (lane < lj[u]) ring[(oj[u] + lane) & RM] = vb[u];
+      }
+      // Dependent matches (a source overlapping the batch's own output, longer than 64 bytes, or
+      // straddling the flush frontier): one output byte per lane, 64 at a time, over the strips
+      // that hold their bytes.  A byte's token is the last batch token starting at or before it:
+      // every token starting in the strip drops its key ((ex + 1) << 18 | dependent << 17 | dist)
+      // at its start in a 64-dword marker array, and a max-scan hands each byte the key of its
+      // token (starts grow with the token order; the key of the last token before the strip seeds
+      // the scan).  A dependent match byte at x copies x - dist; a source inside the strip that is
+      // itself a dependent match byte is resolved by pointer doubling over the strip's lanes (each
+      // round takes the source's own source), so every byte ends on a final one: a literal (4a), an
+      // independent match byte (above), an earlier strip's byte or the bytes before the batch.  The
+      // markers sit in the ring slots just past the batch, free by the flush above.
+      const bool dep = inbt && !lit && !indep;
+      if (__ballot(dep)) {
+        const int32_t Lb = nop - op;
+        const uint32_t key = inbt ? ((uint32_t)(ex + 1) << 18) | (dep ? 1u << 17 : 0u) | (lit ? 0u : (uint32_t)dist) : 0u;
+        const int32_t mk0 = (nop + 3) & ~3;   // dword i at ring slot (mk0 + 4 i) & RM (it may wrap)
+        auto mk = [&](int32_t i) -> B2H_LDS uint32_t& {
+          return *reinterpret_cast<B2H_LDS uint32_t*>(ring + ((mk0 + 4 * i) & RM));
+        };
+        bool far = false;
+        int32_t b = 0;
+        for (;;) {
+          // the next strip holding a dependent match byte
+          const uint64_t nx = __ballot(dep && ex + olen > b);
+          if (!nx) break;
+          b = max(b, __builtin_amdgcn_readlane(ex, __builtin_ctzll(nx))) & ~63;
+          const uint64_t bef = __ballot(inbt && ex < b);
+          const uint32_t seed = bef ? (uint32_t)__builtin_amdgcn_readlane((int)key, 63 - __builtin_clzll(bef)) : 0u;
+          mk(lane) = 0u;
+          if (inbt && ex >= b && ex < b + 64) mk(ex - b) = key;
+          asm volatile("" ::: "memory");   // other lanes' markers: no store-to-load forwarding
+          const uint32_t own = (uint32_t)wave_scan_max((int32_t)max(mk(lane), seed));
+          const int32_t x = b + lane;
+          const bool mb = x < Lb && ((own >> 17) & 1u);
+          int32_t sx = x - (int32_t)(own & 0x1ffffu);   // relative to op
+          bool need = mb && sx >= b;
+          while (__ballot(need)) {
+            const int32_t w = mb ? (sx << 1) | 1 : (x << 1);
+            const int32_t w2 = __shfl(w, need ? sx - b : lane);
+            if (need) {
+              if (w2 & 1) sx = w2 >> 1;
+              else need = false;   // a final byte of this strip
+            }
+            need = need && sx >= b;
+          }
+          const int32_t y = op + sx;
+          uint8_t vb = 0;
+          if (mb && y >= F) vb = ring[y & RM];
+          if (__ballot(mb && y < F)) {   // sources already flushed: read back from `out`
+            if (!far) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+            far = true;
+            if (mb && y < F) vb = out[y];
+          }
+          if (mb) ring[(op + x) & RM] = vb;
+          b += 64;
+        }
+      }
+#else
       // ---- 4b. matches ----
       // Matches whose whole source precedes the batch (src + len <= op, <= 64 bytes) read nothing
       // this batch writes: their reads go out eight at a time, ahead of the writes -- from the
@@ -1578,6 +1683,7 @@ __device__ __forceinline__ int32_t wave_lz_decode_par(gin_t in, int32_t length, 
           F = copy_general<RLOG>(ring, out, oj, src, lj, dj, F);
         }
       }
+#endif
       DPROF_T(t5);
       DPROF_ADD(3, t3, t4);
       DPROF_ADD(4, t4, t5);

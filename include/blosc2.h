@@ -692,7 +692,10 @@ BLOSC_EXPORT blosc2_schunk *blosc2_schunk_from_buffer(uint8_t *cframe, int64_t l
  * frame.c:1720-1870): a contiguous frame file (at `offset`) through the IO backend `udio->id`
  * (registry above; NULL udio = the filesystem backend).  Open reads the header, the trailer and
  * the offsets index only; chunks are read when used, through the backend's read callback, which
- * stays open for the handle's life. */
+ * stays open for the handle's life.  Unlike the reference's, the handle is READ-ONLY: append /
+ * insert / update / delete chunk, append_buffer and set_slice_buffer return
+ * BLOSC2_ERROR_INVALID_PARAM on it (copy the chunks into a blosc2_schunk_new super-chunk and write
+ * that out with blosc2_schunk_to_file to modify a frame). */
 BLOSC_EXPORT blosc2_schunk *blosc2_schunk_open(const char *urlpath);
 BLOSC_EXPORT blosc2_schunk *blosc2_schunk_open_offset(const char *urlpath, int64_t offset);
 BLOSC_EXPORT blosc2_schunk *blosc2_schunk_open_udio(const char *urlpath, const blosc2_io *udio);
