@@ -117,6 +117,9 @@ int bitshuffle_dev(int32_t typesize, int32_t nbytes, const uint8_t* d_src, uint8
 
 // BloscLZ encoder mode, process-wide default: 0 exact (default), 1 fast.  Returns the previous
 // mode.  A plan's own lz_mode (a context's cparams.codec_params, see include/b2h.h) overrides it.
+// Exact encoder workgroup shape (b2h_set_encode_shape): -1,-1 auto; 1,N one LDS-table wave + N
+// global-table waves; 0,1 global-table only.  Returns the previous shape (16 nlds + nglb, -1 auto).
+int set_encode_shape(int nlds, int nglb);
 int set_blosclz_mode(int mode);
 // Fused launches (k_encode_fast_fused / k_encode_fused) off for the calling host thread: a caller
 // that saw a fused launch's hand-off wait time out (BLOSC2_ERROR_FAILURE for the whole batch, e.g.

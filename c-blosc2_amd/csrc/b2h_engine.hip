@@ -2213,7 +2213,7 @@ static bool fused_encode_ok(const CGeom& g) {
     if (!(fuse_bits() & 4)) return false;
     int nl, ng;
     enc_mode(&nl, &ng);
-    return nl == 1 && ng == 3;
+    return (nl == 1 && ng == 3) || nl < 0;   // the fused exact kernel has the hyb3 shape
   }
   const bool small = fast_u16(g);
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
@@ -2621,17 +2621,46 @@ static bool hostside_trunc_ok(int8_t prec, int32_t ts, int* zeroed) {
 // global-table wave), or "hybN" (one LDS-table wave + N global-table waves).  Default: hyb3, i.e.
 // 3 LDS-table + 9 global-table waves per CU (T bench: lds 54.2 ms, glb 30.3, hyb1 34.4, hyb2 33.1,
 // hyb3 28.7, hyb4 32.3 ms per 4 GiB encode -- more global tables than that overflow L2 into MALL).
+// Unset (and b2h_set_encode_shape(-1, -1)): "auto" -- hyb3, except that a batch whose streams all
+// fit the LDS-only shape's resident waves at once (a per-call chunk: blosc1_compress and
+// blosc2_compress_ctx encode one chunk, 8-64 streams) runs there: then every stream has its own
+// LDS table and the call's latency is one stream's walk on it (C1 per call).
+static int g_enc_ml = -2, g_enc_mg = -2;   // -2: not read yet; -1: auto
 static void enc_mode(int* nlds, int* nglb) {
-  static int ml = -1, mg = -1;
-  if (ml < 0) {
+  if (g_enc_ml == -2) {
     const char* e = getenv("B2H_ENC_MODE");
-    ml = 1; mg = 3;
-    if (e && !strcmp(e, "lds")) { ml = 1; mg = 0; }
-    else if (e && !strcmp(e, "glb")) { ml = 0; mg = 1; }
-    else if (e && !strncmp(e, "hyb", 3)) { ml = 1; mg = std::max(1, std::min(4, atoi(e + 3))); }
+    g_enc_ml = -1; g_enc_mg = -1;
+    if (e && !strcmp(e, "lds")) { g_enc_ml = 1; g_enc_mg = 0; }
+    else if (e && !strcmp(e, "glb")) { g_enc_ml = 0; g_enc_mg = 1; }
+    else if (e && !strncmp(e, "hyb", 3)) { g_enc_ml = 1; g_enc_mg = std::max(1, std::min(4, atoi(e + 3))); }
   }
-  *nlds = ml;
-  *nglb = mg;
+  *nlds = g_enc_ml;
+  *nglb = g_enc_mg;
+}
+int set_encode_shape(int nlds, int nglb) {
+  int ml, mg;
+  enc_mode(&ml, &mg);
+  const int prev = ml < 0 ? -1 : ml * 16 + mg;
+  if (nlds == -1 && nglb == -1) { g_enc_ml = -1; g_enc_mg = -1; }
+  else if (nlds == 1 && nglb >= 0 && nglb <= 4) { g_enc_ml = 1; g_enc_mg = nglb; }
+  else if (nlds == 0 && nglb == 1) { g_enc_ml = 0; g_enc_mg = 1; }
+  else if (nlds != -2) return -1;
+  return prev;
+}
+// resident waves of the LDS-only shape (one LDS-table wave per workgroup) on this device
+template <typename POS>
+static int64_t lds_only_slots(int hashlog) {
+  const void* fn = reinterpret_cast<const void*>(&k_encode<POS, 1, 0>);
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  int dev = 0, per_cu = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, enc_wg_lds<POS>(hashlog, 1, 0)) != hipSuccess) per_cu = 1;
+  return (int64_t)std::max(1, per_cu) * std::max(1, ncu);
 }
 
 template <typename POS, int NL, int NG>
@@ -2674,6 +2703,10 @@ static int launch_encode(Workspace* ws, const CGeom& g, int hashlog, const uint8
                          int64_t ntot, int32_t* next, const int32_t* porder, hipStream_t st) {
   int nl, ng;
   enc_mode(&nl, &ng);
+  if (nl < 0) {   // auto
+    nl = 1;
+    ng = ntot <= lds_only_slots<POS>(hashlog) ? 0 : 3;
+  }
   if (nl == 1 && ng == 0) return launch_encode_shape<POS, 1, 0>(ws, g, hashlog, filt, res, ntot, next, porder, st);
   if (nl == 0) return launch_encode_shape<POS, 0, 1>(ws, g, hashlog, filt, res, ntot, next, porder, st);
   if (ng == 1) return launch_encode_shape<POS, 1, 1>(ws, g, hashlog, filt, res, ntot, next, porder, st);

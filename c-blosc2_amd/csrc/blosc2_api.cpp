@@ -2236,6 +2236,7 @@ int32_t b2h_bitshuffle(int32_t typesize, int32_t nbytes, const void* d_src, void
 }
 
 int b2h_set_blosclz_mode(int mode) { return b2h::set_blosclz_mode(mode); }
+int b2h_set_encode_shape(int nlds, int nglb) { return b2h::set_encode_shape(nlds, nglb); }
 void b2h_enable_timing(int on) { b2h::enable_timing(on != 0); }
 void b2h_last_times(float out[5]) {
   const b2h::KernelTimes t = b2h::last_times();

@@ -191,6 +191,14 @@ typedef struct {
  * Any other value only queries. */
 BLOSC_EXPORT int b2h_set_blosclz_mode(int mode);
 
+/* Exact-mode encoder workgroup shape, process-wide (diagnostics and tests; B2H_ENC_MODE sets it at
+ * start-up): (-1, -1) auto -- batches that fit the LDS-only shape's resident waves run one
+ * LDS-table wave per workgroup, larger ones 1 LDS-table + 3 global-table waves; (1, n) one
+ * LDS-table wave + n (0..4) global-table waves; (0, 1) global tables only; (-2, x) only queries.
+ * Same bytes in every shape.  Returns the previous shape as 16 * nlds + nglb (-1: auto), or -1 for
+ * an invalid one. */
+BLOSC_EXPORT int b2h_set_encode_shape(int nlds, int nglb);
+
 /* Per-phase HIP-event timings (ms): filter, encode, finalize, decode, unfilter.  Enabling
  * (re)starts the log and adds event records only: the batch calls never wait on the host; the
  * times are read after the timed work.  last: the latest batch; mean: every batch since enabled. */

@@ -510,3 +510,44 @@ def test_learned_pull_order_keeps_chunks(B):
         for _ in range(2):
             got = B.compress(src, **kw)
             assert isinstance(got, np.ndarray) and np.array_equal(got, want), (n, ts)
+
+
+@pytest.mark.parametrize("shape", [(-1, -1), (1, 0), (1, 3), (1, 1), (0, 1)])
+def test_exact_encoder_shapes_same_bytes(B, shape):
+    """Every exact-encoder workgroup shape (b2h_set_encode_shape: auto, LDS tables only, 1 LDS + 3 /
+    1 global-table waves, global tables only) gives the oracle's bytes: u16 positions (64 KiB
+    streams) and u32 (256 KiB BITSHUFFLE blocks, unsplit), a batch small enough for the LDS-only
+    shape (auto picks it) and one of 600 chunks that is not (auto: 1 + 3), plus the per-call path."""
+    import torch
+    L = B.lib()
+    L.b2h_set_blosclz_mode(0)
+    assert L.b2h_set_encode_shape(*shape) >= -1
+    assert L.b2h_set_encode_shape(-2, 0) == (-1 if shape == (-1, -1) else 16 * shape[0] + shape[1])
+    try:
+        chunk = 1 << 18
+        cases = [(dict(clevel=5, typesize=4, filters=(0, 0, 0, 0, 0, 1)), 600),
+                 (dict(clevel=5, typesize=4, filters=(0, 0, 0, 0, 0, 2), blocksize=262144), 6)]
+        for kw, nchunks in cases:
+            host = gen_f32(7, nchunks * chunk // 4)
+            dsrc = torch.from_numpy(host.view(np.uint8)).cuda()
+            cap = chunk + 32
+            stride = (cap + 255) // 256 * 256
+            ddst = torch.zeros(nchunks * stride, dtype=torch.uint8, device="cuda")
+            dcb = torch.zeros(nchunks, dtype=torch.int32, device="cuda")
+            B.compress_batch(B.cparams(**kw), dsrc.data_ptr(), chunk, nchunks, chunk, ddst.data_ptr(), stride, cap,
+                             dcb.data_ptr())
+            torch.cuda.synchronize()
+            cbytes = dcb.cpu().numpy()
+            out = ddst.cpu().numpy()
+            for i in sorted({0, nchunks // 2, nchunks - 1}):
+                want = oracle_compress(host[i * chunk // 4:(i + 1) * chunk // 4], **kw)
+                assert cbytes[i] == want.nbytes and np.array_equal(out[i * stride:i * stride + cbytes[i]], want), (kw, i)
+        # the per-call drop-in path (one chunk per call)
+        src = RAMP.copy()
+        dst = np.zeros(src.nbytes + 32, np.uint8)
+        L.blosc1_set_compressor(b"blosclz")
+        n = L.blosc1_compress(5, 1, 4, src.nbytes, B._p(src), B._p(dst), dst.nbytes)
+        want = oracle_compress(src, clevel=5, typesize=4, filters=(0, 0, 0, 0, 0, 1))
+        assert n == want.nbytes and np.array_equal(dst[:n], want)
+    finally:
+        L.b2h_set_encode_shape(-1, -1)

@@ -10,6 +10,8 @@
 #   stall_fast|stall_exact  SQ stall / issue / LDS-conflict passes over tests/prof_encode.py (T)
 #   rp_c4|rp_c3|rp_c1  rocprofv3 kernel stats of tools/bench_configs.py for that config (fast mode)
 #   pmc_c4           FETCH_SIZE / WRITE_SIZE over C4 (fast mode)
+#   rpc_<cN>_<mode>  rocprof kernel stats of config cN in that mode (e.g. rpc_c3_exact)
+#   pmcc_<cN>_<mode> FETCH_SIZE / WRITE_SIZE over config cN in that mode, summarised (pmc_traffic.py)
 #   configs          tools/bench_configs.py, both modes
 #   smoke            __graft_entry__.smoke()
 #   frame_e2e        tools/frame_e2e.py (T frame file: write, open + decode warm / cold; host fan-out)
@@ -70,6 +72,17 @@ for job in "$@"; do
           -d $O/${TAG}_pmc_c4_$ctr -o run -- python3 -u $R/tools/bench_configs.py --only C4 --lz-mode fast --steps 1 > "$L" 2>&1 || fail "$job $ctr" $L
       done
       echo "c4 pmc: gpurun_out/${TAG}_pmc_c4_*" ;;
+    rpc_*)   # rpc_<c1..c4>_<fast|exact>: rocprof kernel stats of one config in one mode
+      x=${job#rpc_}; c=${x%_*}; m=${x#*_}; C=${c^^}; cd /tmp
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_rp_${c}_$m -o run -- python3 -u $R/tools/bench_configs.py --only $C --lz-mode $m --steps 3 > "$L" 2>&1 || fail "$job" "$L"
+      tail -1 "$L" | cut -c1-400 ;;
+    pmcc_*)  # pmcc_<c1..c4>_<fast|exact>: FETCH_SIZE / WRITE_SIZE passes of one config, summarised
+      x=${job#pmcc_}; c=${x%_*}; m=${x#*_}; C=${c^^}; cd /tmp
+      for ctr in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 200 rocprofv3 --pmc $ctr --kernel-include-regex "k_" --output-format csv \
+          -d $O/pmc_${TAG}_$c${m}_$ctr -o run -- python3 -u $R/tools/bench_configs.py --only $C --lz-mode $m --steps 1 > "$L" 2>&1 || fail "$job $ctr" $L
+      done
+      python3 $R/tools/pmc_traffic.py $O ${TAG}_$c$m $O/${TAG}_pmc_traffic_${c}_$m.json $m "$C (tools/bench_configs.py --only $C)" > /dev/null && echo "traffic: gpurun_out/${TAG}_pmc_traffic_${c}_$m.json" ;;
     configs)
       for m in fast exact; do
         timeout -k 10 500 python3 -u tools/bench_configs.py --lz-mode $m > $O/${TAG}_configs_$m.log 2>&1 || fail "configs $m" $O/${TAG}_configs_$m.log

@@ -4,7 +4,7 @@ FETCH_SIZE counts half of the bytes of WIDE STREAMING reads (16 B per lane) -- d
 kernels whose reads are of that kind (the shuffle / unshuffle filters); the LZ encoder and decoder
 read with dword and scattered loads, whose FETCH_SIZE is uncalibrated, so they are reported raw
 with the doubled figure beside it as an upper bound.  WRITE_SIZE is exact; both are in KiB.
-    python tools/pmc_traffic.py <gpurun_out dir> <tag> <out.json> [exact|fast]"""
+    python tools/pmc_traffic.py <gpurun_out dir> <tag> <out.json> [exact|fast] [workload]"""
 import collections
 import csv
 import json
@@ -15,7 +15,7 @@ WORKLOAD = "T: float32 ts=4 SHUFFLE+BloscLZ clevel 5, 256 KiB blocks, 4 MiB chun
 STREAMING = ("k_ffilter", "k_dfilter", "k_copy16")
 
 
-def main(root, tag, dst, mode="fast"):
+def main(root, tag, dst, mode="fast", workload=WORKLOAD):
     kern = collections.defaultdict(dict)
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         vals = collections.defaultdict(list)
@@ -33,13 +33,14 @@ def main(root, tag, dst, mode="fast"):
         v["correction"] = ("2 x FETCH + WRITE (16 B/lane streaming reads)" if streaming else
                            "FETCH + WRITE raw (dword / scattered reads: FETCH_SIZE uncalibrated; "
                            "hbm_bytes_upper_bound doubles FETCH)")
-    res = {"workload": WORKLOAD + f" [{mode}]", "tag": tag,
-           "command": "rocprofv3 --pmc <FETCH_SIZE|WRITE_SIZE> --kernel-include-regex ... -- "
-                      f"python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --lz-mode {mode} (one pass per counter)",
+    res = {"workload": workload + f" [{mode}]", "tag": tag,
+           "command": "rocprofv3 --pmc <FETCH_SIZE|WRITE_SIZE> --kernel-include-regex ... -- " +
+                      (f"python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --lz-mode {mode}" if workload == WORKLOAD
+                       else f"python3 tools/bench_configs.py --only <cfg> --lz-mode {mode} --steps 1") + " (one pass per counter)",
            "kernels": kern}
     json.dump(res, open(dst, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:6])
