@@ -76,7 +76,7 @@ for job in "$@"; do
       x=${job#rpc_}; c=${x%_*}; m=${x#*_}; C=${c^^}; cd /tmp
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_rp_${c}_$m -o run -- python3 -u $R/tools/bench_configs.py --only $C --lz-mode $m --steps 3 > "$L" 2>&1 || fail "$job" "$L"
       tail -1 "$L" | cut -c1-400 ;;
-    pmcc_*)  # pmcc_<c1..c4>_<fast|exact>: FETCH_SIZE / WRITE_SIZE passes of one config, summarised
+    pmcc_*)  # pmcc_<c1..c4>_<fast|exact>: FETCH_SIZE / WRITE_SIZE passes of one config, summarised (rename the json to rN_vK[x]_cN_pmc_traffic.json when committing)
       x=${job#pmcc_}; c=${x%_*}; m=${x#*_}; C=${c^^}; cd /tmp
       for ctr in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 200 rocprofv3 --pmc $ctr --kernel-include-regex "k_" --output-format csv \
