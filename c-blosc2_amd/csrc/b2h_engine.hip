@@ -780,12 +780,17 @@ static int launch_encode_seg_t(Workspace* ws, const CGeom& g0, const uint8_t* fi
 
 // BloscLZ mode 3.  Streams of <= 2^16 positions: u32 table entries with a check of the hashed value
 // (no candidate reads); longer streams: u16 entries (their aliasing rule reads the candidates).
-// B2H_SEG_WAVES (1..4, default 3): waves per workgroup sharing one table.
+// B2H_SEG_WAVES (1..4, default 4): waves per workgroup sharing one table (T: 2 / 3 / 4 waves
+// 193.1 / 205.7 / 209.4 GiB/s unfused, profiles/r6_seg_bench_w*.log).
+static int seg_waves() {
+  static const int W = [] { const char* e = getenv("B2H_SEG_WAVES"); return e ? std::max(1, std::min(4, atoi(e))) : 4; }();
+  return W;
+}
 static int launch_encode_seg(Workspace* ws, const CGeom& g, const uint8_t* filt, StreamResult* res, int64_t ntot,
                              int32_t* next, const int32_t* porder, hipStream_t st) {
   const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
   const int tablog = std::min(fast_tablog(), hashlog);
-  static const int W = [] { const char* e = getenv("B2H_SEG_WAVES"); return e ? std::max(1, std::min(4, atoi(e))) : 3; }();
+  const int W = seg_waves();
   const bool chk = chain_len(g) <= 65536;
 #define B2H_SEG_LAUNCH(C, WW) return launch_encode_seg_t<C, WW>(ws, g, filt, res, ntot, next, porder, st, tablog)
   if (chk) {
@@ -2107,7 +2112,10 @@ __global__ void k_fuse_check(const int32_t* __restrict__ sync, int32_t* __restri
 // B2H_FUSE (A/B runs, tests): 0 separate launches; bit 1 finalize + scatter inside the encode launch,
 // bit 2 + the byte shuffle, bit 4 exact mode too (k_encode_fused: per-wave shuffles and copies are
 // latency-bound, T exact 26.98 -> 27.72 ms, so off by default), bit 16 scatter items only once the
-// stream queue is empty, bit 32 plain dword-load scatter copies, bit 64 the parser wave at a
+// stream queue is empty, bit 8 BloscLZ mode 3 too (k_encode_seg_fused, same per-wave protocol:
+// T seg 209.9 GiB/s unfused, 206.5 fused, 204.3 with only finalize + scatter fused -- lone waves'
+// shuffles and copies contend with the segment walks -- so off by default), bit 32 plain
+// dword-load scatter copies, bit 64 the parser wave at a
 // higher issue priority.  Default 83 (1 + 2 + 16 + 64).  Measured on T (tools/fuse_prof.py, profiles/r2_v5_*):
 // separate 1.54 + 16.55 + 1.10 ms; 19: 17.79 ms; scatter items claimed between streams (3) slow
 // the concurrent encoders' short planes ~2x (22.5 ms), with non-temporal copies too (35).
@@ -2208,7 +2216,8 @@ static int launch_encode_fast_fused_t(Workspace* ws, const CGeom& g0, const uint
 // results fit the LDS table (the finalizing workgroup stages them there).
 static void enc_mode(int* nlds, int* nglb);
 static bool fused_encode_ok(const CGeom& g) {
-  if (!fuse_enabled() || g.compcode != 0 || g.dict_size || g.lzmode == 3) return false;
+  if (!fuse_enabled() || g.compcode != 0 || g.dict_size) return false;
+  if (g.lzmode == 3) return (fuse_bits() & 8) != 0;   // mode 3: only with bit 8 (measured slower)
   if (g.lzmode == 0) {   // exact mode: only with bit 4 (measured slower), the default k_encode shape
     if (!(fuse_bits() & 4)) return false;
     int nl, ng;
@@ -2241,8 +2250,10 @@ static int launch_encode_fast_fused(Workspace* ws, const CGeom& g, const uint8_t
 // The arguments (FusedArgs) live in LDS and every phase re-reads the words it needs: kept in
 // registers across the encode they cost ~300 SGPR spills (v_readlane / v_writelane reloads in the
 // parse loops; T exact fused 25.94 ms against 23.03 for k_encode alone).
-template <typename TAB>
-__device__ void encode_loop_fused(const B2H_LDS FusedArgs* A, TAB htab, B2H_LDS uint32_t* dbits, B2H_LDS uint8_t* oring) {
+// `enc(in, len, clevel, out, runs_test)` encodes one stream (write-through output): the exact
+// walker (k_encode_fused) or BloscLZ mode 3's segmented parse (k_encode_seg_fused).
+template <typename ENC>
+__device__ void encode_loop_fused(const B2H_LDS FusedArgs* A, ENC&& enc) {
   const int lane = lane_id();
   auto wadd = [&](int32_t* p, int32_t v) -> int32_t {
     return __builtin_amdgcn_readfirstlane(
@@ -2331,10 +2342,9 @@ __device__ void encode_loop_fused(const B2H_LDS FusedArgs* A, TAB htab, B2H_LDS 
       r.size = run_byte;
       r.kind = r.size ? kStreamByteRun : kStreamZeroRun;
     } else {
-      r = encode_stream<TAB, true>(in, len, clevel, out, htab, dbits, oring, runs_test);
+      r = enc(in, len, clevel, out, runs_test);
     }
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
-    if (TAB::kGlobal) r.windows |= 1 << 30;
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
     {
       const CGeom g = lds_uniform(&A->g);
@@ -2459,12 +2469,55 @@ void k_encode_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint8_t* 
   if (NLDS > 0 && w < NLDS) {
     LdsTab<POS> t;
     t.t = (volatile B2H_LDS POS*)(smem + w * tabsz);
-    encode_loop_fused(static_cast<const B2H_LDS FusedArgs*>(A), t, dbits, oring);
+    encode_loop_fused(static_cast<const B2H_LDS FusedArgs*>(A), [&](gin_t in, int32_t len, int clevel, gout_t out, bool rt) {
+      return encode_stream<LdsTab<POS>, true>(in, len, clevel, out, t, dbits, oring, rt);
+    });
   } else if (NGLB > 0) {
     GlbTab<POS> t;
     t.t = (B2H_GLB POS*)(gtab + (((size_t)blockIdx.x * NGLB + (w - NLDS)) << hashlog));
-    encode_loop_fused(static_cast<const B2H_LDS FusedArgs*>(A), t, dbits, oring);
+    encode_loop_fused(static_cast<const B2H_LDS FusedArgs*>(A), [&](gin_t in, int32_t len, int clevel, gout_t out, bool rt) {
+      StreamResult r = encode_stream<GlbTab<POS>, true>(in, len, clevel, out, t, dbits, oring, rt);
+      r.windows |= 1 << 30;   // diagnostics: the stream ran on a global-table wave
+      return r;
+    });
   }
+}
+
+// BloscLZ mode 3 in one launch: k_encode_seg's W waves per workgroup (one shared candidate table
+// under the LDS lock), each pulling its own streams through encode_loop_fused's per-wave protocol
+// (typesize-4 SHUFFLE claims ahead of the wave's stream with the run verdict, finalisation by the
+// wave completing a chunk, scatter items once the stream queue is empty).
+template <bool CHK, int W>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 8)))
+void k_encode_seg_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint8_t* __restrict__ sbuf_arg,
+                        StreamResult* __restrict__ res_arg, int32_t nstreams_total_arg, int32_t* __restrict__ next_arg,
+                        int tablog, const int32_t* __restrict__ porder_arg, EncFuse f_arg) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  B2H_LDS uint8_t* tab = (B2H_LDS uint8_t*)smem;
+  B2H_LDS FusedArgs* A = (B2H_LDS FusedArgs*)(smem + (CHK ? (size_t)4 << tablog : (size_t)2 << tablog));
+  const int64_t sb = seg_scratch_bytes(chain_len(g_arg));
+  int32_t* lock = reinterpret_cast<int32_t*>(g_arg.chain + (int64_t)gridDim.x * W * sb) + 64 * blockIdx.x;
+  if (threadIdx.x == 0) {
+    atomicExch(lock, 0);
+    lds_store(&A->g, g_arg);
+    lds_store(&A->f, f_arg);
+    A->filt = filt_arg;
+    A->sbuf = sbuf_arg;
+    A->res = res_arg;
+    A->next = next_arg;
+    A->porder = porder_arg;
+    A->nstreams_total = nstreams_total_arg;
+    A->tablog = tablog;
+  }
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* mine = g_arg.chain + ((int64_t)blockIdx.x * W + wave) * sb;
+  B2H_GLB uint32_t* dist = (B2H_GLB uint32_t*)mine;
+  B2H_GLB uint64_t* mask = (B2H_GLB uint64_t*)(mine + seg_dist_bytes(chain_len(g_arg)));
+  B2H_GLB uint32_t* snv = (B2H_GLB uint32_t*)(mine + seg_dist_bytes(chain_len(g_arg)) + seg_mask_bytes(chain_len(g_arg)));
+  encode_loop_fused(static_cast<const B2H_LDS FusedArgs*>(A), [&](gin_t in, int32_t len, int clevel, gout_t out, bool rt) {
+    return encode_stream_seg<true, CHK>(in, len, clevel, out, tab, lds_uniform(&A->tablog), dist, mask, snv, rt, lock);
+  });
 }
 
 // exact mode, default shape (1 LDS-table wave + 3 global-table waves, enc_mode hyb3) only
@@ -2491,6 +2544,48 @@ static int launch_encode_exact_fused(Workspace* ws, const CGeom& g, int hashlog,
   k_fuse_check<<<(f.nchunks + 255) / 256, 256, 0, st>>>(f.sync, f.cbytes, f.nchunks);
   HIPCHK(hipGetLastError());
   return 0;
+}
+template <bool CHK, int W>
+static int launch_encode_seg_fused_t(Workspace* ws, const CGeom& g0, const uint8_t* filt, StreamResult* res, int64_t ntot,
+                                     int32_t* next, const int32_t* porder, EncFuse f, hipStream_t st, int tablog) {
+  CGeom g = g0;
+  const size_t lds = (CHK ? (size_t)4 << tablog : (size_t)2 << tablog) + ((sizeof(FusedArgs) + 15) & ~size_t(15));
+  const void* fn = reinterpret_cast<const void*>(&k_encode_seg_fused<CHK, W>);
+  static bool attr_set = false;
+  if (!attr_set) {   // > 64 KiB of dynamic LDS at tablog 14: opt in once
+    HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  const int slots = resident_slots(fn, lds, 64 * W);
+  const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>((ntot + W - 1) / W, fuse_grid_cap(slots)));
+  const int64_t sb = seg_scratch_bytes(chain_len(g));
+  if (ws->fchain.ensure((size_t)grid * W * (size_t)sb + (size_t)grid * 256 + 256)) return E_MEMORY;   // + lock words
+  g.chain = ws->fchain.as<uint8_t>();
+  if (fuse_prepare(ws, g, ntot, f, st)) return E_MEMORY;
+  k_encode_seg_fused<CHK, W><<<grid, 64 * W, lds, st>>>(g, filt, ws->sbuf.as<uint8_t>(), res, (int32_t)ntot, next, tablog,
+                                                        porder, f);
+  HIPCHK(hipGetLastError());
+  k_fuse_check<<<(f.nchunks + 255) / 256, 256, 0, st>>>(f.sync, f.cbytes, f.nchunks);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+static int launch_encode_seg_fused(Workspace* ws, const CGeom& g, const uint8_t* filt, StreamResult* res, int64_t ntot,
+                                   int32_t* next, const int32_t* porder, const EncFuse& f, hipStream_t st) {
+  const int hashlog = g.clevel == 1 ? 12 : (g.clevel == 2 ? 13 : 14);
+  const int tablog = std::min(fast_tablog(), hashlog);
+  const int W = seg_waves();
+#define B2H_SEG_LAUNCH(C, WW) return launch_encode_seg_fused_t<C, WW>(ws, g, filt, res, ntot, next, porder, f, st, tablog)
+  if (chain_len(g) <= 65536) {
+    if (W == 1) B2H_SEG_LAUNCH(true, 1);
+    if (W == 2) B2H_SEG_LAUNCH(true, 2);
+    if (W == 3) B2H_SEG_LAUNCH(true, 3);
+    B2H_SEG_LAUNCH(true, 4);
+  }
+  if (W == 1) B2H_SEG_LAUNCH(false, 1);
+  if (W == 2) B2H_SEG_LAUNCH(false, 2);
+  if (W == 3) B2H_SEG_LAUNCH(false, 3);
+  B2H_SEG_LAUNCH(false, 4);
+#undef B2H_SEG_LAUNCH
 }
 // ============================================================ compression: host driver ====
 static int32_t split_block(int32_t splitmode, int compcode, const uint8_t* filters, int32_t ts, int32_t bs) {
@@ -2964,7 +3059,8 @@ static int encode_stage(Workspace* ws, const CompressPlan& P, CGeom& g, const ui
       f.cbytes = d_cbytes;
       f.htpl = htpl;
       f.nchunks = nchunks;
-      if (g.lzmode != 0) rc = launch_encode_fast_fused(ws, g, filt, res, ntot, next, porder, f, st);
+      if (g.lzmode == 3) rc = launch_encode_seg_fused(ws, g, filt, res, ntot, next, porder, f, st);
+      else if (g.lzmode != 0) rc = launch_encode_fast_fused(ws, g, filt, res, ntot, next, porder, f, st);
       else rc = small ? launch_encode_exact_fused<uint16_t>(ws, g, hashlog, filt, res, ntot, next, porder, f, st)
                       : launch_encode_exact_fused<uint32_t>(ws, g, hashlog, filt, res, ntot, next, porder, f, st);
     } else if (g.lzmode == 3) rc = launch_encode_seg(ws, g, filt, res, ntot, next, porder, st);

@@ -390,14 +390,15 @@ def test_gpu_deep_mode_ratio(fast, data):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lzmode", [1, 2, 0], ids=["fast", "deep", "exact"])
+@pytest.mark.parametrize("lzmode", [1, 2, 0, 3], ids=["fast", "deep", "exact", "seg"])
 @pytest.mark.parametrize("shape", ["T", "ts4_runplanes", "leftover", "clevel9_ts8", "ds8", "ds8_ramp", "ds2_leftover",
                                    "ds4_odd_leftover"])
 def test_gpu_fused_launch_matches_separate_launches(fast, shape, lzmode, monkeypatch):
     """The one-launch fast-mode encode (byte shuffle, finalize and payload scatter inside the
     encoder launch, k_encode_fast_fused) writes the same chunks as the separate launches
     (B2H_FUSE=0; 83 is the default, 3 also claims scatter items between streams), in both BloscLZ
-    modes (exact: k_encode_fused, per-wave hand-offs; its chunks also equal the oracle's), on T's shape (4 MiB chunks: fused shuffle) and on shapes where only the
+    modes (exact: k_encode_fused, per-wave hand-offs; its chunks also equal the oracle's; mode 3:
+    k_encode_seg_fused, the same per-wave protocol), on T's shape (4 MiB chunks: fused shuffle) and on shapes where only the
     finalize/scatter is fused (a leftover block not of whole 64-byte groups, typesize 8)."""
     import torch
     B = fast
@@ -441,8 +442,8 @@ def test_gpu_fused_launch_matches_separate_launches(fast, shape, lzmode, monkeyp
     cp = B.cparams(**kw, lz_mode=lzmode)
     got = {}
     for fuse in ("83", "3", "0"):
-        # exact mode fuses only with bit 4 (k_encode_fused)
-        monkeypatch.setenv("B2H_FUSE", fuse if lzmode != 0 or fuse == "0" else str(int(fuse) | 4))
+        # exact mode fuses only with bit 4 (k_encode_fused), mode 3 only with bit 8 (k_encode_seg_fused)
+        monkeypatch.setenv("B2H_FUSE", fuse if lzmode in (1, 2) or fuse == "0" else str(int(fuse) | (4 if lzmode == 0 else 8)))
         comp = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
         cb = torch.zeros(n, dtype=torch.int32, device=dev)
         B.compress_batch(cp, src.data_ptr(), chunk, n, chunk, comp.data_ptr(), stride, cap, cb.data_ptr(), 0)
