@@ -986,6 +986,28 @@ __host__ __device__ constexpr int32_t ring_piece(int rlog) { return (1 << rlog) 
 // than the ring, and ring flushes.  Returns the new flush frontier F.
 // A source before the stream start (src < 0, LZ4 with a dictionary) reads the dictionary's tail:
 // position y < 0 is dict[dsz + y] (LZ4_decompress_safe_usingDict's external dictionary).
+// B2H_FAR_COPY=1 (build option, off by default): a 1 KiB piece whose whole source has left the
+// ring (C4's plane 1: 250-16 K byte matches 2-32 KiB back) is copied with sixteen byte loads per
+// lane in flight -- one round trip per KiB instead of per 64 bytes -- then the ring writes.  It
+// halves plane 1's decode (1.11 M -> 0.58 M cycles per stream) and C4 decompress gains 1-5 %, but
+// with the call in copy_general, inline or not, the decoder's other paths lose: C1 decompress
+// -3..-10 %, C3 -2 % (same-box A/B, profiles/r6_ab_far_copy.txt).  The source ends before the
+// flush frontier <= the piece's destination, so no byte of it is written here.
+#ifndef B2H_FAR_COPY
+#define B2H_FAR_COPY 0
+#endif
+template <int RLOG>
+__device__ __noinline__ void copy_far(B2H_LDS uint8_t* ring, gout_t out, int32_t dst, int32_t src, int32_t n) {
+  constexpr int32_t RM = (1 << RLOG) - 1;
+  const int lane = lane_id();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  uint8_t b[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) b[k] = lane + 64 * k < n ? out[src + lane + 64 * k] : (uint8_t)0;
+#pragma unroll
+  for (int k = 0; k < 16; k++)
+    if (lane + 64 * k < n) ring[(dst + lane + 64 * k) & RM] = b[k];
+}
 template <int RLOG>
 __device__ __noinline__ int32_t copy_general(B2H_LDS uint8_t* ring, gout_t out, int32_t op, int32_t src, int32_t len, int32_t dist, int32_t F,
                                              gin_t dict = nullptr, int32_t dsz = 0) {
@@ -1060,6 +1082,10 @@ __device__ __noinline__ int32_t copy_general(B2H_LDS uint8_t* ring, gout_t out, 
         for (int k = 0; k < 16; k++)
           if (lane + 64 * k < m) ring[(op + sub + lane + 64 * k) & RM] = b[k];
       }
+      continue;
+    }
+    if (B2H_FAR_COPY && n == STEP && src + done >= 0 && src + done + n <= F) {
+      copy_far<RLOG>(ring, out, op + done, src + done, n);
       continue;
     }
     if (src < F) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
