@@ -61,3 +61,18 @@ for b in range(nblk):
 tot = dur.sum() / 100
 print(f"stream-us total {tot:.0f}; by kind:", {kinds[k]: round(float(dur[rec['kind'] == k].sum() / 100 / max(tot, 1)), 3)
                                               for k in range(4)})
+# concurrency over the launch: streams in flight per 0.5 ms bin (100 MHz realtime), and when the
+# last stream of each kind started / ended
+end = start + dur
+span = int(end.max())
+pts = np.arange(25000, span, 50000)
+act = [int(((start <= t) & (end > t)).sum()) for t in pts]
+print("in flight at 0.25, 0.75, ... ms:", act)
+lz = rec["kind"] == 3
+print("LZ in flight:", [int(((start <= t) & (end > t) & lz).sum()) for t in pts])
+for q in (0.5, 0.9, 0.99):
+    print(f"  LZ stream duration p{int(q * 100)}: {np.quantile(dur[lz], q) / 100:.0f} us")
+for k in range(4):
+    m = rec["kind"] == k
+    if m.any():
+        print(f"  {kinds[k]}: last start {start[m].max() / 100:.0f} us, last end {end[m].max() / 100:.0f} us")
