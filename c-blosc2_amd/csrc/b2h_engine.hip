@@ -1814,6 +1814,44 @@ __device__ __forceinline__ bool fuse_verdict(const EncFuse& f, const CGeom& g, b
   return f.ds ? g.spb == f.ds : (g.spb == 4 && (g.bs & 255) == 0);
 }
 
+// The (DELTA, SHUFFLE) filter jobs of a fused fast launch, run ahead of it by a launch of their own
+// (B2H_DS_PREPASS=1, off by default): one 256-thread workgroup per block, many per CU, instead of
+// one wave pair each inside the encoder launch.  There a pair holds ~465 us per 512 KiB block and
+// C4's encoder launch keeps only ~600 of its 2 048 pair slots on streams
+// (profiles/r6_streams_C4_fast.log) -- but the separate pass costs about what exact mode's
+// k_ffilter_ds does, and C4 compress went 7.2 -> 8.8 ms (profiles/r6_ab_ds_prepass.txt): the
+// in-launch jobs overlap the encoding.  Each block's ready word is published exactly as the
+// in-launch job does (1 | runs << 1, the verdict bit with it), and the claim counter is left at
+// the block count, so the encoder launch claims no job and finds every block ready.
+__global__ __launch_bounds__(256) void k_ds_prepass(EncFuse f, CGeom g, int32_t nblk) {
+  __shared__ uint32_t red_s;
+  B2H_LDS uint32_t* red = (B2H_LDS uint32_t*)&red_s;
+  for (int32_t k = blockIdx.x; k < nblk; k += gridDim.x) {
+    const int32_t cc = k / g.nblocks, b = k - cc * g.nblocks;
+    const bool lo = b == g.nblocks - 1 && g.leftover;
+    const int32_t bsize = lo ? g.leftover : g.bs;
+    const uint8_t* chunk = f.raw + (int64_t)cc * f.raw_stride;
+    uint8_t* fd = f.filt + (int64_t)cc * g.wstride + (int64_t)b * g.bs;
+    uint32_t runs = 0;
+    if (fuse_verdict(f, g, lo)) {
+      const uint8_t* src = chunk + (int64_t)b * g.bs;
+      if (f.ds == 8) runs = ds_block_runs<8>(src, chunk, fd, bsize / 8, b == 0, threadIdx.x, blockDim.x, red);
+      else if (f.ds == 4) runs = ds_block_runs<4>(src, chunk, fd, bsize / 4, b == 0, threadIdx.x, blockDim.x, red);
+      else runs = ds_block_runs<2>(src, chunk, fd, bsize / 2, b == 0, threadIdx.x, blockDim.x, red);
+      runs |= 1u << 29;
+    } else {
+      fuse_ds_block(chunk, fd, f.ds, b, bsize, g.bs, threadIdx.x, blockDim.x);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) f.sync[kFuseHdr + k] = (int32_t)(1u | (runs << 1));
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) f.sync[0] = nblk;   // every job claimed
+}
+static bool ds_prepass() {   // read per call (tests switch it)
+  const char* e = getenv("B2H_DS_PREPASS");
+  return e && atoi(e) != 0;
+}
+
 #undef FUSE_TRACE_PTR
 #define FUSE_TRACE_PTR lds_uniform(&A->f.trace)
 #ifndef B2H_FAST_WPE
@@ -2182,6 +2220,11 @@ static int launch_encode_fast_fused_t(Workspace* ws, const CGeom& g0, const uint
   const uint32_t grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(ntot, fuse_grid_cap(slots)));
   if (fuse_prepare(ws, g, ntot, f, st)) return E_MEMORY;
   if (chain_prepare<POS>(ws, g, grid)) return E_MEMORY;
+  if (f.raw && f.ds && ds_prepass()) {   // the (DELTA, SHUFFLE) jobs first, bandwidth-parallel
+    const int32_t nblk = f.nchunks * g.nblocks;
+    k_ds_prepass<<<(uint32_t)std::min<int32_t>(nblk, 8192), 256, 0, st>>>(f, g, nblk);
+    HIPCHK(hipGetLastError());
+  }
   static int32_t* trace = nullptr;
   static const bool tr = getenv("B2H_FUSE_TRACE") != nullptr;
   if (tr && !trace) HIPCHK(hipHostMalloc(&trace, 4 << 20, hipHostMallocCoherent));
