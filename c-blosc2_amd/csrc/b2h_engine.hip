@@ -1510,6 +1510,19 @@ struct EncFuse {
   int32_t mode_bits;       // fuse_bits()
   int32_t ds;              // raw's filter job: 0 the typesize-4 SHUFFLE, 2/4/8 (DELTA, SHUFFLE) at that typesize
 };
+// B2H_SEG_PROF (diagnostics build): the fused fast launch's per-phase clock, thread 0 of each
+// workgroup into g_seg_prof[16..25] (b2h_debug_seg_prof): 16 filter-job cycles, 17 ready-word
+// waits, 18 stream encodes, 19 job store drains, 20 jobs, 21 streams encoded, 22 / 23 the DS job's
+// verdict / store pass, 24 scatter items
+#ifdef B2H_SEG_PROF
+#define FPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define FPROF_ADD(i, a, b) do { if (threadIdx.x == 0) atomicAdd(&g_seg_prof[(i)], (unsigned long long)((b) - (a))); } while (0)
+#define FPROF_CNT(i) do { if (threadIdx.x == 0) atomicAdd(&g_seg_prof[(i)], 1ull); } while (0)
+#else
+#define FPROF_T(v)
+#define FPROF_ADD(i, a, b)
+#define FPROF_CNT(i)
+#endif
 constexpr int32_t kFuseHdr = 16;   // [0] shuffle claims [1] scatter claims [2] ready slots [3] published items [4] timeouts
 constexpr int32_t kFuseSpi = 8;    // streams per scatter item
 
@@ -1733,6 +1746,7 @@ __device__ uint32_t ds_block_runs(const uint8_t* __restrict__ src, const uint8_t
   };
   if (tid == 0) *red = 0u;
   __syncthreads();
+  FPROF_T(pv0);
   uint32_t mis = 0;
   for (int32_t q = tid; q < quads; q += nth) {
     uint32_t o[TS];
@@ -1747,6 +1761,8 @@ __device__ uint32_t ds_block_runs(const uint8_t* __restrict__ src, const uint8_t
   __syncthreads();
   const uint32_t M = __builtin_amdgcn_readfirstlane(*red);
   __syncthreads();
+  FPROF_T(pv1);
+  FPROF_ADD(22, pv0, pv1);
   if (M) {
     const __amdgpu_buffer_rsrc_t r = wt_rsrc((gout_t)dst);
     for (int32_t q = tid; q < quads; q += nth) {
@@ -1757,6 +1773,8 @@ __device__ uint32_t ds_block_runs(const uint8_t* __restrict__ src, const uint8_t
         if ((M >> plane) & 1u) __builtin_amdgcn_raw_buffer_store_b32(o[plane], r, plane * n + 4 * q, 0, 16);
     }
   }
+  FPROF_T(pv2);
+  FPROF_ADD(23, pv1, pv2);
   return ~M & ((1u << TS) - 1u);
 }
 __device__ __noinline__ uint32_t fuse_ds_block_runs(const uint8_t* chunk, uint8_t* d, int32_t ts, int32_t b, int32_t bsize,
@@ -2001,6 +2019,7 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
           // a split (DELTA, SHUFFLE) block of a chunk with run streams (extended header): the run
           // verdict comes with the filter job, published with the block (ready word 1 | runs << 1)
           uint32_t runs = 0;
+          FPROF_T(ja);
           if (fuse_verdict(fk, gk, lo)) {
             uint8_t* fd = fk.filt + (int64_t)cc * gk.wstride + (int64_t)b * gk.bs;
             runs = fk.ds ? fuse_ds_block_runs(fk.raw + (int64_t)cc * fk.raw_stride, fd, fk.ds, b, bsize, gk.bs, &sh->runred)
@@ -2010,8 +2029,13 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
           } else {
             fuse_filter_block(fk, gk, cc, b, bsize, threadIdx.x, blockDim.x);
           }
+          FPROF_T(jd);
           drain_stores();
           __syncthreads();
+          FPROF_T(jb);
+          FPROF_ADD(16, ja, jb);
+          FPROF_ADD(19, jd, jb);
+          FPROF_CNT(20);
           int32_t nk = -1;
           if (threadIdx.x == 0) {
             st_agent(fk.sync + kFuseHdr + k, (int32_t)(1u | (runs << 1)));
@@ -2021,6 +2045,7 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
         }
         FUSE_TRACE(5, gb);
         int32_t rv = 0;
+        FPROF_T(wa);
         if (threadIdx.x == 0) {
           int32_t* sync = lds_uniform(&A->f.sync);
           rv = wait_nonzero(sync + kFuseHdr + gb, sync + 4);
@@ -2028,6 +2053,8 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
           drain_stores();
         }
         rv = bcast(rv);
+        FPROF_T(wb);
+        FPROF_ADD(17, wa, wb);
         // the stream's plane was found a run by the filter job: its byte is plane j's of the
         // block's first element after DELTA, and nothing was stored for it
         const int32_t j = l - blk * g.spb;
@@ -2061,8 +2088,10 @@ void k_encode_fast_fused(CGeom g_arg, const uint8_t* __restrict__ filt_arg, uint
       r.kind = run_byte ? kStreamByteRun : kStreamZeroRun;
     } else {
       r = encode_stream_fast<POS, true, DEEP>(in, len, clevel, out, tab, tablog, oring, sh, runs, matcher, chain);
+      FPROF_CNT(21);
     }
     r.cycles = (int64_t)(__builtin_amdgcn_s_memtime() - t0);
+    FPROF_ADD(18, t0, (uint64_t)__builtin_amdgcn_s_memtime());
     r.t_start = (int64_t)((rt0 << 24) | ((__builtin_amdgcn_s_memrealtime() - rt0) & 0xffffff));
     if (!matcher && lane_id() == 0) {
       int32_t* fin = lds_uniform(&A->f.fin);
