@@ -8,6 +8,7 @@
 #   rp_fast|rp_exact rocprofv3 --kernel-trace --stats of bench.py in that mode
 #   pmc_fast|pmc_exact  FETCH_SIZE / WRITE_SIZE passes of bench.py, summarised by pmc_traffic.py
 #   stall_fast|stall_exact  SQ stall / issue / LDS-conflict passes over tests/prof_encode.py (T)
+#   stall_c4         the same counters over C4's fused fast encoder launch
 #   rp_c4|rp_c3|rp_c1  rocprofv3 kernel stats of tools/bench_configs.py for that config (fast mode)
 #   pmc_c4           FETCH_SIZE / WRITE_SIZE over C4 (fast mode)
 #   rpc_<cN>_<mode>  rocprof kernel stats of config cN in that mode (e.g. rpc_c3_exact)
@@ -60,6 +61,12 @@ for job in "$@"; do
       P="python3 $R/tests/prof_encode.py 1024 $m"
       timeout -s KILL 150 rocprofv3 --pmc $SQA --kernel-include-regex "k_encode" --output-format csv -d $O/${TAG}_${job}_a -o run -- $P > "$L" 2>&1 || fail "$job a" $L
       timeout -s KILL 150 rocprofv3 --pmc $SQB --kernel-include-regex "k_encode" --output-format csv -d $O/${TAG}_${job}_b -o run -- $P >> "$L" 2>&1 || fail "$job b" $L
+      echo "stall counters: gpurun_out/${TAG}_${job}_{a,b}" ;;
+    stall_c4)   # SQ stall / issue / LDS counters of C4's fused fast encoder launch
+      cd /tmp
+      P="python3 -u $R/tools/bench_configs.py --only C4 --lz-mode fast --steps 1"
+      timeout -s KILL 200 rocprofv3 --pmc $SQA --kernel-include-regex "k_encode" --output-format csv -d $O/${TAG}_${job}_a -o run -- $P > "$L" 2>&1 || fail "$job a" $L
+      timeout -s KILL 200 rocprofv3 --pmc $SQB --kernel-include-regex "k_encode" --output-format csv -d $O/${TAG}_${job}_b -o run -- $P >> "$L" 2>&1 || fail "$job b" $L
       echo "stall counters: gpurun_out/${TAG}_${job}_{a,b}" ;;
     rp_c4|rp_c3|rp_c1)
       c=${job#rp_}; C=${c^^}; cd /tmp
