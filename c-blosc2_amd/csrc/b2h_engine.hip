@@ -4327,13 +4327,15 @@ __global__ void k_dstatus(const DChunk* __restrict__ ch, int32_t* __restrict__ s
   status[c] = (d.status >= 0 && d.errkey != kNoErr) ? -(int32_t)(d.errkey & 0xff) : d.status;
 }
 
-static int dec_ring_log() {
-  static int v = 0;
-  if (!v) {
-    const char* e = getenv("B2H_DEC_RING");
-    v = e ? std::max(12, std::min(15, atoi(e))) : 13;
-  }
-  return v;
+// B2H_DEC_RING (read per call) forces the ring; unset: 8 KiB (20 waves per CU, T's best), or
+// 32 KiB when every stream of the batch fits the 32 KiB shape's resident waves at once (a
+// per-call chunk: then occupancy buys nothing, and the larger ring keeps far sources in LDS,
+// allows 8 KiB batches and lifts the 96-VGPR cap).
+static int dec_ring_log(int64_t nstreams) {
+  const char* e = getenv("B2H_DEC_RING");
+  if (e) return std::max(12, std::min(15, atoi(e)));
+  static const int slots15 = resident_slots(reinterpret_cast<const void*>(&k_decode<15>), size_t(1) << 15);
+  return nstreams <= slots15 ? 15 : 13;
 }
 
 template <int RLOG>
@@ -4419,7 +4421,7 @@ static int decompress_locked(Workspace* ws, const uint8_t* const* d_src, const i
         if (ws->ddbg.ensure(sizeof(int64_t) * 2 * (size_t)h.nstreams)) return E_MEMORY;
         dbg = ws->ddbg.as<int64_t>();
       }
-      const int rlog = dec_ring_log();
+      const int rlog = dec_ring_log(h.nstreams);
       uint8_t* stage = ws->stage.as<uint8_t>();
       if (rlog == 12) launch_decode<12>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, order, bcnt, dbg, st);
       else if (rlog == 13) launch_decode<13>(d_src, d_dst, ch, streams, stage, tot, h.nstreams, d_maskout, mask_stride, next, order, bcnt, dbg, st);

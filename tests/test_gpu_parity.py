@@ -551,3 +551,28 @@ def test_exact_encoder_shapes_same_bytes(B, shape):
         assert n == want.nbytes and np.array_equal(dst[:n], want)
     finally:
         L.b2h_set_encode_shape(-1, -1)
+
+
+@pytest.mark.parametrize("rlog", [None, "12", "13", "14", "15"])
+def test_decoder_ring_sizes_same_output(B, rlog, monkeypatch):
+    """The decoder's LDS ring (B2H_DEC_RING; unset: 32 KiB for batches whose streams all fit its
+    resident waves, else 8 KiB) never changes the output: exact-mode chunks of T's shape and of
+    C1's b2bench data (long far matches), decoded at every ring size, equal the input."""
+    import torch
+    from datagen import b2bench_values
+    if rlog is None:
+        monkeypatch.delenv("B2H_DEC_RING", raising=False)
+    else:
+        monkeypatch.setenv("B2H_DEC_RING", rlog)
+    L = B.lib()
+    L.b2h_set_blosclz_mode(0)
+    for name, host, kw in [("f32", gen_f32(5, 3 * (1 << 20) // 4), dict(clevel=5, typesize=4, filters=(0, 0, 0, 0, 0, 1))),
+                           ("b2bench", b2bench_values(1_000_000, 19), dict(clevel=5, typesize=4, filters=(0, 0, 0, 0, 0, 1)))]:
+        raw = host.view(np.uint8).reshape(-1)
+        chunk = oracle_compress(host, **kw)
+        assert isinstance(chunk, np.ndarray)
+        out = np.zeros(raw.nbytes, np.uint8)
+        dctx = L.blosc2_create_dctx(B.dparams())
+        n = L.blosc2_decompress_ctx(dctx, B._p(chunk), chunk.nbytes, B._p(out), out.nbytes)
+        L.blosc2_free_ctx(dctx)
+        assert n == raw.nbytes and np.array_equal(out, raw), (name, rlog)
